@@ -1,0 +1,137 @@
+"""OvercookedBatch: B independent kitchens stepped by the HIP engine (torch ROCm buffers).
+
+This is the batched counterpart of ``OvercookedEnvironment.reset/step``
+(gym_cooking/envs/overcooked_environment.py:201-306).  All buffers are torch uint8/uint64
+tensors on one GPU in the structure-of-arrays layout of include/oc_engine.h; every call is
+enqueued on torch's current stream through the C-ABI (liboc_engine.so).  There is no CPU
+fallback: without the built library or a GPU the constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import torch
+
+from . import capi
+from . import levels as _levels
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class OvercookedBatch:
+    """B envs of one level on one GPU.
+
+    Args:
+        level: builtin level name, level-file path, or :class:`levels.Level`.
+        num_agents: A (1..4).
+        B: batch size (envs on this device).
+        max_T: ``--max-num-timesteps`` (main.py:24; 0 = unlimited).
+        device: torch device (``cuda:N``).
+    """
+
+    def __init__(self, level, num_agents: int, B: int, max_T: int = 100, device="cuda:0"):
+        if isinstance(level, str):
+            level = _levels.load_level(level)
+        self.level = level
+        self.A = num_agents
+        self.B = int(B)
+        self.max_T = max_T
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("OvercookedBatch runs on the GPU only (no CPU fallback)")
+        self.lib = capi.load_library()
+        self._desc = capi.level_desc(level, num_agents)
+        h = ctypes.c_void_p()
+        capi.check(self.lib.oc_create(ctypes.byref(self._desc), num_agents, max_T,
+                                      self.device.index or 0, ctypes.byref(h)))
+        self._h = h
+        lay = capi.OcLayout()
+        capi.check(self.lib.oc_get_layout(self._h, self.B, ctypes.byref(lay)))
+        self.layout = lay
+        self.K = lay.num_items
+        self.pitch = lay.pitch
+        n = ctypes.c_int64()
+        capi.check(self.lib.oc_stats_size(self._h, self.B, ctypes.byref(n)))
+        self.stats_bytes = n.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and getattr(self, "lib", None) is not None:
+            self.lib.oc_destroy(h)
+            self._h = None
+
+    # ---- buffers ---------------------------------------------------------------------
+    def new_state(self) -> torch.Tensor:
+        return torch.empty(self.layout.state_bytes, dtype=torch.uint8, device=self.device)
+
+    def new_actions(self, steps: int = 1) -> torch.Tensor:
+        return torch.full((steps, self.A * self.pitch), 4, dtype=torch.uint8, device=self.device).squeeze(0)
+
+    def new_exec(self) -> torch.Tensor:
+        return torch.empty(self.A * self.pitch, dtype=torch.uint8, device=self.device)
+
+    def new_coll(self) -> torch.Tensor:
+        return torch.empty(self.pitch, dtype=torch.uint8, device=self.device)
+
+    def new_stats(self) -> torch.Tensor:
+        return torch.zeros(self.stats_bytes // 8, dtype=torch.uint64, device=self.device)
+
+    def planes(self, state: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """Named views of a state buffer ([A|K, pitch] u8 planes; t is [pitch] u16)."""
+        L, P, A, K = self.layout, self.pitch, self.A, self.K
+        s = state.view(L.num_planes, P)
+        return dict(
+            agent_x=s[L.plane_agent_x:L.plane_agent_x + A], agent_y=s[L.plane_agent_y:L.plane_agent_y + A],
+            agent_hold=s[L.plane_agent_hold:L.plane_agent_hold + A],
+            item_loc=s[L.plane_item_loc:L.plane_item_loc + K], item_mask=s[L.plane_item_mask:L.plane_item_mask + K],
+            t=s[L.plane_t:L.plane_t + 2].reshape(-1).view(torch.int16)[:P], flags=s[L.plane_flags],
+        )
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ---- hot path ----------------------------------------------------------------------
+    def reset(self, state: torch.Tensor) -> torch.Tensor:
+        """Broadcast the level template (reset(), overcooked_environment.py:201-250)."""
+        self._check(state, self.layout.state_bytes)
+        capi.check(self.lib.oc_reset(self._h, _ptr(state), self.B, self._stream()))
+        return state
+
+    def step(self, state_in: torch.Tensor, state_out: torch.Tensor, actions: torch.Tensor,
+             exec_out: Optional[torch.Tensor] = None, coll: Optional[torch.Tensor] = None,
+             stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One step of every env (step(), overcooked_environment.py:255-306)."""
+        self._check(state_in, self.layout.state_bytes)
+        self._check(state_out, self.layout.state_bytes)
+        self._check(actions, self.A * self.pitch)
+        if exec_out is not None:
+            self._check(exec_out, self.A * self.pitch)
+        if coll is not None:
+            self._check(coll, self.pitch)
+        if stats is not None:
+            self._check(stats, self.stats_bytes)
+        capi.check(self.lib.oc_step(self._h, _ptr(state_in), _ptr(state_out), _ptr(actions), _ptr(exec_out),
+                                    _ptr(coll), _ptr(stats), self.B, self._stream()))
+        return state_out
+
+    def gen_actions(self, actions: torch.Tensor, step: int, seed: int = 0, env_offset: int = 0) -> torch.Tensor:
+        self._check(actions, self.A * self.pitch)
+        capi.check(self.lib.oc_gen_actions(self._h, _ptr(actions), self.B, env_offset, step, seed, self._stream()))
+        return actions
+
+    def reduce_stats(self, stats: torch.Tensor) -> torch.Tensor:
+        """[OC_NSTATS] uint64 device totals of a partial-stats buffer."""
+        out = torch.empty(capi.OC_NSTATS, dtype=torch.uint64, device=self.device)
+        capi.check(self.lib.oc_stats_reduce(self._h, _ptr(stats), self.B, _ptr(out), self._stream()))
+        return out
+
+    def _check(self, t: torch.Tensor, nbytes: int) -> None:
+        if t.device != self.device or not t.is_contiguous():
+            raise ValueError("buffer must be contiguous on %s" % self.device)
+        if t.numel() * t.element_size() < nbytes:
+            raise ValueError("buffer too small: %d < %d bytes" % (t.numel() * t.element_size(), nbytes))
+        if t.data_ptr() % 16:
+            raise ValueError("buffer must be 16-byte aligned")

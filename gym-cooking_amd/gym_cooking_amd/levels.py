@@ -1,0 +1,257 @@
+"""Kitchen levels for the batched Overcooked step engine (host side).
+
+This module turns a kitchen level into the static tables the engine needs:
+a tile-class grid, the initial item slots, the agent spawns and the recipe
+goal masks.  It restates the parsing rules of the reference loader
+``OvercookedEnvironment.load_level`` (gym_cooking/envs/overcooked_environment.py:130-198):
+
+* map characters go through ``RepToClass`` (gym_cooking/utils/core.py:372-381):
+  ``' '`` Floor, ``-`` Counter, ``/`` Cutboard, ``*`` Delivery, ``t l o p`` a Counter
+  holding a fresh Tomato / Lettuce / Onion / a Plate (overcooked_environment.py:158-165);
+  any other character becomes Floor (overcooked_environment.py:170-173);
+* only Floor is non-collidable (core.py:34, 64);
+* width is the last map row's length, height the number of map rows
+  (overcooked_environment.py:196-197);
+* agents ``agent-1..A`` take the first A spawn lines (overcooked_environment.py:186-193);
+* recipe lines name recipe classes (recipe_planner/recipe.py:199-228); each recipe
+  contributes one ``Deliver(full_plate_name)`` subtask (recipe.py:39-47) whose goal
+  object has every food in its last state (navigation_planner/utils.py:231-238).
+
+Item contents are encoded as a 7-bit mask: bit0 Tomato,
+bit1 Lettuce, bit2 Onion, bit3 Plate, bit4/5/6 Tomato/Lettuce/Onion chopped.  The
+mask is exact because a level may hold at most one of each food type (validated).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from typing import Dict, List, Sequence, Tuple
+
+TILE_FLOOR = 0
+TILE_COUNTER = 1
+TILE_CUTBOARD = 2
+TILE_DELIVERY = 3
+
+M_TOMATO = 0x01
+M_LETTUCE = 0x02
+M_ONION = 0x04
+M_PLATE = 0x08
+M_TOMATO_CHOPPED = 0x10
+M_LETTUCE_CHOPPED = 0x20
+M_ONION_CHOPPED = 0x40
+M_FOODS = M_TOMATO | M_LETTUCE | M_ONION
+
+# Engine limits (include/oc_engine.h).
+MAX_AGENTS = 4
+MAX_ITEMS = 8
+MAX_CELLS = 64
+MAX_GOALS = 4
+LOC_DEAD = 0xFF
+HOLD_NONE = 0xFF
+
+# Action codes: World.NAV_ACTIONS order (gym_cooking/utils/world.py:16) + no-op.
+ACTIONS: Tuple[Tuple[int, int], ...] = ((0, 1), (0, -1), (-1, 0), (1, 0), (0, 0))
+NOOP = 4
+ACTION_CODE = {a: i for i, a in enumerate(ACTIONS)}
+
+_CHAR_TILE = {" ": TILE_FLOOR, "-": TILE_COUNTER, "/": TILE_CUTBOARD, "*": TILE_DELIVERY}
+_CHAR_ITEM = {"t": M_TOMATO, "l": M_LETTUCE, "o": M_ONION, "p": M_PLATE}
+_FOOD_NAMES = (("Tomato", M_TOMATO), ("Lettuce", M_LETTUCE), ("Onion", M_ONION))
+
+
+def chopped(mask_bit: int) -> int:
+    """Chopped-state bit of a food presence bit."""
+    return mask_bit << 4
+
+
+# Recipe -> Deliver goal mask (recipe.py:199-228; foods in last state, plated).
+RECIPE_GOALS: Dict[str, int] = {
+    "SimpleTomato": M_PLATE | M_TOMATO | chopped(M_TOMATO),
+    "SimpleLettuce": M_PLATE | M_LETTUCE | chopped(M_LETTUCE),
+    "Salad": M_PLATE | M_TOMATO | M_LETTUCE | chopped(M_TOMATO) | chopped(M_LETTUCE),
+    "OnionSalad": (M_PLATE | M_TOMATO | M_LETTUCE | M_ONION
+                   | chopped(M_TOMATO) | chopped(M_LETTUCE) | chopped(M_ONION)),
+}
+
+
+def mask_full_name(mask: int) -> str:
+    """Reference ``Object.full_name`` of an item mask (core.py:161-171): contents sorted by
+    base name, foods prefixed by their state, joined by '-'."""
+    parts = []
+    for name, bit in _FOOD_NAMES:
+        if mask & bit:
+            parts.append((name, ("Chopped" if mask & chopped(bit) else "Fresh") + name))
+    if mask & M_PLATE:
+        parts.append(("Plate", "Plate"))
+    parts.sort()
+    return "-".join(p[1] for p in parts)
+
+
+def full_name_mask(full_name: str) -> int:
+    """Inverse of :func:`mask_full_name`."""
+    mask = 0
+    for part in full_name.split("-"):
+        if part == "Plate":
+            mask |= M_PLATE
+            continue
+        for name, bit in _FOOD_NAMES:
+            if part == "Fresh" + name:
+                mask |= bit
+                break
+            if part == "Chopped" + name:
+                mask |= bit | chopped(bit)
+                break
+        else:
+            raise ValueError("unknown content %r" % part)
+    return mask
+
+
+@dataclasses.dataclass
+class Level:
+    """Static description of one kitchen (what ``load_level`` builds)."""
+
+    name: str
+    width: int
+    height: int
+    tiles: List[int]                      # row-major, cell = y * width + x
+    items: List[Tuple[int, int]]          # (cell, mask) in map scan order
+    spawns: List[Tuple[int, int]]         # (x, y) spawn lines
+    recipes: List[str]
+
+    @property
+    def ncells(self) -> int:
+        return self.width * self.height
+
+    @property
+    def goals(self) -> List[int]:
+        """Unique Deliver goal masks, in recipe order."""
+        out: List[int] = []
+        for r in self.recipes:
+            g = RECIPE_GOALS[r]
+            if g not in out:
+                out.append(g)
+        return out
+
+    @property
+    def delivery_cell(self) -> int:
+        """First Delivery in scan order: ``done()`` reads only that one
+        (overcooked_environment.py:349)."""
+        for c, t in enumerate(self.tiles):
+            if t == TILE_DELIVERY:
+                return c
+        raise ValueError("level %s has no Delivery" % self.name)
+
+    def tile_at(self, x: int, y: int) -> int:
+        return self.tiles[y * self.width + x]
+
+    def cell(self, x: int, y: int) -> int:
+        return y * self.width + x
+
+    def xy(self, cell: int) -> Tuple[int, int]:
+        return cell % self.width, cell // self.width
+
+    def validate(self, num_agents: int) -> None:
+        """Reject levels outside the engine's exact-semantics envelope (raises ValueError)."""
+        if not 1 <= num_agents <= MAX_AGENTS:
+            raise ValueError("num_agents must be in 1..%d" % MAX_AGENTS)
+        if len(self.spawns) < num_agents:
+            raise ValueError("level %s has %d spawns < %d agents" % (self.name, len(self.spawns), num_agents))
+        if self.ncells > MAX_CELLS:
+            raise ValueError("level %s has %d cells > %d" % (self.name, self.ncells, MAX_CELLS))
+        if len(self.items) > MAX_ITEMS:
+            raise ValueError("level %s has %d items > %d" % (self.name, len(self.items), MAX_ITEMS))
+        for bit in (M_TOMATO, M_LETTUCE, M_ONION):
+            if sum(1 for _, m in self.items if m & bit) > 1:
+                raise ValueError("level %s holds a food type twice; masks would be ambiguous" % self.name)
+        if not self.recipes:
+            raise ValueError("level %s has no recipe (done() asserts a Deliver subtask)" % self.name)
+        if len(self.goals) > MAX_GOALS:
+            raise ValueError("too many goals")
+        self.delivery_cell  # noqa: B018 -- raises if absent
+        # is_collision indexes loc+action without clamping (overcooked_environment.py:692-700):
+        # a Floor on the border would let an agent look outside the grid, where the
+        # reference raises.  Every reference level has a non-Floor border.
+        W, H = self.width, self.height
+        for x in range(W):
+            for y in (0, H - 1):
+                if self.tile_at(x, y) == TILE_FLOOR:
+                    raise ValueError("level %s: Floor on border at (%d,%d)" % (self.name, x, y))
+        for y in range(H):
+            for x in (0, W - 1):
+                if self.tile_at(x, y) == TILE_FLOOR:
+                    raise ValueError("level %s: Floor on border at (%d,%d)" % (self.name, x, y))
+        for (x, y) in self.spawns[:num_agents]:
+            if not (0 <= x < W and 0 <= y < H) or self.tile_at(x, y) != TILE_FLOOR:
+                raise ValueError("level %s: spawn (%d,%d) is not a Floor" % (self.name, x, y))
+
+
+def parse_level_text(text: str, name: str = "custom") -> Level:
+    """Parse the reference's level file format (overcooked_environment.py:144-193):
+    map rows, blank line, recipe class names, blank line, ``x y`` spawn lines."""
+    phase = 1
+    rows: List[str] = []
+    recipes: List[str] = []
+    spawns: List[Tuple[int, int]] = []
+    for line in text.split("\n"):
+        line = line.rstrip("\r")
+        if line == "":
+            phase += 1
+        elif phase == 1:
+            rows.append(line)
+        elif phase == 2:
+            if line not in RECIPE_GOALS:
+                raise ValueError("unknown recipe %r" % line)
+            recipes.append(line)
+        elif phase == 3:
+            xs = line.split(" ")
+            spawns.append((int(xs[0]), int(xs[1])))
+    if not rows:
+        raise ValueError("empty map")
+    width = len(rows[-1])
+    if any(len(r) != width for r in rows):
+        raise ValueError("ragged map rows are not supported")
+    tiles: List[int] = []
+    items: List[Tuple[int, int]] = []
+    for y, row in enumerate(rows):
+        for x, ch in enumerate(row):
+            if ch in _CHAR_ITEM:
+                tiles.append(TILE_COUNTER)
+                items.append((y * width + x, _CHAR_ITEM[ch]))
+            else:
+                tiles.append(_CHAR_TILE.get(ch, TILE_FLOOR))
+    return Level(name=name, width=width, height=len(rows), tiles=tiles, items=items,
+                 spawns=spawns, recipes=recipes)
+
+
+def _builtin(divider: str, recipes: Sequence[str], name: str) -> Level:
+    """The nine shipped kitchens share one 7x7 frame: tomato (5,0), lettuce (6,1),
+    plates (6,5) and (5,6), delivery (0,3), cutboards (0,1) and (0,2); they differ
+    only in the x=3 divider (open: none, partial: y=1..4, full: y=1..5) and the recipes."""
+    div_rows = {"open": (), "partial": (1, 2, 3, 4), "full": (1, 2, 3, 4, 5)}[divider]
+    left = {1: "/", 2: "/", 3: "*", 4: "-", 5: "-"}
+    right = {1: "l", 2: "-", 3: "-", 4: "-", 5: "p"}
+    rows = ["-----t-"]
+    for y in range(1, 6):
+        mid = "  " + ("-" if y in div_rows else " ") + "  "
+        rows.append(left[y] + mid + right[y])
+    rows.append("-----p-")
+    text = "\n".join(rows) + "\n\n" + "\n".join(recipes) + "\n\n" + "2 1\n4 1\n4 4\n2 4\n"
+    return parse_level_text(text, name)
+
+
+_RECIPE_SETS = {"salad": ("Salad",), "tomato": ("SimpleTomato",), "tl": ("SimpleTomato", "SimpleLettuce")}
+
+BUILTIN_LEVELS: Dict[str, Level] = {
+    "%s-divider_%s" % (d, r): _builtin(d, rs, "%s-divider_%s" % (d, r))
+    for d in ("open", "partial", "full") for r, rs in _RECIPE_SETS.items()
+}
+
+
+def load_level(name_or_path: str) -> Level:
+    """A builtin level by name, or a level file in the reference's text format."""
+    if name_or_path in BUILTIN_LEVELS:
+        return BUILTIN_LEVELS[name_or_path]
+    if os.path.isfile(name_or_path):
+        with open(name_or_path) as f:
+            return parse_level_text(f.read(), os.path.splitext(os.path.basename(name_or_path))[0])
+    raise KeyError("unknown level %r" % name_or_path)

@@ -1,0 +1,167 @@
+/*
+ * oc_engine.h -- C-ABI of the MI355X batched Overcooked step engine (liboc_engine.so).
+ *
+ * The reference (deletfsi/gym-cooking) is pure Python and has no FFI; each entry point
+ * below replaces one reference routine on the environment-step hot path and is what a
+ * ctypes/cffi binding of that routine binds (INTEGRATION.md shows the binding):
+ *
+ *   oc_create / oc_destroy   <- OvercookedEnvironment.load_level + run_recipes
+ *                               (gym_cooking/envs/overcooked_environment.py:130-198, :396-473)
+ *   oc_reset                 <- OvercookedEnvironment.reset      (overcooked_environment.py:201-250)
+ *   oc_step                  <- OvercookedEnvironment.step       (overcooked_environment.py:255-306)
+ *                               = check_collisions (:724-762) + execute_navigation/interact
+ *                               (:767-770, gym_cooking/utils/interact.py:4-89) + done/reward (:316-376)
+ *   oc_gen_actions           <- synthetic action streams (the reference env has no RNG)
+ *   oc_stats_*               <- the per-episode bookkeeping main.py keeps in its metrics Bag
+ *                               (gym_cooking/misc/metrics/metrics_bag.py:40-72), reduced per GPU
+ *
+ * Conventions
+ *  - All entry points return 0 on success and a negative OC_E* code on failure; the message
+ *    of the last failure on the calling thread is available from oc_last_error().
+ *  - Every buffer is caller-owned device memory (e.g. torch ROCm tensors); the engine never
+ *    allocates in oc_step / oc_reset / oc_gen_actions, so they are hipGraph-capturable.
+ *  - `stream` is a hipStream_t passed as void* (NULL = the null stream).  Calls are
+ *    stream-ordered and not synchronised; a handle is not thread-safe.
+ *  - State is structure-of-arrays: `num_planes` byte planes of `pitch` bytes each (see
+ *    oc_layout).  Env e of plane p lives at byte p*pitch + e (the t plane holds u16 at
+ *    2*e and spans two planes).  pitch = B rounded up to OC_PITCH_ALIGN.
+ */
+#ifndef OC_ENGINE_H_
+#define OC_ENGINE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OC_ABI_VERSION 1
+
+#define OC_MAX_AGENTS 4
+#define OC_MAX_ITEMS 8
+#define OC_MAX_CELLS 64
+#define OC_MAX_GOALS 4
+#define OC_PITCH_ALIGN 4096
+
+/* status codes */
+#define OC_OK 0
+#define OC_EINVAL (-1)   /* bad argument / unsupported shape */
+#define OC_EHIP (-2)     /* HIP runtime error */
+#define OC_ELEVEL (-3)   /* level outside the exact-semantics envelope */
+
+/* tile classes (gym_cooking/utils/core.py:28-120; only Floor is non-collidable) */
+#define OC_TILE_FLOOR 0
+#define OC_TILE_COUNTER 1
+#define OC_TILE_CUTBOARD 2
+#define OC_TILE_DELIVERY 3
+
+/* item content mask bits: presence T,L,O,P + chopped T,L,O */
+#define OC_M_TOMATO 0x01u
+#define OC_M_LETTUCE 0x02u
+#define OC_M_ONION 0x04u
+#define OC_M_PLATE 0x08u
+#define OC_M_CHOPPED_SHIFT 4
+
+/* action codes: World.NAV_ACTIONS order (gym_cooking/utils/world.py:16) + no-op.
+ * Codes > 4 are treated as OC_ACT_NOOP. */
+#define OC_ACT_DOWN 0   /* ( 0, 1) */
+#define OC_ACT_UP 1     /* ( 0,-1) */
+#define OC_ACT_LEFT 2   /* (-1, 0) */
+#define OC_ACT_RIGHT 3  /* ( 1, 0) */
+#define OC_ACT_NOOP 4   /* ( 0, 0) */
+
+#define OC_HOLD_NONE 0xFFu
+#define OC_LOC_DEAD 0xFFu
+
+/* flags plane bits */
+#define OC_FLAG_DONE 0x01u    /* done() returned True (overcooked_environment.py:316-363) */
+#define OC_FLAG_SUCCESS 0x02u /* reward() == 1 (overcooked_environment.py:365-376) */
+#define OC_FLAG_ERR 0x04u     /* the reference raises at new_obs = copy.copy(self)
+                                 (overcooked_environment.py:289 -> :108-113 -> world.py:417):
+                                 two co-located agents both holding.  ERR implies DONE. */
+
+/* per-GPU episode statistics (oc_stats_reduce output, uint64 each) */
+#define OC_STAT_EPISODES 0   /* envs whose episode ended this window (DONE newly set) */
+#define OC_STAT_SUCCESSES 1  /* of those, reward 1 */
+#define OC_STAT_STEPS 2      /* sum of t over ended episodes (episode lengths) */
+#define OC_STAT_COLLISIONS 3 /* sum over steps of colliding agent pairs (CollisionRepr count) */
+#define OC_STAT_ERRORS 4     /* envs that hit the ERR condition */
+#define OC_NSTATS 5
+
+typedef struct oc_level_desc {
+    int32_t width, height;           /* width*height <= OC_MAX_CELLS; non-Floor border */
+    int32_t num_items;               /* <= OC_MAX_ITEMS, at most one of each food type */
+    int32_t num_spawns;              /* >= num_agents */
+    int32_t num_goals;               /* 1..OC_MAX_GOALS Deliver goal masks */
+    uint8_t tiles[OC_MAX_CELLS];     /* OC_TILE_* per cell, cell = y*width + x */
+    uint8_t item_cell[OC_MAX_ITEMS]; /* initial item cells, map scan order */
+    uint8_t item_mask[OC_MAX_ITEMS]; /* initial item content masks */
+    uint8_t spawn_x[OC_MAX_AGENTS];
+    uint8_t spawn_y[OC_MAX_AGENTS];
+    uint8_t goal_mask[OC_MAX_GOALS];
+} oc_level_desc;
+
+typedef struct oc_layout {
+    int64_t pitch;          /* bytes per byte-plane */
+    int64_t state_bytes;    /* num_planes * pitch */
+    int32_t num_agents;     /* A */
+    int32_t num_items;      /* K (item slots; >= level items, extra slots dead) */
+    int32_t plane_agent_x;  /* A planes, u8 */
+    int32_t plane_agent_y;  /* A planes, u8 */
+    int32_t plane_agent_hold; /* A planes, u8 item slot or OC_HOLD_NONE */
+    int32_t plane_item_loc; /* K planes, u8 cell or OC_LOC_DEAD */
+    int32_t plane_item_mask;/* K planes, u8 content mask */
+    int32_t plane_t;        /* u16 step counter, spans 2 planes */
+    int32_t plane_flags;    /* u8 OC_FLAG_* */
+    int32_t num_planes;     /* 3A + 2K + 3 */
+} oc_layout;
+
+typedef struct oc_handle oc_handle;
+
+/* Library identity. */
+int oc_abi_version(void);
+const char* oc_last_error(void);
+
+/* Static level tables + episode settings.  max_T = --max-num-timesteps (main.py:24; 0 = no
+ * limit).  device = HIP ordinal the handle's launches target (recorded, validated). */
+int oc_create(const oc_level_desc* level, int32_t num_agents, int32_t max_T, int32_t device,
+              oc_handle** out);
+int oc_destroy(oc_handle* h);
+
+/* Layout of a B-env batch for this handle. */
+int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out);
+
+/* Broadcast the level's initial state (reset(), overcooked_environment.py:201-250) to B envs. */
+int oc_reset(const oc_handle* h, void* state, int64_t B, void* stream);
+
+/* One env step for B envs (step(), overcooked_environment.py:255-306).
+ *   state_in/state_out : layout buffers (may alias: in-place is allowed)
+ *   actions            : u8 [A][pitch] action codes
+ *   exec_actions       : u8 [A][pitch] executed (post-collision) codes = env.agent_actions
+ *                        (overcooked_environment.py:770); nullable
+ *   coll_mask          : u8 [pitch] colliding pairs in itertools.combinations order
+ *                        (0,1),(0,2),(0,3),(1,2),(1,3),(2,3) (overcooked_environment.py:731-752); nullable
+ *   stats              : u64 partial-sum buffer of oc_stats_size() bytes (zeroed by the caller
+ *                        once per window); nullable
+ * An env whose input flags carry OC_FLAG_DONE is reset to the level template instead of
+ * stepped (next-step auto-reset; its exec actions read OC_ACT_NOOP, coll 0). */
+int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
+            uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, int64_t B, void* stream);
+
+/* Synthetic i.i.d. uniform action codes 0..4 for B envs at step `step`:
+ * code = splitmix64(seed ^ gid*0x9E3779B97F4A7C15 ^ step*0xC2B2AE3D27D4EB4F ^ agent) % 5,
+ * gid = env_offset + e (global env id: identical for any GPU count). */
+int oc_gen_actions(const oc_handle* h, uint8_t* actions, int64_t B, int64_t env_offset,
+                   int64_t step, uint64_t seed, void* stream);
+
+/* Statistics: size of the partial buffer for B envs, and its reduction into OC_NSTATS
+ * device uint64 totals. */
+int oc_stats_size(const oc_handle* h, int64_t B, int64_t* nbytes);
+int oc_stats_reduce(const oc_handle* h, const uint64_t* stats, int64_t B, uint64_t* totals,
+                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OC_ENGINE_H_ */

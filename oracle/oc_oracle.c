@@ -1,0 +1,513 @@
+/*
+ * oracle/oc_oracle.c -- TEST INFRASTRUCTURE, NOT PRODUCT CODE.
+ *
+ * A scalar CPU restatement of the reference environment step of deletfsi/gym-cooking
+ * (pure Python; nothing to compile), written object-by-object after the reference so that
+ * each routine can be read against the line it restates.  It is the parity checker for the
+ * HIP engine (tests/) and the CPU baseline leg of bench.py.  Only tests/, smoke() and
+ * bench.py's cpu_baseline may load it; the product path (liboc_engine.so) never does.
+ *
+ * Pinning: tests/test_oracle_golden.py replays every fixture under tests/golden/ (generated
+ * by importing the reference itself, tests/golden/gen_golden.py) and requires bit-exact
+ * agreement of the canonical state, executed actions, collision masks and flags.
+ *
+ * State layout = include/oc_engine.h oc_layout (byte planes, canonical App. A.11 fields).
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/oc_engine.h"
+
+#define NFOOD 3 /* Tomato, Lettuce, Onion */
+
+typedef struct { int x, y; } Loc;
+
+/* core.Object (gym_cooking/utils/core.py:130-219).  Contents: at most one of each food
+ * (level validation) with its FRESH_CHOPPED state index (core.py:250-252, 310-346), plus
+ * a plate count. */
+typedef struct {
+    int alive; /* present in World.objects */
+    Loc location;
+    int is_held;
+    int food_present[NFOOD];
+    int food_state[NFOOD]; /* 0 = Fresh, 1 = Chopped */
+    int plates;
+} Obj;
+
+/* utils.agent.SimAgent (gym_cooking/utils/agent.py:371-423) */
+typedef struct {
+    Loc location;
+    int holding; /* index into objs, -1 = None */
+    Loc action;
+} Agent;
+
+typedef struct {
+    const oc_level_desc* L;
+    int A, K;
+    int t;
+    Obj objs[OC_MAX_ITEMS];
+    Agent agents[OC_MAX_AGENTS];
+} Env;
+
+static const Loc NAV[5] = {{0, 1}, {0, -1}, {-1, 0}, {1, 0}, {0, 0}};
+
+static int loc_eq(Loc a, Loc b) { return a.x == b.x && a.y == b.y; }
+static Loc loc_add(Loc a, Loc b) { Loc r = {a.x + b.x, a.y + b.y}; return r; }
+
+static int action_code(Loc a) {
+    for (int i = 0; i < 5; ++i)
+        if (loc_eq(a, NAV[i])) return i;
+    abort();
+}
+
+/* World.get_gridsquare_at (world.py:421-430): the unique GridSquare at location. The
+ * reference asserts when there is none (off-grid); level validation excludes that. */
+static int gridsquare_at(const Env* e, Loc l) {
+    if (l.x < 0 || l.y < 0 || l.x >= e->L->width || l.y >= e->L->height) abort();
+    return e->L->tiles[l.y * e->L->width + l.x];
+}
+
+/* GridSquare.collidable: only Floor is walkable (core.py:34, 64) */
+static int collidable(int tile) { return tile != OC_TILE_FLOOR; }
+
+/* World.inbounds (world.py:432-436) */
+static Loc inbounds(const Env* e, Loc l) {
+    Loc r;
+    r.x = l.x < 0 ? 0 : (l.x > e->L->width - 1 ? e->L->width - 1 : l.x);
+    r.y = l.y < 0 ? 0 : (l.y > e->L->height - 1 ? e->L->height - 1 : l.y);
+    return r;
+}
+
+/* World.is_occupied (world.py:285-290): an un-held Object at location */
+static int is_occupied(const Env* e, Loc l) {
+    for (int i = 0; i < e->K; ++i)
+        if (e->objs[i].alive && loc_eq(e->objs[i].location, l) && !e->objs[i].is_held) return 1;
+    return 0;
+}
+
+/* World.get_object_at(location, None, find_held_objects) (world.py:389-419); returns -1
+ * where the reference's `assert len(objs) == 1` would fail. */
+static int object_at(const Env* e, Loc l, int find_held) {
+    int found = -1, n = 0;
+    for (int i = 0; i < e->K; ++i)
+        if (e->objs[i].alive && loc_eq(e->objs[i].location, l) && e->objs[i].is_held == find_held) {
+            found = i;
+            ++n;
+        }
+    return n == 1 ? found : -1;
+}
+
+static int n_contents(const Obj* o) {
+    int n = o->plates;
+    for (int f = 0; f < NFOOD; ++f) n += o->food_present[f];
+    return n;
+}
+
+/* Food.done (core.py:293-296): state index is the last of FRESH_CHOPPED */
+static int food_done(const Obj* o, int f) { return o->food_state[f] == 1; }
+
+/* Object.needs_chopped (core.py:176-178) -> Food.needs_chopped (core.py:285-291) /
+ * Plate.needs_chopped (core.py:365-366) */
+static int needs_chopped(const Obj* o) {
+    if (n_contents(o) > 1) return 0;
+    if (o->plates) return 0;
+    for (int f = 0; f < NFOOD; ++f)
+        if (o->food_present[f]) return o->food_state[f] == 0; /* next state is Chopped */
+    return 0;
+}
+
+/* Object.chop (core.py:187-192) */
+static void chop(Obj* o) {
+    for (int f = 0; f < NFOOD; ++f)
+        if (o->food_present[f]) o->food_state[f] += 1;
+}
+
+/* Object.is_deliverable (core.py:214-219) */
+static int is_deliverable(const Obj* o) {
+    for (int f = 0; f < NFOOD; ++f)
+        if (o->food_present[f] && !food_done(o, f)) return 0;
+    return n_contents(o) > 1; /* is_merged */
+}
+
+/* mergeable (core.py:222-241): drop up to one Plate; a second Plate => False; otherwise
+ * every remaining content must be in its last state. */
+static int mergeable(const Obj* a, const Obj* b) {
+    int plates = a->plates + b->plates;
+    if (plates >= 2) return 0;
+    for (int f = 0; f < NFOOD; ++f) {
+        if (a->food_present[f] && !food_done(a, f)) return 0;
+        if (b->food_present[f] && !food_done(b, f)) return 0;
+    }
+    return 1;
+}
+
+/* Object.merge (core.py:194-202): contents += other's contents */
+static void merge(Obj* a, const Obj* b) {
+    a->plates += b->plates;
+    for (int f = 0; f < NFOOD; ++f)
+        if (b->food_present[f]) {
+            if (a->food_present[f]) abort(); /* duplicate food: outside the level envelope */
+            a->food_present[f] = 1;
+            a->food_state[f] = b->food_state[f];
+        }
+}
+
+/* SimAgent.acquire (agent.py:408-414) */
+static void agent_acquire(Env* e, Agent* ag, int obj) {
+    if (ag->holding < 0) {
+        ag->holding = obj;
+        e->objs[obj].is_held = 1;
+        e->objs[obj].location = ag->location;
+    } else {
+        merge(&e->objs[ag->holding], &e->objs[obj]);
+    }
+}
+
+/* SimAgent.release (agent.py:416-418) */
+static void agent_release(Env* e, Agent* ag) {
+    e->objs[ag->holding].is_held = 0;
+    ag->holding = -1;
+}
+
+/* SimAgent.move_to (agent.py:420-423) */
+static void agent_move_to(Env* e, Agent* ag, Loc l) {
+    ag->location = l;
+    if (ag->holding >= 0) e->objs[ag->holding].location = l;
+}
+
+/* interact(agent, world) (utils/interact.py:4-89), world.arglist.play == False */
+static void interact(Env* e, Agent* ag) {
+    if (loc_eq(ag->action, NAV[OC_ACT_NOOP])) return;                /* :19-20 */
+    Loc target = inbounds(e, loc_add(ag->location, ag->action));     /* :22 */
+    int gs = gridsquare_at(e, target);                               /* :24 */
+    if (gs == OC_TILE_FLOOR) {                                       /* :28-30 */
+        agent_move_to(e, ag, target);
+    } else if (ag->holding >= 0) {                                   /* :33 */
+        if (gs == OC_TILE_DELIVERY) {                                /* :35-40 */
+            Obj* obj = &e->objs[ag->holding];
+            if (is_deliverable(obj)) {
+                obj->location = target; /* Delivery.acquire (core.py:110-112) */
+                agent_release(e, ag);
+            }
+        } else if (is_occupied(e, target)) {                         /* :43-56 */
+            int o = object_at(e, target, 0);
+            if (o < 0) abort();
+            if (mergeable(&e->objs[ag->holding], &e->objs[o])) {
+                e->objs[o].alive = 0;   /* world.remove(obj); gs.release() */
+                /* world.remove(agent.holding) + world.insert(agent.holding): the holder's
+                 * object survives under its new name (identity kept in its slot). */
+                agent_acquire(e, ag, o); /* holding.merge(obj) */
+            }
+        } else {                                                     /* :60-70 */
+            Obj* obj = &e->objs[ag->holding];
+            if (gs == OC_TILE_CUTBOARD && needs_chopped(obj)) {
+                chop(obj);
+            } else {
+                obj->location = target; /* gs.acquire(obj) (core.py:50-52) */
+                agent_release(e, ag);
+            }
+        }
+    } else {                                                         /* :73-89 */
+        if (is_occupied(e, target) && gs != OC_TILE_DELIVERY) {
+            int o = object_at(e, target, 0);
+            if (o < 0) abort();
+            agent_acquire(e, ag, o); /* gs.release(); agent.acquire(obj) */
+        }
+    }
+}
+
+/* OvercookedEnvironment.is_collision (overcooked_environment.py:671-718) */
+static void is_collision(const Env* e, Loc l1, Loc l2, Loc a1, Loc a2, int exec_[2]) {
+    exec_[0] = 1;
+    exec_[1] = 1;
+    Loc n1 = loc_add(l1, a1);
+    if (collidable(gridsquare_at(e, n1))) n1 = l1;
+    Loc n2 = loc_add(l2, a2);
+    if (collidable(gridsquare_at(e, n2))) n2 = l2;
+    Loc zero = NAV[OC_ACT_NOOP];
+    if (loc_eq(n1, n2)) {
+        if (loc_eq(n1, l1) && !loc_eq(a1, zero)) {
+            exec_[1] = 0;
+        } else if (loc_eq(n2, l2) && !loc_eq(a2, zero)) {
+            exec_[0] = 0;
+        } else {
+            exec_[0] = 0;
+            exec_[1] = 0;
+        }
+    } else if (loc_eq(l1, n2) && loc_eq(l2, n1)) {
+        exec_[0] = 0;
+        exec_[1] = 0;
+    }
+}
+
+/* OvercookedEnvironment.check_collisions (overcooked_environment.py:724-762); returns the
+ * pair mask in itertools.combinations order. */
+static int check_collisions(Env* e) {
+    int execute[OC_MAX_AGENTS];
+    for (int i = 0; i < e->A; ++i) execute[i] = 1;
+    int pair = 0, mask = 0;
+    for (int i = 0; i < e->A; ++i)
+        for (int j = i + 1; j < e->A; ++j, ++pair) {
+            int ex[2];
+            is_collision(e, e->agents[i].location, e->agents[j].location, e->agents[i].action,
+                         e->agents[j].action, ex);
+            if (!ex[0]) execute[i] = 0;
+            if (!ex[1]) execute[j] = 0;
+            if (!(ex[0] && ex[1])) mask |= 1 << pair; /* CollisionRepr appended */
+        }
+    for (int i = 0; i < e->A; ++i)
+        if (!execute[i]) e->agents[i].action = NAV[OC_ACT_NOOP];
+    return mask;
+}
+
+/* new_obs = copy.copy(self) (overcooked_environment.py:289 -> __copy__ :108-113): every
+ * holding agent must find exactly one held object at its location (world.py:417). */
+static int copy_would_raise(const Env* e) {
+    for (int i = 0; i < e->A; ++i)
+        if (e->agents[i].holding >= 0 && object_at(e, e->agents[i].location, 1) < 0) return 1;
+    return 0;
+}
+
+/* done() (overcooked_environment.py:316-363) + reward() (:365-376). Returns flags. */
+static int done_flags(const Env* e, int max_T) {
+    if (e->t >= max_T && max_T) return OC_FLAG_DONE; /* :328-332 */
+    const oc_level_desc* L = e->L;
+    int dcell = -1; /* first Delivery in World.objects order = map scan order (:349) */
+    for (int c = 0; c < L->width * L->height; ++c)
+        if (L->tiles[c] == OC_TILE_DELIVERY) { dcell = c; break; }
+    Loc dloc = {dcell % L->width, dcell / L->width};
+    for (int g = 0; g < L->num_goals; ++g) { /* every Deliver subtask (:344-359) */
+        int gm = L->goal_mask[g], ok = 0;
+        for (int i = 0; i < e->K; ++i) {
+            const Obj* o = &e->objs[i];
+            if (!o->alive || !loc_eq(o->location, dloc)) continue;
+            int m = o->plates ? OC_M_PLATE : 0; /* goal_obj == o (core.py:143-148) */
+            for (int f = 0; f < NFOOD; ++f)
+                if (o->food_present[f]) m |= (1 << f) | (o->food_state[f] << (f + OC_M_CHOPPED_SHIFT));
+            if (m == gm) ok = 1;
+        }
+        if (!ok) return 0;
+    }
+    return OC_FLAG_DONE | OC_FLAG_SUCCESS;
+}
+
+/* ---- canonical layout <-> object model ---- */
+
+typedef struct {
+    const oc_level_desc* L;
+    int A, K, max_T;
+    int64_t pitch;
+} Cfg;
+
+static void unpack(const Cfg* c, const uint8_t* s, int64_t e, Env* env, int* flags) {
+    const int64_t P = c->pitch;
+    env->L = c->L;
+    env->A = c->A;
+    env->K = c->K;
+    const int A = c->A, K = c->K;
+    const uint8_t* ax = s + 0 * A * P;
+    const uint8_t* ay = s + 1 * A * P;
+    const uint8_t* ah = s + 2 * A * P;
+    const uint8_t* il = s + 3 * A * P;
+    const uint8_t* im = s + (3 * A + K) * P;
+    const uint16_t* tp = (const uint16_t*)(s + (3 * A + 2 * K) * P);
+    const uint8_t* fl = s + (3 * A + 2 * K + 2) * P;
+    env->t = tp[e];
+    *flags = fl[e];
+    for (int k = 0; k < K; ++k) {
+        Obj* o = &env->objs[k];
+        memset(o, 0, sizeof(*o));
+        uint8_t loc = il[k * P + e], m = im[k * P + e];
+        o->alive = loc != OC_LOC_DEAD;
+        o->location.x = loc % c->L->width;
+        o->location.y = loc / c->L->width;
+        o->plates = (m & OC_M_PLATE) ? 1 : 0;
+        for (int f = 0; f < NFOOD; ++f) {
+            o->food_present[f] = (m >> f) & 1;
+            o->food_state[f] = (m >> (f + OC_M_CHOPPED_SHIFT)) & 1;
+        }
+    }
+    for (int a = 0; a < A; ++a) {
+        Agent* g = &env->agents[a];
+        g->location.x = ax[a * P + e];
+        g->location.y = ay[a * P + e];
+        uint8_t h = ah[a * P + e];
+        g->holding = h == OC_HOLD_NONE ? -1 : h;
+        if (g->holding >= K) abort();
+        g->action = NAV[OC_ACT_NOOP];
+    }
+    for (int a = 0; a < A; ++a)
+        if (env->agents[a].holding >= 0) env->objs[env->agents[a].holding].is_held = 1;
+}
+
+static void pack(const Cfg* c, const Env* env, int flags, uint8_t* s, int64_t e) {
+    const int64_t P = c->pitch;
+    const int A = c->A, K = c->K;
+    uint8_t* ax = s + 0 * A * P;
+    uint8_t* ay = s + 1 * A * P;
+    uint8_t* ah = s + 2 * A * P;
+    uint8_t* il = s + 3 * A * P;
+    uint8_t* im = s + (3 * A + K) * P;
+    uint16_t* tp = (uint16_t*)(s + (3 * A + 2 * K) * P);
+    uint8_t* fl = s + (3 * A + 2 * K + 2) * P;
+    tp[e] = (uint16_t)env->t;
+    fl[e] = (uint8_t)flags;
+    for (int a = 0; a < A; ++a) {
+        ax[a * P + e] = (uint8_t)env->agents[a].location.x;
+        ay[a * P + e] = (uint8_t)env->agents[a].location.y;
+        ah[a * P + e] = env->agents[a].holding < 0 ? OC_HOLD_NONE : (uint8_t)env->agents[a].holding;
+    }
+    for (int k = 0; k < K; ++k) {
+        const Obj* o = &env->objs[k];
+        if (!o->alive) {
+            il[k * P + e] = OC_LOC_DEAD;
+            im[k * P + e] = 0;
+            continue;
+        }
+        il[k * P + e] = (uint8_t)(o->location.y * c->L->width + o->location.x);
+        int m = o->plates ? OC_M_PLATE : 0;
+        for (int f = 0; f < NFOOD; ++f)
+            if (o->food_present[f]) m |= (1 << f) | (o->food_state[f] << (f + OC_M_CHOPPED_SHIFT));
+        im[k * P + e] = (uint8_t)m;
+    }
+}
+
+/* reset() (overcooked_environment.py:201-250) -> load_level (:130-198) template */
+static void template_env(const Cfg* c, Env* env) {
+    memset(env, 0, sizeof(*env));
+    env->L = c->L;
+    env->A = c->A;
+    env->K = c->K;
+    env->t = 0;
+    for (int k = 0; k < c->K; ++k) {
+        Obj* o = &env->objs[k];
+        if (k >= c->L->num_items) { o->alive = 0; continue; }
+        o->alive = 1;
+        o->location.x = c->L->item_cell[k] % c->L->width;
+        o->location.y = c->L->item_cell[k] / c->L->width;
+        int m = c->L->item_mask[k];
+        o->plates = (m & OC_M_PLATE) ? 1 : 0;
+        for (int f = 0; f < NFOOD; ++f) {
+            o->food_present[f] = (m >> f) & 1;
+            o->food_state[f] = (m >> (f + OC_M_CHOPPED_SHIFT)) & 1;
+        }
+    }
+    for (int a = 0; a < c->A; ++a) {
+        env->agents[a].location.x = c->L->spawn_x[a];
+        env->agents[a].location.y = c->L->spawn_y[a];
+        env->agents[a].holding = -1;
+        env->agents[a].action = NAV[OC_ACT_NOOP];
+    }
+}
+
+/* step() (overcooked_environment.py:255-306) for env e. */
+static void step_one(const Cfg* c, const uint8_t* sin, uint8_t* sout, const uint8_t* act,
+                     uint8_t* exec_out, uint8_t* coll_out, int64_t e) {
+    Env env;
+    int flags;
+    unpack(c, sin, e, &env, &flags);
+    const int64_t P = c->pitch;
+    if (flags & OC_FLAG_DONE) { /* next-step auto-reset (build definition) */
+        template_env(c, &env);
+        pack(c, &env, 0, sout, e);
+        for (int a = 0; a < c->A; ++a)
+            if (exec_out) exec_out[a * P + e] = OC_ACT_NOOP;
+        if (coll_out) coll_out[e] = 0;
+        return;
+    }
+    env.t += 1; /* :257 */
+    for (int a = 0; a < c->A; ++a) { /* :263-264 */
+        int code = act[a * P + e];
+        env.agents[a].action = NAV[code > OC_ACT_NOOP ? OC_ACT_NOOP : code];
+    }
+    int cmask = check_collisions(&env); /* :267 */
+    int ex[OC_MAX_AGENTS];
+    for (int a = 0; a < c->A; ++a) { /* execute_navigation :767-770 */
+        interact(&env, &env.agents[a]);
+        ex[a] = action_code(env.agents[a].action);
+    }
+    int out_flags;
+    if (copy_would_raise(&env))
+        out_flags = OC_FLAG_DONE | OC_FLAG_ERR;
+    else
+        out_flags = done_flags(&env, c->max_T); /* :295-298 */
+    pack(c, &env, out_flags, sout, e);
+    for (int a = 0; a < c->A; ++a)
+        if (exec_out) exec_out[a * P + e] = (uint8_t)ex[a];
+    if (coll_out) coll_out[e] = (uint8_t)cmask;
+}
+
+typedef struct {
+    const Cfg* c;
+    const uint8_t* sin;
+    uint8_t* sout;
+    const uint8_t* act;
+    uint8_t* ex;
+    uint8_t* coll;
+    int64_t lo, hi;
+} Job;
+
+static void* run_job(void* p) {
+    Job* j = (Job*)p;
+    for (int64_t e = j->lo; e < j->hi; ++e) step_one(j->c, j->sin, j->sout, j->act, j->ex, j->coll, e);
+    return NULL;
+}
+
+/* Batched oracle step over the canonical layout (same semantics as oc_step). */
+int oco_step(const oc_level_desc* L, int A, int K, int max_T, const uint8_t* sin, uint8_t* sout,
+             const uint8_t* act, uint8_t* exec_out, uint8_t* coll_out, int64_t B, int64_t pitch,
+             int nthreads) {
+    if (A < 1 || A > OC_MAX_AGENTS || K < 1 || K > OC_MAX_ITEMS || B < 0 || pitch < B) return OC_EINVAL;
+    Cfg c = {L, A, K, max_T, pitch};
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads == 1 || B < 4096) {
+        Job j = {&c, sin, sout, act, exec_out, coll_out, 0, B};
+        run_job(&j);
+        return OC_OK;
+    }
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    Job jobs[256];
+    int64_t chunk = (B + nthreads - 1) / nthreads;
+    for (int i = 0; i < nthreads; ++i) {
+        int64_t lo = i * chunk, hi = lo + chunk > B ? B : lo + chunk;
+        if (lo > B) lo = B;
+        Job j = {&c, sin, sout, act, exec_out, coll_out, lo, hi};
+        jobs[i] = j;
+        pthread_create(&th[i], NULL, run_job, &jobs[i]);
+    }
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+    return OC_OK;
+}
+
+int oco_reset(const oc_level_desc* L, int A, int K, uint8_t* state, int64_t B, int64_t pitch) {
+    if (A < 1 || A > OC_MAX_AGENTS || K < 1 || K > OC_MAX_ITEMS || pitch < B) return OC_EINVAL;
+    Cfg c = {L, A, K, 0, pitch};
+    Env env;
+    template_env(&c, &env);
+    for (int64_t e = 0; e < B; ++e) pack(&c, &env, 0, state, e);
+    return OC_OK;
+}
+
+/* splitmix64 counter RNG (SURVEY 8d synthetic streams) */
+static uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+uint8_t oco_action_code(uint64_t seed, uint64_t gid, uint64_t step, uint64_t agent) {
+    uint64_t x = seed ^ (gid * 0x9E3779B97F4A7C15ull) ^ (step * 0xC2B2AE3D27D4EB4Full) ^ agent;
+    return (uint8_t)(splitmix64(x) % 5u);
+}
+
+int oco_gen_actions(int A, uint8_t* act, int64_t B, int64_t pitch, int64_t env_offset, int64_t step,
+                    uint64_t seed) {
+    for (int a = 0; a < A; ++a)
+        for (int64_t e = 0; e < B; ++e)
+            act[a * pitch + e] = oco_action_code(seed, (uint64_t)(env_offset + e), (uint64_t)step, (uint64_t)a);
+    return OC_OK;
+}

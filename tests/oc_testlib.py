@@ -1,0 +1,165 @@
+"""Shared test helpers: canonical state views, golden-fixture replay."""
+from __future__ import annotations
+
+import os
+import sys
+from typing import Dict, List
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gym-cooking_amd"))
+sys.path.insert(0, ROOT)
+
+from gym_cooking_amd import capi, levels  # noqa: E402
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+PAD = 255
+
+
+def planes_view(state: np.ndarray, A: int, K: int, pitch: int) -> Dict[str, np.ndarray]:
+    """Split a flat layout buffer (host numpy) into named plane views."""
+    P = capi.layout_planes(A, K)
+    s = state.reshape(P["num_planes"], pitch)
+    return dict(
+        ax=s[P["agent_x"]:P["agent_x"] + A], ay=s[P["agent_y"]:P["agent_y"] + A],
+        ah=s[P["agent_hold"]:P["agent_hold"] + A], il=s[P["item_loc"]:P["item_loc"] + K],
+        im=s[P["item_mask"]:P["item_mask"] + K],
+        t=s[P["t"]:P["t"] + 2].reshape(-1).view(np.uint16)[:pitch], fl=s[P["flags"]],
+    )
+
+
+def canonical(state: np.ndarray, A: int, K: int, pitch: int, width: int, B: int):
+    """SURVEY App. A.7 canonical form of the first B envs: t, flags, agents [B,4,3]
+    (x, y, held mask), items [B,K,4] sorted (mask, x, y, held), PAD rows last."""
+    v = planes_view(state, A, K, pitch)
+    ax, ay, ah = v["ax"][:, :B].T, v["ay"][:, :B].T, v["ah"][:, :B].T      # [B, A]
+    il, im = v["il"][:, :B].T.astype(np.int64), v["im"][:, :B].T.astype(np.int64)  # [B, K]
+    agents = np.full((B, 4, 3), PAD, np.uint8)
+    agents[:, :A, 0] = ax
+    agents[:, :A, 1] = ay
+    hold = ah.astype(np.int64)
+    hm = np.where(hold < K, np.take_along_axis(im, np.minimum(hold, K - 1), axis=1), 0)
+    agents[:, :A, 2] = hm
+    held = np.zeros((B, K), bool)
+    for a in range(A):
+        held |= hold[:, a:a + 1] == np.arange(K)[None, :]
+    alive = il != 0xFF
+    x, y = il % width, il // width
+    key = (im << 24) | (x << 16) | (y << 8) | held.astype(np.int64)
+    key = np.where(alive, key, 0xFFFFFFFF)
+    key.sort(axis=1)
+    items = np.stack([(key >> 24) & 0xFF, (key >> 16) & 0xFF, (key >> 8) & 0xFF, key & 0xFF], -1)
+    items = np.where((key == 0xFFFFFFFF)[..., None], PAD, items).astype(np.uint8)
+    if K < 4:
+        items = np.concatenate([items, np.full((B, 4 - K, 4), PAD, np.uint8)], 1)
+    return dict(t=v["t"][:B].copy(), flags=v["fl"][:B].copy(), agents=agents, items=items[:, :4])
+
+
+def load_fixture(name: str):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+class EpisodeGroup:
+    """Fixture episodes sharing (level, A, max_T), replayed in lockstep as one batch."""
+
+    def __init__(self, fx, idx: List[int]):
+        self.fx = fx
+        self.idx = idx
+        e0 = idx[0]
+        self.level = levels.load_level(str(fx["level_names"][fx["ep_level"][e0]]))
+        self.A = int(fx["ep_A"][e0])
+        self.max_T = int(fx["ep_maxT"][e0])
+        self.B = len(idx)
+        self.T = np.array([fx["ep_T"][e] for e in idx])
+        self.K = capi.item_slots(self.level)
+
+    def actions_at(self, step: int) -> np.ndarray:
+        """[A, B] action codes at `step` (noop past an episode's end)."""
+        out = np.full((self.A, self.B), 4, np.uint8)
+        for b, e in enumerate(self.idx):
+            if step < self.fx["ep_T"][e]:
+                out[:, b] = self.fx["act"][self.fx["ep_act_off"][e] + step][:self.A]
+        return out
+
+    def relocate(self, state: np.ndarray, pitch: int) -> None:
+        v = planes_view(state, self.A, self.K, pitch)
+        for b, e in enumerate(self.idx):
+            st = self.fx["ep_start"][e]
+            for a in range(self.A):
+                if st[a, 0] != PAD:
+                    v["ax"][a, b], v["ay"][a, b] = st[a, 0], st[a, 1]
+
+    def expected(self, step_state: int, b: int):
+        """Expected canonical record after `step_state` steps for batch env b (None past end)."""
+        e = self.idx[b]
+        if step_state > self.fx["ep_T"][e]:
+            return None
+        o = self.fx["ep_state_off"][e] + step_state
+        return dict(t=self.fx["t"][o], flags=self.fx["flags"][o], agents=self.fx["agents"][o],
+                    items=self.fx["items"][o])
+
+    def expected_step(self, step: int, b: int):
+        e = self.idx[b]
+        if step >= self.fx["ep_T"][e]:
+            return None
+        o = self.fx["ep_act_off"][e] + step
+        return self.fx["exe"][o], self.fx["coll"][o]
+
+
+def episode_groups(fx) -> List[EpisodeGroup]:
+    keys = {}
+    for e in range(len(fx["ep_T"])):
+        k = (int(fx["ep_level"][e]), int(fx["ep_A"][e]), int(fx["ep_maxT"][e]))
+        keys.setdefault(k, []).append(e)
+    return [EpisodeGroup(fx, v) for _, v in sorted(keys.items())]
+
+
+def compare_group(group: EpisodeGroup, step_fn, init_state: np.ndarray, pitch: int, width: int):
+    """Replay `group` through step_fn(state_in, actions[A,B]) -> (state_out, exec[A,B], coll[B]),
+    comparing against the fixtures; returns the list of mismatch descriptions."""
+    errs = []
+    state = init_state
+    alive = np.ones(group.B, bool)
+    c = canonical(state, group.A, group.K, pitch, width, group.B)
+    for b in range(group.B):
+        exp = group.expected(0, b)
+        if not _eq(c, b, exp):
+            errs.append("env %d: initial state mismatch" % group.idx[b])
+    for step in range(int(group.T.max())):
+        acts = group.actions_at(step)
+        state, ex, coll = step_fn(state, acts)
+        c = canonical(state, group.A, group.K, pitch, width, group.B)
+        for b in range(group.B):
+            if not alive[b]:
+                continue
+            exp = group.expected(step + 1, b)
+            if exp is None:
+                alive[b] = False
+                continue
+            if exp["flags"] & 0x04:  # ERR: the reference raised; only the flag is defined
+                if c["flags"][b] != exp["flags"]:
+                    errs.append("env %d step %d: ERR flag %d vs %d" % (group.idx[b], step + 1,
+                                                                       c["flags"][b], exp["flags"]))
+                alive[b] = False
+                continue
+            if not _eq(c, b, exp):
+                errs.append("env %d step %d: state mismatch got t=%d fl=%d ag=%s it=%s | exp t=%d fl=%d ag=%s it=%s" % (
+                    group.idx[b], step + 1, c["t"][b], c["flags"][b], c["agents"][b].tolist(),
+                    c["items"][b].tolist(), exp["t"], exp["flags"], exp["agents"].tolist(),
+                    exp["items"].tolist()))
+                alive[b] = False
+                continue
+            eex, ecoll = group.expected_step(step, b)
+            if not (np.array_equal(ex[:, b], eex[:group.A]) and coll[b] == ecoll):
+                errs.append("env %d step %d: exec %s coll %d vs %s %d" % (
+                    group.idx[b], step + 1, ex[:, b].tolist(), coll[b], eex[:group.A].tolist(), ecoll))
+                alive[b] = False
+        if len(errs) > 20:
+            break
+    return errs
+
+
+def _eq(c, b, exp) -> bool:
+    return (int(c["t"][b]) == int(exp["t"]) and int(c["flags"][b]) == int(exp["flags"])
+            and np.array_equal(c["agents"][b], exp["agents"]) and np.array_equal(c["items"][b], exp["items"]))

@@ -1,0 +1,61 @@
+"""CPU-side checks of the C-ABI library: it loads and exports every symbol include/oc_engine.h
+declares (no compute calls: there is no GPU here), and layout arithmetic agrees."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import oc_testlib as tl
+from gym_cooking_amd import capi, levels
+
+HEADER = os.path.join(tl.ROOT, "include", "oc_engine.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(oc_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declarations_match_binding():
+    assert _declared() == sorted(capi.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_symbol():
+    if not os.path.isfile(capi.LIB_PATH):
+        pytest.skip("liboc_engine.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(capi.LIB_PATH)
+    for sym in _declared():
+        assert hasattr(lib, sym), sym
+    lib = capi.load_library()
+    assert lib.oc_abi_version() == 1
+
+
+def test_create_layout_and_validation_without_gpu():
+    """oc_create / oc_get_layout are host-only: exercise them (and the level validation)."""
+    if not os.path.isfile(capi.LIB_PATH):
+        pytest.skip("liboc_engine.so not built")
+    lib = capi.load_library()
+    lv = levels.load_level("partial-divider_salad")
+    d = capi.level_desc(lv, 2)
+    h = ctypes.c_void_p()
+    assert lib.oc_create(ctypes.byref(d), 2, 100, 0, ctypes.byref(h)) == 0
+    lay = capi.OcLayout()
+    assert lib.oc_get_layout(h, 1 << 20, ctypes.byref(lay)) == 0
+    P = capi.layout_planes(2, 4)
+    assert lay.num_planes == P["num_planes"] == 17  # S(A=2) = 3A + 11 bytes per env
+    assert lay.pitch == 1 << 20 and lay.state_bytes == 17 << 20
+    assert (lay.plane_item_loc, lay.plane_t, lay.plane_flags) == (P["item_loc"], P["t"], P["flags"])
+    n = ctypes.c_int64()
+    assert lib.oc_stats_size(h, 1 << 20, ctypes.byref(n)) == 0 and n.value == 1024 * 5 * 8
+    assert lib.oc_destroy(h) == 0
+    # bad levels are rejected with a message
+    bad = capi.level_desc(lv, 2)
+    bad.tiles[0] = 0  # Floor on the border
+    assert lib.oc_create(ctypes.byref(bad), 2, 100, 0, ctypes.byref(h)) == capi_err("ELEVEL")
+    assert b"border" in lib.oc_last_error()
+    assert lib.oc_create(ctypes.byref(d), 5, 100, 0, ctypes.byref(h)) == capi_err("EINVAL")
+
+
+def capi_err(name):
+    return {"EINVAL": -1, "EHIP": -2, "ELEVEL": -3}[name]

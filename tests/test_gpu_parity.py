@@ -1,0 +1,174 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle and the reference's
+golden fixtures.  Integer state => bit-exact equality, no tolerance."""
+import numpy as np
+import pytest
+
+import oc_testlib as tl
+from gym_cooking_amd import capi, levels
+
+from oracle import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from gym_cooking_amd import engine  # noqa: F401  (loads liboc_engine.so or raises)
+    return torch.device("cuda:0")
+
+
+def _batch(level, A, B, max_T=100):
+    from gym_cooking_amd.engine import OvercookedBatch
+    return OvercookedBatch(level, A, B, max_T=max_T, device="cuda:0")
+
+
+def _gpu_step_fn(eb):
+    def fn(state, acts):
+        s_in = torch.from_numpy(state).cuda()
+        a = torch.full((eb.A, eb.pitch), 4, dtype=torch.uint8)
+        a[:, :eb.B] = torch.from_numpy(acts)
+        a = a.reshape(-1).cuda()
+        out = eb.new_state()
+        ex = eb.new_exec()
+        coll = eb.new_coll()
+        eb.step(s_in, out, a, ex, coll)
+        return (out.cpu().numpy(), ex.view(eb.A, eb.pitch)[:, :eb.B].cpu().numpy(),
+                coll[:eb.B].cpu().numpy())
+    return fn
+
+
+@pytest.mark.parametrize("fixture", ["kat.npz", "streams.npz"])
+def test_engine_matches_reference_fixtures(dev, fixture):
+    fx = tl.load_fixture(fixture)
+    for g in tl.episode_groups(fx):
+        eb = _batch(g.level, g.A, g.B, g.max_T)
+        s = eb.new_state()
+        eb.reset(s)
+        host = s.cpu().numpy()
+        g.relocate(host, eb.pitch)
+        errs = tl.compare_group(g, _gpu_step_fn(eb), host, eb.pitch, g.level.width)
+        assert not errs, "\n".join(errs[:10])
+
+
+def _run_parity(level, A, B, steps, seed, max_T=100, check_every=1, nthreads=8):
+    """Engine vs oracle, full-buffer bit-exact over `steps` steps of counter-RNG actions."""
+    eb = _batch(level, A, B, max_T)
+    ob = oracle.OracleBatch(eb.level, A, max_T, B)
+    assert ob.pitch == eb.pitch
+    s_gpu, s_next = eb.new_state(), eb.new_state()
+    eb.reset(s_gpu)
+    s_cpu = ob.new_state()
+    ob.reset(s_cpu)
+    a_gpu = eb.new_actions()
+    ex_gpu, coll_gpu, stats = eb.new_exec(), eb.new_coll(), eb.new_stats()
+    a_cpu = ob.new_actions()
+    ex_cpu = np.zeros(A * ob.pitch, np.uint8)
+    coll_cpu = np.zeros(ob.pitch, np.uint8)
+    nxt_cpu = ob.new_state()
+    P = ob.pitch
+    totals = np.zeros(5, np.int64)
+    for t in range(steps):
+        eb.gen_actions(a_gpu, t, seed)
+        ob.gen_actions(a_cpu, 0, t, seed)
+        eb.step(s_gpu, s_next, a_gpu, ex_gpu, coll_gpu, stats)
+        s_gpu, s_next = s_next, s_gpu
+        fl_in = tl.planes_view(s_cpu, A, ob.K, P)["fl"][:B].copy()
+        ob.step(s_cpu, nxt_cpu, a_cpu, ex_cpu, coll_cpu, nthreads=nthreads)
+        s_cpu, nxt_cpu = nxt_cpu, s_cpu
+        v = tl.planes_view(s_cpu, A, ob.K, P)
+        ended = ((fl_in & 1) == 0) & ((v["fl"][:B] & 1) == 1)
+        totals += [ended.sum(), (ended & ((v["fl"][:B] & 2) == 2)).sum(), v["t"][:B][ended].astype(np.int64).sum(),
+                   np.unpackbits(coll_cpu[:B]).sum(), (ended & ((v["fl"][:B] & 4) == 4)).sum()]
+        if t % check_every == 0 or t == steps - 1:
+            g = s_gpu.cpu().numpy().reshape(-1, P)[:, :B]
+            c = s_cpu.reshape(-1, P)[:, :B]
+            if not np.array_equal(g, c):
+                bad = np.argwhere(g != c)
+                raise AssertionError("state mismatch at step %d: %d bytes differ, first (plane, env) %s"
+                                     % (t, len(bad), bad[:5].tolist()))
+            assert np.array_equal(a_gpu.cpu().numpy().reshape(A, P)[:, :B], a_cpu.reshape(A, P)[:, :B])
+            assert np.array_equal(ex_gpu.cpu().numpy().reshape(A, P)[:, :B], ex_cpu.reshape(A, P)[:, :B])
+            assert np.array_equal(coll_gpu.cpu().numpy()[:B], coll_cpu[:B])
+    got = eb.reduce_stats(stats).cpu().numpy().astype(np.int64)
+    assert np.array_equal(got, totals), (got, totals)
+    return totals
+
+
+def test_c2_partial_salad_65536_bitexact(dev):
+    """BASELINE config C2: partial-divider_salad, 2 agents, B=65,536, bit-exact vs CPU."""
+    tot = _run_parity("partial-divider_salad", 2, 65536, 250, seed=3, check_every=1)
+    assert tot[0] > 0  # episodes ended (timeouts at t=100) -> auto-reset exercised
+
+
+def test_c3_full_tl_3a_1m(dev):
+    """BASELINE config C3 shape: full-divider_tl, 3 agents, B=2^20 (collision-heavy path)."""
+    _run_parity("full-divider_tl", 3, 1 << 20, 12, seed=11, check_every=4, nthreads=16)
+
+
+def test_c5_layout_full_salad_4a(dev):
+    _run_parity("full-divider_salad", 4, 1 << 16, 120, seed=5, check_every=7)
+
+
+@pytest.mark.parametrize("level", sorted(levels.BUILTIN_LEVELS))
+@pytest.mark.parametrize("A", [1, 2, 3, 4])
+def test_all_levels_all_agent_counts(dev, level, A):
+    _run_parity(level, A, 3000, 110, seed=A * 7 + len(level), max_T=50, check_every=9)
+
+
+@pytest.mark.parametrize("B", [1, 3, 4097, 8192 + 5])
+def test_ragged_batch_sizes(dev, B):
+    _run_parity("open-divider_tl", 3, B, 60, seed=B, max_T=25)
+
+
+def test_unlimited_max_T_and_long_t(dev):
+    _run_parity("open-divider_salad", 2, 2048, 300, seed=9, max_T=0, check_every=50)
+
+
+def test_in_place_step_equals_ping_pong(dev):
+    eb = _batch("partial-divider_salad", 2, 1 << 14)
+    a, b, c = eb.new_state(), eb.new_state(), eb.new_state()
+    eb.reset(a)
+    b.copy_(a)
+    act = eb.new_actions()
+    for t in range(40):
+        eb.gen_actions(act, t, 1)
+        eb.step(a, c, act)
+        a.copy_(c)
+        eb.step(b, b, act)
+        assert torch.equal(a, b)
+
+
+def test_invalid_action_codes_are_noops(dev):
+    eb = _batch("open-divider_salad", 2, 4096)
+    s0, s1, s2 = eb.new_state(), eb.new_state(), eb.new_state()
+    eb.reset(s0)
+    bad = torch.randint(5, 256, (eb.A * eb.pitch,), dtype=torch.uint8, device="cuda")
+    ex = eb.new_exec()
+    eb.step(s0, s1, bad, ex)
+    eb.step(s0, s2, eb.new_actions(), None)
+    assert torch.equal(s1, s2)
+    assert bool((ex.view(eb.A, eb.pitch)[:, :eb.B] == 4).all())
+
+
+def test_sharded_ids_match_single_batch(dev):
+    """Multi-GPU partitioning: envs [off, off+n) stepped as their own batch with env_offset
+    reproduce the same envs of the full batch (RNG keyed by global env id)."""
+    full = _batch("partial-divider_salad", 2, 8192)
+    half = _batch("partial-divider_salad", 2, 4096)
+    sf, sf2 = full.new_state(), full.new_state()
+    sh, sh2 = half.new_state(), half.new_state()
+    full.reset(sf)
+    half.reset(sh)
+    af, ah = full.new_actions(), half.new_actions()
+    for t in range(30):
+        full.gen_actions(af, t, 42)
+        half.gen_actions(ah, t, 42, env_offset=4096)
+        full.step(sf, sf2, af)
+        half.step(sh, sh2, ah)
+        sf, sf2, sh, sh2 = sf2, sf, sh2, sh
+    pf = full.planes(sf)
+    ph = half.planes(sh)
+    for k in pf:
+        assert torch.equal(pf[k][..., 4096:8192], ph[k][..., :4096]), k
