@@ -17,10 +17,12 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
 #include "../../include/oc_engine.h"
+#include "oc_swar.h"
 
 namespace {
 
@@ -43,168 +45,11 @@ struct LevelArgs {
     uint32_t tmpl_cell[2], tmpl_mask[2];  // item slots 0..7, one per byte
     int64_t pitch;
     int64_t B;
+    ocsw::SwarLevel sw;  // replicated constants / LUTs of the SWAR step
 };
 
-// action code -> (dx + 1) / (dy + 1), 4 bits per code: World.NAV_ACTIONS (world.py:16) + noop
-constexpr uint32_t kDXLUT = 0x12011u;  // codes 0..4 -> dx 0,0,-1,+1,0
-constexpr uint32_t kDYLUT = 0x11102u;  // codes 0..4 -> dy +1,-1,0,0,0
-
-__device__ __forceinline__ uint32_t bit64(uint64_t m, uint32_t c) {
-    return (uint32_t)(m >> (c & 63u)) & 1u;
-}
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, int j) { return (w >> (8 * j)) & 0xFFu; }
-__device__ __forceinline__ uint32_t byte_of2(const uint32_t (&w)[2], int j) {
-    return byte_of(w[j >> 2], j & 3);
-}
-
-// Object.is_deliverable (core.py:214-219): >= 2 contents, every food in its last state.
-__device__ __forceinline__ bool deliverable(uint32_t m) {
-    return __popc(m & 0xFu) >= 2 && ((m & 7u) & ~(m >> OC_M_CHOPPED_SHIFT)) == 0u;
-}
-// mergeable (core.py:222-241): at most one plate, every food chopped.
-__device__ __forceinline__ bool mergeable(uint32_t a, uint32_t b) {
-    const uint32_t c = a | b;
-    return ((a & b) & OC_M_PLATE) == 0u && ((c & 7u) & ~(c >> OC_M_CHOPPED_SHIFT)) == 0u;
-}
-// Object.needs_chopped (core.py:176-178, 285-291): a single fresh food.
-__device__ __forceinline__ bool needs_chop(uint32_t m) {
-    return m != 0u && m <= 4u && (m & (m - 1u)) == 0u;
-}
-
-// One env transition (step(), overcooked_environment.py:255-306) on register-resident fields.
-template <int A, int K>
-__device__ __forceinline__ void step_env(const LevelArgs& L, uint32_t (&ax)[A], uint32_t (&ay)[A],
-                                         uint32_t (&ah)[A], uint32_t (&il)[K], uint32_t (&im)[K],
-                                         uint32_t& t, uint32_t& fl, const uint32_t (&act_in)[A],
-                                         uint32_t (&ex)[A], uint32_t& coll) {
-    const bool rst = (fl & OC_FLAG_DONE) != 0u;  // next-step auto-reset
-
-    uint32_t act[A], loc[A], nraw[A], nxt[A];
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-        act[a] = min(act_in[a], (uint32_t)OC_ACT_NOOP);
-        loc[a] = ay[a] * (uint32_t)L.W + ax[a];
-        nraw[a] = loc[a] + ((uint32_t)(L.dcell_lut >> (8u * act[a])) & 0xFFu) - 128u;
-        // is_collision: a collidable next square reverts to the current one (:692-700)
-        nxt[a] = bit64(L.floor_mask, nraw[a]) ? nraw[a] : loc[a];
-    }
-
-    // check_collisions: pairs in itertools.combinations order on the ORIGINAL actions,
-    // blocked agents zeroed after all pairs (:724-762).
-    uint32_t blk = 0u, cm = 0u;
-    int p = 0;
-#pragma unroll
-    for (int i = 0; i < A; ++i) {
-#pragma unroll
-        for (int j = i + 1; j < A; ++j, ++p) {
-            const bool eq = nxt[i] == nxt[j];
-            const bool c1 = nxt[i] == loc[i] && act[i] != OC_ACT_NOOP;
-            const bool c2 = nxt[j] == loc[j] && act[j] != OC_ACT_NOOP;
-            const bool sw = loc[i] == nxt[j] && loc[j] == nxt[i];
-            const bool bi = eq ? !c1 : sw;
-            const bool bj = eq ? (c1 || !c2) : sw;
-            blk |= ((uint32_t)bi << i) | ((uint32_t)bj << j);
-            cm |= (uint32_t)(bi || bj) << p;
-        }
-    }
-
-    // execute_navigation: interact() per agent in order, each seeing earlier agents' effects.
-#pragma unroll
-    for (int k = 0; k < A; ++k) {
-        const bool blocked = (blk >> k) & 1u;
-        const uint32_t e = blocked ? (uint32_t)OC_ACT_NOOP : act[k];
-        ex[k] = e;
-        const bool go = e != OC_ACT_NOOP;
-        // target = inbounds(loc + action) (interact.py:22); agents stand on Floor and the
-        // border is never Floor, so the clamp is the identity and target = nraw.
-        const uint32_t tc = nraw[k];
-        const bool isF = bit64(L.floor_mask, tc);
-        const bool isD = bit64(L.deliv_mask, tc);
-        const bool isC = bit64(L.cut_mask, tc);
-        const uint32_t h = ah[k];
-        const bool hold = h != OC_HOLD_NONE;
-        // the un-held object at target (world.is_occupied / get_object_at): any item on a
-        // non-Floor cell is un-held, since held items sit on their holder's Floor cell.
-        uint32_t o = OC_HOLD_NONE, om = 0u, hm = 0u;
-#pragma unroll
-        for (int j = K - 1; j >= 0; --j) {
-            const bool at = il[j] == tc;
-            o = at ? (uint32_t)j : o;
-            om = at ? im[j] : om;
-            hm = (h == (uint32_t)j) ? im[j] : hm;
-        }
-        const bool hasO = o != OC_HOLD_NONE;
-        const bool nf = go && !isF;
-        const bool move = go && isF;                                           // :28-30
-        const bool deliver = nf && hold && isD && deliverable(hm);             // :35-40
-        const bool merge = nf && hold && !isD && hasO && mergeable(hm, om);    // :43-56
-        const bool empty = nf && hold && !isD && !hasO;                        // :60-70
-        const bool chop = empty && isC && needs_chop(hm);
-        const bool put = empty && !chop;
-        const bool pick = nf && !hold && hasO && !isD;                         // :73-84
-        const bool relocate_h = move || deliver || put;  // held item goes to tc
-        const uint32_t dxp = (kDXLUT >> (4u * e)) & 0xFu;
-        const uint32_t dyp = (kDYLUT >> (4u * e)) & 0xFu;
-        ax[k] = move ? ax[k] + dxp - 1u : ax[k];
-        ay[k] = move ? ay[k] + dyp - 1u : ay[k];
-        const uint32_t merged = hm | om;
-        const uint32_t chopped = hm | (hm << OC_M_CHOPPED_SHIFT);
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const bool isH = h == (uint32_t)j;
-            const bool isO = o == (uint32_t)j;
-            uint32_t l = il[j], m = im[j];
-            l = (isH && relocate_h) ? tc : l;
-            m = (isH && merge) ? merged : m;
-            m = (isH && chop) ? chopped : m;
-            l = (isO && merge) ? (uint32_t)OC_LOC_DEAD : l;
-            m = (isO && merge) ? 0u : m;
-            l = (isO && pick) ? loc[k] : l;
-            il[j] = l;
-            im[j] = m;
-        }
-        ah[k] = (deliver || put) ? (uint32_t)OC_HOLD_NONE : (pick ? o : h);
-    }
-
-    // new_obs = copy.copy(self) raises when two co-located agents both hold (ERR).
-    bool err = false;
-#pragma unroll
-    for (int i = 0; i < A; ++i)
-#pragma unroll
-        for (int j = i + 1; j < A; ++j)
-            err |= ax[i] == ax[j] && ay[i] == ay[j] && ah[i] != OC_HOLD_NONE && ah[j] != OC_HOLD_NONE;
-
-    const uint32_t tn = t + 1u;  // :257
-    // done(): timeout first (:328-332), then every Deliver goal on the delivery cell (:344-363)
-    const bool tout = L.max_T != 0 && tn >= (uint32_t)L.max_T;
-    bool all_ok = true;
-    for (int g = 0; g < L.ngoals; ++g) {  // wave-uniform trip count
-        const uint32_t gm = (L.goals >> (8 * g)) & 0xFFu;
-        bool ok = false;
-#pragma unroll
-        for (int j = 0; j < K; ++j) ok |= il[j] == (uint32_t)L.done_cell && im[j] == gm;
-        all_ok &= ok;
-    }
-    const uint32_t fn = err ? (OC_FLAG_DONE | OC_FLAG_ERR)
-                            : (tout ? OC_FLAG_DONE : (all_ok ? (OC_FLAG_DONE | OC_FLAG_SUCCESS) : 0u));
-
-    // auto-reset: an env that was done at the input restarts from the level template
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-        ax[a] = rst ? byte_of(L.tmpl_x, a) : ax[a];
-        ay[a] = rst ? byte_of(L.tmpl_y, a) : ay[a];
-        ah[a] = rst ? (uint32_t)OC_HOLD_NONE : ah[a];
-        ex[a] = rst ? (uint32_t)OC_ACT_NOOP : ex[a];
-    }
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        il[j] = rst ? byte_of2(L.tmpl_cell, j) : il[j];
-        im[j] = rst ? byte_of2(L.tmpl_mask, j) : im[j];
-    }
-    t = rst ? 0u : tn;
-    fl = rst ? 0u : fn;
-    coll = rst ? 0u : cm;
-}
+__device__ __forceinline__ uint32_t byte_of2(const uint32_t (&w)[2], int j) { return byte_of(w[j >> 2], j & 3); }
 
 // Statistics partial sums, one row of OC_NSTATS uint64 per block.
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
@@ -213,6 +58,93 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
+// One lane's slice of the batch: kEPL consecutive envs, one dword per byte plane.
+template <int A, int K>
+struct Chunk {
+    uint32_t wx[A], wy[A], wh[A], wa[A], wl[K], wm[K];
+    uint2 wt;
+    uint32_t wf;
+};
+
+template <int A, int K>
+__device__ __forceinline__ void load_chunk(Chunk<A, K>& c, const uint8_t* __restrict__ sin,
+                                           const uint8_t* __restrict__ actions, int64_t P, uint32_t g) {
+    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+    auto ld32 = [&](int plane) -> uint32_t { return reinterpret_cast<const uint32_t*>(sin + plane * P)[g]; };
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        c.wx[a] = ld32(a);
+        c.wy[a] = ld32(kPY + a);
+        c.wh[a] = ld32(kPH + a);
+        c.wa[a] = reinterpret_cast<const uint32_t*>(actions + a * P)[g];
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        c.wl[j] = ld32(kPL + j);
+        c.wm[j] = ld32(kPM + j);
+    }
+    c.wt = reinterpret_cast<const uint2*>(sin + kPT * P)[g];
+    c.wf = ld32(kPF);
+}
+
+struct StepStats {
+    uint32_t eps = 0u, succ = 0u, steps = 0u, coll = 0u, err = 0u;
+};
+
+// Step the kEPL envs of chunk c (SWAR, oc_swar.h) and store every output plane word of lane g.
+template <int A, int K>
+__device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tbl, Chunk<A, K>& c,
+                                           uint8_t* __restrict__ sout, uint8_t* __restrict__ exec_out,
+                                           uint8_t* __restrict__ coll_out, int64_t P, uint32_t g, StepStats& st) {
+    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+    auto cls_of = [tbl](uint32_t cells) -> uint32_t {
+        const uint32_t b0 = tbl[cells & 0xFFu], b1 = tbl[(cells >> 8) & 0xFFu], b2 = tbl[(cells >> 16) & 0xFFu],
+                       b3 = tbl[cells >> 24];
+        return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    };
+    const uint32_t f_in = c.wf;
+    uint32_t T0 = c.wt.x, T1 = c.wt.y, ex[A], cm;
+    ocsw::step4<A, K>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, c.wa, ex, cm, cls_of);
+
+    // statistics over the valid envs: an episode ended iff DONE is newly set
+    const int64_t rem = L.B - (int64_t)g * kEPL;
+    const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (rem <= 0 ? 0u : (1u << (8 * (uint32_t)rem)) - 1u);
+    const uint32_t ended = (c.wf & ~f_in & vmask) & ocsw::k01;  // bit0 per env
+    st.eps += __popc(ended);
+    st.succ += __popc(c.wf & (ended << 1));
+    st.err += __popc(c.wf & (ended << 2));
+    st.coll += __popc(cm & vmask);
+    const uint32_t e16a = __builtin_amdgcn_perm(0u, ended * 0xFFu, 0x01010000u);  // env 0,1 -> u16 masks
+    const uint32_t e16b = __builtin_amdgcn_perm(0u, ended * 0xFFu, 0x03030202u);  // env 2,3
+    const uint32_t sa = T0 & e16a, sb = T1 & e16b;
+    st.steps += (sa & 0xFFFFu) + (sa >> 16) + (sb & 0xFFFFu) + (sb >> 16);
+
+    auto st32 = [&](int plane, uint32_t v) { reinterpret_cast<uint32_t*>(sout + plane * P)[g] = v; };
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        st32(a, c.wx[a]);
+        st32(kPY + a, c.wy[a]);
+        st32(kPH + a, c.wh[a]);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        st32(kPL + j, c.wl[j]);
+        st32(kPM + j, c.wm[j]);
+    }
+    reinterpret_cast<uint2*>(sout + kPT * P)[g] = make_uint2(T0, T1);
+    st32(kPF, c.wf);
+    if (exec_out != nullptr) {
+#pragma unroll
+        for (int a = 0; a < A; ++a) reinterpret_cast<uint32_t*>(exec_out + a * P)[g] = ex[a];
+    }
+    if (coll_out != nullptr) reinterpret_cast<uint32_t*>(coll_out)[g] = cm;
+}
+
+// Persistent, software-pipelined step: a grid of a few blocks per CU walks the batch in
+// chunks of kEnvsPerBlock envs; each lane issues the loads of its next chunk before stepping
+// the current one, so HBM reads, VALU work and stores of different chunks overlap instead of
+// running as three chip-wide phases.  Every lane leaves the loop after ceil(lanes/stride)
+// iterations (no inter-block communication, no spin).
 template <int A, int K>
 __global__ __launch_bounds__(kBlock) void oc_step_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
                                                          uint8_t* __restrict__ sout,
@@ -221,104 +153,37 @@ __global__ __launch_bounds__(kBlock) void oc_step_kernel(LevelArgs L, const uint
                                                          uint8_t* __restrict__ coll_out,
                                                          uint64_t* __restrict__ stats) {
     const int64_t P = L.pitch;
-    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t e0 = g * kEPL;  // first env of this lane
-    constexpr int kPA = 0, kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K,
-                  kPF = 3 * A + 2 * K + 2;
-    auto ld32 = [&](int plane) -> uint32_t {
-        return *reinterpret_cast<const uint32_t*>(sin + plane * P + e0);
-    };
-    // ---- coalesced loads: one dword per byte plane, 8 bytes of the u16 t plane
-    uint32_t wx[A], wy[A], wh[A], wl[K], wm[K], wa[A];
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-        wx[a] = ld32(kPA + a);
-        wy[a] = ld32(kPY + a);
-        wh[a] = ld32(kPH + a);
-        wa[a] = *reinterpret_cast<const uint32_t*>(actions + a * P + e0);
+    const uint32_t nlanes = (uint32_t)(P / kEPL);        // multiple of kBlock
+    // tile class per cell (bit7 Floor, bit6 Delivery, bit5 Cutboard); cells >= 64 read 0
+    __shared__ uint8_t tbl[256];
+    {
+        tbl[threadIdx.x] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, threadIdx.x);  // kBlock == 256
+        __syncthreads();
     }
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        wl[j] = ld32(kPL + j);
-        wm[j] = ld32(kPM + j);
-    }
-    const uint2 wt = *reinterpret_cast<const uint2*>(sin + kPT * P + 2 * e0);
-    const uint32_t wf = ld32(kPF);
-
-    uint32_t ox[A] = {}, oy[A] = {}, oh[A] = {}, ol[K] = {}, om[K] = {}, oe[A] = {};
-    uint32_t ot[2] = {0u, 0u}, of = 0u, oc = 0u;
-    uint32_t s_eps = 0u, s_succ = 0u, s_steps = 0u, s_coll = 0u, s_err = 0u;
-
-#pragma unroll
-    for (int q = 0; q < kEPL; ++q) {
-        uint32_t ax[A], ay[A], ah[A], il[K], im[K], ac[A], ex[A];
-#pragma unroll
-        for (int a = 0; a < A; ++a) {
-            ax[a] = byte_of(wx[a], q);
-            ay[a] = byte_of(wy[a], q);
-            ah[a] = byte_of(wh[a], q);
-            ac[a] = byte_of(wa[a], q);
+    const uint32_t stride = gridDim.x * (uint32_t)kBlock;
+    uint32_t g = blockIdx.x * (uint32_t)kBlock + threadIdx.x;
+    StepStats st;
+    // Two register sets used in turn (loop unrolled by 2: no register copies of in-flight
+    // loads).  The prefetch is unconditional so the compiler's counted vmcnt waits stay exact;
+    // past the last chunk it re-reads the current one (an L2 hit, no HBM traffic).
+    Chunk<A, K> ca, cb;
+    if (g < nlanes) {  // block-uniform
+        load_chunk<A, K>(ca, sin, actions, P, g);
+        for (;;) {
+            load_chunk<A, K>(cb, sin, actions, P, g + stride < nlanes ? g + stride : g);
+            step_chunk<A, K>(L, tbl, ca, sout, exec_out, coll_out, P, g, st);
+            g += stride;
+            if (g >= nlanes) break;
+            load_chunk<A, K>(ca, sin, actions, P, g + stride < nlanes ? g + stride : g);
+            step_chunk<A, K>(L, tbl, cb, sout, exec_out, coll_out, P, g, st);
+            g += stride;
+            if (g >= nlanes) break;
         }
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            il[j] = byte_of(wl[j], q);
-            im[j] = byte_of(wm[j], q);
-        }
-        uint32_t t = ((q < 2 ? wt.x : wt.y) >> (16 * (q & 1))) & 0xFFFFu;
-        uint32_t fl = byte_of(wf, q);
-        const bool was_done = (fl & OC_FLAG_DONE) != 0u;
-        uint32_t coll;
-        step_env<A, K>(L, ax, ay, ah, il, im, t, fl, ac, ex, coll);
-        const int sh = 8 * q;
-#pragma unroll
-        for (int a = 0; a < A; ++a) {
-            ox[a] |= (ax[a] & 0xFFu) << sh;
-            oy[a] |= (ay[a] & 0xFFu) << sh;
-            oh[a] |= (ah[a] & 0xFFu) << sh;
-            oe[a] |= ex[a] << sh;
-        }
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            ol[j] |= (il[j] & 0xFFu) << sh;
-            om[j] |= (im[j] & 0xFFu) << sh;
-        }
-        ot[q >> 1] |= (t & 0xFFFFu) << (16 * (q & 1));
-        of |= fl << sh;
-        oc |= coll << sh;
-        const bool valid = e0 + q < L.B;
-        const bool ended = valid && !was_done && (fl & OC_FLAG_DONE);
-        s_eps += ended;
-        s_succ += ended && (fl & OC_FLAG_SUCCESS);
-        s_steps += ended ? t : 0u;
-        s_err += ended && (fl & OC_FLAG_ERR);
-        s_coll += valid ? __popc(coll) : 0u;
     }
-
-    auto st32 = [&](int plane, uint32_t v) {
-        *reinterpret_cast<uint32_t*>(sout + plane * P + e0) = v;
-    };
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-        st32(kPA + a, ox[a]);
-        st32(kPY + a, oy[a]);
-        st32(kPH + a, oh[a]);
-    }
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        st32(kPL + j, ol[j]);
-        st32(kPM + j, om[j]);
-    }
-    *reinterpret_cast<uint2*>(sout + kPT * P + 2 * e0) = make_uint2(ot[0], ot[1]);
-    st32(kPF, of);
-    if (exec_out != nullptr) {
-#pragma unroll
-        for (int a = 0; a < A; ++a) *reinterpret_cast<uint32_t*>(exec_out + a * P + e0) = oe[a];
-    }
-    if (coll_out != nullptr) *reinterpret_cast<uint32_t*>(coll_out + e0) = oc;
 
     if (stats != nullptr) {
         __shared__ uint32_t red[kBlock / 64][OC_NSTATS];
-        const uint32_t v[OC_NSTATS] = {s_eps, s_succ, s_steps, s_coll, s_err};
+        const uint32_t v[OC_NSTATS] = {st.eps, st.succ, st.steps, st.coll, st.err};
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
         for (int c = 0; c < OC_NSTATS; ++c) {
@@ -355,6 +220,45 @@ __global__ __launch_bounds__(kBlock) void oc_reset_kernel(LevelArgs L, uint8_t* 
     }
     *reinterpret_cast<uint2*>(s + (3 * A + 2 * K) * P + 2 * e0) = make_uint2(0u, 0u);
     st32(3 * A + 2 * K + 2, 0u);
+}
+
+// Order-sensitive 64-bit checksum of the state of envs [0, B):
+//   sum_e (2e + 1) * sum_p (byte_p(e) + 1) * M_p,   M_p = 0x9E3779B97F4A7C15 * (2p + 1)  (mod 2^64)
+// over the byte planes p (the u16 t plane as its low / high byte planes).  It reads the state
+// exactly like oc_step does (one dword per plane per lane), so it doubles as the known-byte
+// read pass that calibrates the FETCH_SIZE counter for this access pattern.
+template <int NP>
+__global__ __launch_bounds__(kBlock) void oc_checksum_kernel(const uint8_t* __restrict__ s, int64_t pitch,
+                                                             int64_t B,
+                                                             unsigned long long* __restrict__ out) {
+    constexpr int plane_t = NP - 3;  // t precedes the flags plane (oc_layout)
+    const uint32_t g = blockIdx.x * (uint32_t)kBlock + threadIdx.x;
+    const int64_t e0 = (int64_t)g * kEPL;
+    uint64_t h[kEPL] = {};
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const uint64_t Mp = 0x9E3779B97F4A7C15ull * (uint64_t)(2 * p + 1);
+        if (p == plane_t) {
+            const uint2 w = reinterpret_cast<const uint2*>(s + p * pitch)[g];
+            const uint64_t Mq = 0x9E3779B97F4A7C15ull * (uint64_t)(2 * p + 3);
+#pragma unroll
+            for (int q = 0; q < kEPL; ++q) {
+                const uint32_t v = ((q < 2 ? w.x : w.y) >> (16 * (q & 1))) & 0xFFFFu;
+                h[q] += (uint64_t)((v & 0xFFu) + 1u) * Mp + (uint64_t)((v >> 8) + 1u) * Mq;
+            }
+        } else if (p != plane_t + 1) {
+            const uint32_t w = reinterpret_cast<const uint32_t*>(s + p * pitch)[g];
+#pragma unroll
+            for (int q = 0; q < kEPL; ++q) h[q] += (uint64_t)(((w >> (8 * q)) & 0xFFu) + 1u) * Mp;
+        }
+    }
+    uint64_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < kEPL; ++q)
+        acc += (e0 + q < B) ? h[q] * (uint64_t)(2 * (e0 + q) + 1) : 0ull;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -410,6 +314,15 @@ int hip_check(const char* what) {
     return OC_OK;
 }
 
+// MI355X: 256 CUs.  The step grid is persistent: min(blocks needed, kCUs * blocks per CU).
+constexpr int kCUs = 256;
+
+int64_t step_grid(int64_t pitch, int blocks_per_cu) {
+    const int64_t need = pitch / kEnvsPerBlock;
+    const int64_t cap = (int64_t)kCUs * blocks_per_cu;
+    return need < cap ? need : cap;
+}
+
 int64_t pitch_for(int64_t B) {
     int64_t p = (B + OC_PITCH_ALIGN - 1) / OC_PITCH_ALIGN * OC_PITCH_ALIGN;
     return p < OC_PITCH_ALIGN ? OC_PITCH_ALIGN : p;
@@ -420,6 +333,7 @@ int64_t pitch_for(int64_t B) {
 struct oc_handle {
     oc_level_desc level;
     int32_t A, K, max_T, device;
+    int32_t blocks_per_cu;  // persistent step grid: blocks per CU (OC_BLOCKS_PER_CU, default 2)
     LevelArgs args;
 };
 
@@ -487,12 +401,20 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     L.max_T = max_T;
     const int dcell[5] = {W, -W, -1, 1, 0};
     for (int c = 0; c < 5; ++c) L.dcell_lut |= (uint64_t)((dcell[c] + 128) & 0xFF) << (8 * c);
+    if (max_T > 0x7FFF) return fail(OC_EINVAL, "max_T %d > 32767", max_T);
+    ocsw::build_swar_level(L.sw, W, H, L.done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y,
+                           num_agents, cell, mask);
     oc_handle* h = new oc_handle;
     h->level = *lv;
     h->A = num_agents;
     h->K = K;
     h->max_T = max_T;
     h->device = device;
+    h->blocks_per_cu = 2;
+    if (const char* e = getenv("OC_BLOCKS_PER_CU")) {  // tuning knob
+        const int v = atoi(e);
+        if (v >= 1 && v <= 16) h->blocks_per_cu = v;
+    }
     h->args = L;
     *out = h;
     return OC_OK;
@@ -558,7 +480,7 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
     LevelArgs L = h->args;
     L.pitch = pitch_for(B);
     L.B = B;
-    const dim3 grid((unsigned)(L.pitch / kEnvsPerBlock));
+    const dim3 grid((unsigned)step_grid(L.pitch, h->blocks_per_cu));
     hipStream_t s = (hipStream_t)stream;
 #define OC_LAUNCH_STEP(A, K)                                                                          \
     hipLaunchKernelGGL((oc_step_kernel<A, K>), grid, dim3(kBlock), 0, s, L, (const uint8_t*)state_in, \
@@ -577,15 +499,38 @@ int oc_gen_actions(const oc_handle* h, uint8_t* actions, int64_t B, int64_t env_
     return hip_check("oc_gen_actions launch");
 }
 
+int oc_state_checksum(const oc_handle* h, const void* state, int64_t B, uint64_t* out, void* stream) {
+    if (h == nullptr || state == nullptr || out == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(out, 0, sizeof(uint64_t), s) != hipSuccess) return hip_check("oc_state_checksum memset");
+    if (B == 0) return OC_OK;
+    const int64_t P = pitch_for(B);
+    const int np = 3 * h->A + 2 * h->K + 3;
+    const dim3 grid((unsigned)(P / kEnvsPerBlock));
+#define OC_CK(NP) hipLaunchKernelGGL((oc_checksum_kernel<NP>), grid, dim3(kBlock), 0, s, (const uint8_t*)state, P, B, (unsigned long long*)out)
+    switch (np) {
+        case 17: OC_CK(17); break;   // A=2 K=4
+        case 14: OC_CK(14); break;   // A=1 K=4
+        case 20: OC_CK(20); break;   // A=3 K=4
+        case 23: OC_CK(23); break;   // A=4 K=4
+        case 22: OC_CK(22); break;   // A=1 K=8
+        case 25: OC_CK(25); break;   // A=2 K=8
+        case 28: OC_CK(28); break;   // A=3 K=8
+        case 31: OC_CK(31); break;   // A=4 K=8
+        default: return fail(OC_EINVAL, "unsupported plane count %d", np);
+    }
+    return hip_check("oc_state_checksum launch");
+}
+
 int oc_stats_size(const oc_handle* h, int64_t B, int64_t* nbytes) {
     if (h == nullptr || nbytes == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
-    *nbytes = (pitch_for(B) / kEnvsPerBlock) * OC_NSTATS * (int64_t)sizeof(uint64_t);
+    *nbytes = step_grid(pitch_for(B), h->blocks_per_cu) * OC_NSTATS * (int64_t)sizeof(uint64_t);
     return OC_OK;
 }
 
 int oc_stats_reduce(const oc_handle* h, const uint64_t* stats, int64_t B, uint64_t* totals, void* stream) {
     if (h == nullptr || stats == nullptr || totals == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
-    const int64_t rows = pitch_for(B) / kEnvsPerBlock;
+    const int64_t rows = step_grid(pitch_for(B), h->blocks_per_cu);
     hipLaunchKernelGGL(oc_stats_reduce_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, stats, rows, totals);
     return hip_check("oc_stats_reduce launch");
 }

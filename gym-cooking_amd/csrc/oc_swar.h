@@ -1,0 +1,316 @@
+// oc_swar.h -- the env step of oc_step_kernel as SWAR over four envs per dword.
+//
+// Every state plane is loaded one dword per lane, i.e. byte q of a plane word belongs to
+// env q of that lane (q = 0..3).  The step runs on those words directly: all per-env
+// predicates are byte masks, computed with carry-free byte arithmetic and v_bitop3 logic,
+// selects are v_bitop3 (m ? a : b), per-env table lookups are v_perm byte selects, and the
+// tile class of a cell comes from a 64-entry LDS table.  Measured on MI355X (tools/
+// valubench.hip): v_add / v_xor / shifts / v_bitop3 issue at ~2.9 cycles per wave-instruction,
+// v_perm / v_bfi / v_bfe / v_cndmask / v_cmp at ~5, so the formulation leans on the former.
+//
+// Mask conventions (per byte lane):
+//   "h80"  : 0x80 where true, 0x00 where false (only bit 7 used)
+//   "full" : 0xFF where true, 0x00 where false (select operand)
+//
+// Semantics restated (reference file:line):
+//   is_collision / check_collisions    gym_cooking/envs/overcooked_environment.py:671-762
+//   interact                           gym_cooking/utils/interact.py:4-89
+//   SimAgent.acquire/release/move_to   gym_cooking/utils/agent.py:408-423
+//   Object predicates, mergeable       gym_cooking/utils/core.py:176-241
+//   copy crash (ERR)                   overcooked_environment.py:289 -> :108-113 -> world.py:417
+//   done / reward                      overcooked_environment.py:316-376
+//
+// The includer provides __device__/__forceinline__ and the __builtin_amdgcn_* intrinsics
+// (the HIP compiler; tests/swar_host/ builds this header on the host for unit tests).
+#pragma once
+
+#include <stdint.h>
+
+#define OC_SW __device__ __forceinline__
+
+namespace ocsw {
+
+constexpr uint32_t k01 = 0x01010101u, k04 = 0x04040404u, k07 = 0x07070707u, k08 = 0x08080808u,
+                   k0F = 0x0F0F0F0Fu, k78 = 0x78787878u, k7F = 0x7F7F7F7Fu, k80 = 0x80808080u,
+                   kFF = 0xFFFFFFFFu;
+constexpr uint32_t kLanes = 0x03020100u;  // v_perm selector: byte q <- byte q
+
+// ---- bitop3 with a truth table built from a boolean function of (a, b, c) ----
+template <class F>
+constexpr uint32_t lut3(F f) {
+    uint32_t r = 0;
+    for (int i = 0; i < 8; ++i) r |= (uint32_t)(f((i >> 2) & 1, (i >> 1) & 1, i & 1) & 1) << i;
+    return r;
+}
+#define OC_LUT(expr) ::ocsw::lut3([](int a, int b, int c) constexpr { (void)a; (void)b; (void)c; return (expr); })
+template <uint32_t IMM>
+OC_SW uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, IMM); }
+
+OC_SW uint32_t sel(uint32_t m, uint32_t a, uint32_t b) { return bop3<OC_LUT(a ? b : c)>(m, a, b); }
+OC_SW uint32_t and3(uint32_t a, uint32_t b, uint32_t c) { return bop3<OC_LUT(a & b & c)>(a, b, c); }
+OC_SW uint32_t or3(uint32_t a, uint32_t b, uint32_t c) { return bop3<OC_LUT(a | b | c)>(a, b, c); }
+OC_SW uint32_t andn(uint32_t a, uint32_t b) { return bop3<OC_LUT(a & !b)>(a, b, 0u); }  // a & ~b
+OC_SW uint32_t perm(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_perm(hi, lo, s); }
+
+// h80 -> full mask: (h >> 7) * 0xFF per byte, carry-free
+OC_SW uint32_t full80(uint32_t h) {
+    const uint32_t s = h >> 7;
+    return (s << 8) - s;
+}
+// bytes <= 0x7F: h80 of (byte != 0) / (byte == 0)
+OC_SW uint32_t nz80(uint32_t x) { return (x + k7F) & k80; }
+OC_SW uint32_t z80(uint32_t x) { return andn(k80, x + k7F); }
+// bytes may have bit 7 set (0xFF sentinels): h80 of (a == b) on the low 7 bits
+OC_SW uint32_t eq80(uint32_t a, uint32_t b) { return z80(bop3<OC_LUT((a ^ b) & c)>(a, b, k7F)); }
+
+// Per-level constants the SWAR step reads (all wave-uniform, kernel-argument resident).
+struct SwarLevel {
+    uint32_t W;              // grid width
+    uint32_t yw_lo, yw_hi;   // v_perm LUT: y -> y*W (y = 0..7)
+    uint32_t dc_lo, dc_hi;   // v_perm LUT: action code -> cell delta + 0x80
+    uint32_t done_rep;       // first Delivery cell, replicated to every byte
+    uint32_t goals_rep[4];   // Deliver goal masks, replicated
+    int32_t ngoals;
+    uint32_t maxT_rep;       // max_T replicated to both u16 halves (0 = no limit)
+    uint32_t tmpl_x[4], tmpl_y[4], tmpl_l[8], tmpl_m[8];  // reset template, replicated
+    int32_t tall;            // H > 8: y*W by multiply instead of the 8-entry LUT
+};
+
+// Host-side construction of the SwarLevel constants (called by oc_create after validation).
+// cell/mask: item slot templates (OC_LOC_DEAD / 0 past the level's items).
+__host__ __device__ inline void build_swar_level(SwarLevel& S, int W, int H, int done_cell, const uint8_t* goal_mask,
+                             int ngoals, int max_T, const uint8_t* spawn_x, const uint8_t* spawn_y,
+                             int num_agents, const uint8_t* cell, const uint8_t* mask) {
+    S = SwarLevel{};
+    S.W = (uint32_t)W;
+    S.tall = H > 8;
+    const int dcell[5] = {W, -W, -1, 1, 0};
+    for (int y = 0; y < 8; ++y) {
+        const uint32_t v = (uint32_t)(y * W) & 0xFFu;
+        if (y < 4) S.yw_lo |= v << (8 * y); else S.yw_hi |= v << (8 * (y - 4));
+    }
+    for (int c = 0; c < 8; ++c) {
+        const uint32_t v = (uint32_t)((c < 5 ? dcell[c] : 0) + 128) & 0xFFu;
+        if (c < 4) S.dc_lo |= v << (8 * c); else S.dc_hi |= v << (8 * (c - 4));
+    }
+    S.done_rep = (uint32_t)done_cell * 0x01010101u;
+    for (int g = 0; g < 4; ++g) S.goals_rep[g] = (uint32_t)(g < ngoals ? goal_mask[g] : 0) * 0x01010101u;
+    S.ngoals = ngoals;
+    S.maxT_rep = (uint32_t)max_T * 0x00010001u;
+    for (int a = 0; a < 4; ++a) {
+        S.tmpl_x[a] = (uint32_t)(a < num_agents ? spawn_x[a] : 0) * 0x01010101u;
+        S.tmpl_y[a] = (uint32_t)(a < num_agents ? spawn_y[a] : 0) * 0x01010101u;
+    }
+    for (int j = 0; j < 8; ++j) {
+        S.tmpl_l[j] = (uint32_t)cell[j] * 0x01010101u;
+        S.tmpl_m[j] = (uint32_t)mask[j] * 0x01010101u;
+    }
+}
+
+// Tile class byte of a cell (the LDS table): 0x80 Floor, 0x40 Delivery, 0x20 Cutboard.
+__host__ __device__ inline uint8_t tile_class(uint64_t floor_mask, uint64_t deliv_mask, uint64_t cut_mask, uint32_t c) {
+    if (c >= 64u) return 0;
+    return (uint8_t)((((floor_mask >> c) & 1u) << 7) | (((deliv_mask >> c) & 1u) << 6) | (((cut_mask >> c) & 1u) << 5));
+}
+
+// dx + 1 / dy + 1 per action code (World.NAV_ACTIONS order, world.py:16, + no-op)
+constexpr uint32_t kDXlo = 0x02000101u, kDXhi = 0x01010101u;  // codes 0..3 | 4..7
+constexpr uint32_t kDYlo = 0x01010002u, kDYhi = 0x01010101u;
+
+// Gather V[idx] per byte lane from K slot words; idx bits given as h80 masks b0, b1, b2.
+template <int K>
+OC_SW uint32_t gather(const uint32_t (&V)[K], uint32_t s, uint32_t f1, uint32_t f2) {
+    // s: v_perm selector picking byte q of the even (bit0 = 0) or odd slot of a pair
+    const uint32_t g01 = perm(V[1], V[0], s), g23 = perm(V[3], V[2], s);
+    const uint32_t lo = sel(f1, g23, g01);
+    if constexpr (K == 4) {
+        (void)f2;
+        return lo;
+    } else {
+        const uint32_t g45 = perm(V[5], V[4], s), g67 = perm(V[7], V[6], s);
+        return sel(f2, sel(f1, g67, g45), lo);
+    }
+}
+
+// One step of 4 envs x A agents x K item slots.  `cls_of(cellword)` returns per byte the
+// tile class bits of that cell: 0x80 Floor, 0x40 Delivery, 0x20 Cutboard.
+template <int A, int K, class ClassOf>
+OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_t (&H)[A],
+                 uint32_t (&Lc)[K], uint32_t (&M)[K], uint32_t& T0, uint32_t& T1, uint32_t& F,
+                 const uint32_t (&ACT)[A], uint32_t (&EX)[A], uint32_t& CM, ClassOf cls_of) {
+    const uint32_t rst = full80((F << 7) & k80);  // input DONE => next-step auto-reset
+
+    // ---- positions, next squares, collidability (is_collision :692-700) ----
+    uint32_t act[A], loc[A], nraw[A], cls[A], nn80[A], bump80[A], nxt[A], blk80[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        uint32_t c = ACT[a];
+        const uint32_t ge5 = bop3<OC_LUT((a | b) & c)>((c & k7F) + 0x7B7B7B7Bu, c, k80);
+        if (ge5 != 0u) c = sel(full80(ge5), k04, c);  // codes > 4 act as (0, 0)
+        act[a] = c;
+        nn80[a] = nz80(c ^ k04);
+        uint32_t yw;
+        if (L.tall)  // wave-uniform: H > 8 rows
+            yw = Y[a] * L.W;
+        else
+            yw = perm(L.yw_hi, L.yw_lo, Y[a]);
+        loc[a] = yw + X[a];
+        nraw[a] = (loc[a] + perm(L.dc_hi, L.dc_lo, c)) ^ k80;  // loc + delta (bias removed)
+        cls[a] = cls_of(nraw[a]);
+        const uint32_t onF80 = cls[a] & k80;
+        nxt[a] = sel(full80(onF80), nraw[a], loc[a]);
+        bump80[a] = andn(nn80[a], onF80);  // a != (0,0) but next square collidable
+        blk80[a] = 0u;
+    }
+
+    // ---- check_collisions (:724-762): pairs in itertools.combinations order ----
+    uint32_t cm = 0u;
+    int p = 0;
+#pragma unroll
+    for (int i = 0; i < A; ++i) {
+#pragma unroll
+        for (int j = i + 1; j < A; ++j, ++p) {
+            const uint32_t eq = z80(nxt[i] ^ nxt[j]);
+            const uint32_t sw = bop3<OC_LUT((!a) & (!b) & c)>((loc[i] ^ nxt[j]) + k7F, (loc[j] ^ nxt[i]) + k7F, k80);
+            const uint32_t bi = bop3<OC_LUT(a ? !b : c)>(eq, bump80[i], sw);
+            const uint32_t u = bop3<OC_LUT((a | !b) & c)>(bump80[i], bump80[j], k80);
+            const uint32_t bj = sel(eq, u, sw);
+            blk80[i] |= bi;
+            blk80[j] |= bj;
+            cm |= (bi | bj) >> (7 - p);
+        }
+    }
+
+    // ---- execute_navigation: interact per agent, in order (:767-770, interact.py:4-89) ----
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+        const uint32_t go80 = andn(nn80[k], blk80[k]);
+        EX[k] = sel(full80(go80), act[k], k04);
+        const uint32_t tc = nraw[k];  // inbounds(loc + a): identity on a non-Floor border
+        const uint32_t isF80 = cls[k] & k80;
+        const uint32_t isD80 = (cls[k] << 1) & k80;
+        const uint32_t isC80 = (cls[k] << 2) & k80;
+        const uint32_t h = H[k];
+        const uint32_t hold80 = andn(k80, h);  // slot index < 0x80, none = 0xFF
+        // un-held items at tc (a non-Delivery cell holds at most one; held items sit on Floor)
+        uint32_t at80[K], seen = 0u, ob0 = 0u, ob1 = 0u, ob2 = 0u;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            at80[j] = eq80(Lc[j], tc);
+            seen |= at80[j];
+            if (j & 1) ob0 |= at80[j];
+            if (j & 2) ob1 |= at80[j];
+            if (j & 4) ob2 |= at80[j];
+        }
+        const uint32_t fo1 = full80(ob1), fo2 = (K == 8) ? full80(ob2) : 0u;
+        const uint32_t om = gather<K>(M, (ob0 >> 5) | kLanes, fo1, fo2);
+        const uint32_t sh = bop3<OC_LUT((a & b) | c)>(h << 2, k04, kLanes);  // (h & 1) * 4 + q
+        const uint32_t fh1 = full80((h << 6) & k80), fh2 = (K == 8) ? full80((h << 5) & k80) : 0u;
+        const uint32_t hm = gather<K>(M, sh, fh1, fh2);
+        const uint32_t hl = gather<K>(Lc, sh, fh1, fh2);
+
+        const uint32_t nf = andn(go80, isF80), mv = go80 & isF80;
+        // Object.is_deliverable (core.py:214-219): >= 2 contents, all foods chopped
+        const uint32_t c4 = hm & k0F;
+        const uint32_t two = nz80(((c4 | k80) - k01) & c4);
+        const uint32_t allch = z80(bop3<OC_LUT((!a) & b & c)>(hm >> 4, hm, k07));
+        // mergeable (core.py:222-241): <= 1 plate, every food chopped
+        const uint32_t cu = hm | om;
+        const uint32_t plate_ok = z80(and3(hm, om, k08));
+        const uint32_t food_ok = z80(bop3<OC_LUT((!a) & b & c)>(cu >> 4, cu, k07));
+        // Object.needs_chopped (core.py:176-178): exactly one content, a fresh food
+        const uint32_t nch = bop3<OC_LUT(a & !b & c)>(nz80(c4), two, z80(hm & k78));
+        const uint32_t nfh = nf & hold80;
+        const uint32_t deliver = and3(nfh & isD80, two, allch);                  // :35-40
+        const uint32_t cnt = andn(nfh, isD80);
+        const uint32_t merge = and3(cnt, seen, plate_ok & food_ok);              // :43-56
+        const uint32_t empty = andn(cnt, seen);                                  // :60-70
+        const uint32_t chop = and3(empty, isC80, nch);
+        const uint32_t put = andn(empty, chop);
+        const uint32_t pick = andn(bop3<OC_LUT(a & !b & c)>(nf, hold80, seen), isD80);  // :73-84
+        const uint32_t reloc = or3(mv, deliver, put);  // the held item ends on tc
+
+        // SimAgent.move_to (agent.py:420-423)
+        const uint32_t fmv = full80(mv);
+        X[k] = sel(fmv, X[k] + perm(kDXhi, kDXlo, act[k]) - k01, X[k]);
+        Y[k] = sel(fmv, Y[k] + perm(kDYhi, kDYlo, act[k]) - k01, Y[k]);
+        // new values of the target slot o and the held slot h
+        const uint32_t fmg = full80(merge), fpk = full80(pick);
+        const uint32_t newOl = fmg | sel(fpk, loc[k], tc);  // merged away: dead (0xFF)
+        const uint32_t newOm = andn(om, fmg);
+        const uint32_t newHl = sel(full80(reloc), tc, hl);
+        // Object.chop (core.py:187-192): the single food's chopped bit (bits 4..6, no cross-byte spill)
+        const uint32_t chopped = bop3<OC_LUT((a & b) | c)>(hm << 4, 0x70707070u, hm);
+        const uint32_t newHm = sel(fmg, cu, sel(full80(chop), chopped, hm));
+        // scatter: target slot on merge / pick, held slot on reloc / merge / chop
+        const uint32_t wo = merge | pick;
+        const uint32_t oh = perm(0x80402010u, 0x08040201u, h);  // 1 << h per byte (h < 8)
+        const uint32_t wh01 = (and3(hold80, or3(reloc, merge, chop), k80)) >> 7;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const uint32_t eo = full80(at80[j] & wo);
+            const uint32_t eh01 = and3(oh >> j, wh01, k01);
+            const uint32_t eh = (eh01 << 8) - eh01;
+            Lc[j] = sel(eh, newHl, sel(eo, newOl, Lc[j]));
+            M[j] = sel(eh, newHm, sel(eo, newOm, M[j]));
+        }
+        // holding: released on deliver / put down, the target slot on pick-up
+        const uint32_t oidx = (ob0 >> 7) | (ob1 >> 6) | (ob2 >> 5);
+        H[k] = sel(full80(deliver | put), kFF, sel(fpk, oidx, h));
+    }
+
+    // ---- new_obs = copy.copy(self) raises: two co-located agents both holding (ERR) ----
+    uint32_t err = 0u;
+#pragma unroll
+    for (int i = 0; i < A; ++i)
+#pragma unroll
+        for (int j = i + 1; j < A; ++j) {
+            const uint32_t same = z80(bop3<OC_LUT((a ^ b) | c)>(X[i], X[j], Y[i] ^ Y[j]));
+            err |= and3(same, andn(k80, H[i]), andn(k80, H[j]));
+        }
+
+    // ---- done() (:316-363) and reward() (:365-376) ----
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 one = {1, 1};
+    u16x2 t0 = __builtin_bit_cast(u16x2, T0) + one, t1 = __builtin_bit_cast(u16x2, T1) + one;
+    uint32_t tout = 0u;
+    if (L.maxT_rep != 0u) {  // t >= max_T first (:328-332): sat(max_T - t) == 0
+        const u16x2 mt = __builtin_bit_cast(u16x2, L.maxT_rep);
+        const uint32_t d0 = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(mt, t0));
+        const uint32_t d1 = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(mt, t1));
+        const uint32_t z0 = andn(0x80008000u, ((d0 & 0x7FFF7FFFu) + 0x7FFF7FFFu) | d0);
+        const uint32_t z1 = andn(0x80008000u, ((d1 & 0x7FFF7FFFu) + 0x7FFF7FFFu) | d1);
+        tout = perm(z1, z0, 0x07050301u);  // high byte of each u16 half -> env byte
+    }
+    uint32_t ok = k80;
+    for (int g = 0; g < L.ngoals; ++g) {  // every Deliver goal: an item == goal at the delivery cell
+        uint32_t hit = 0u;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            hit |= z80(bop3<OC_LUT((a | b) & c)>(Lc[j] ^ L.done_rep, M[j] ^ L.goals_rep[g], k7F));
+        ok &= hit;
+    }
+    const uint32_t done80 = or3(err, tout, ok);
+    const uint32_t succ80 = bop3<OC_LUT(a & !b & !c)>(ok, err, tout);
+    uint32_t fl = or3(done80 >> 7, succ80 >> 6, err >> 5);
+
+    // ---- auto-reset of envs that were done at the input: the level template ----
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        X[a] = sel(rst, L.tmpl_x[a], X[a]);
+        Y[a] = sel(rst, L.tmpl_y[a], Y[a]);
+        H[a] = H[a] | rst;
+        EX[a] = sel(rst, k04, EX[a]);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        Lc[j] = sel(rst, L.tmpl_l[j], Lc[j]);
+        M[j] = sel(rst, L.tmpl_m[j], M[j]);
+    }
+    T0 = andn(__builtin_bit_cast(uint32_t, t0), perm(rst, rst, 0x01010000u));
+    T1 = andn(__builtin_bit_cast(uint32_t, t1), perm(rst, rst, 0x03030202u));
+    F = andn(fl, rst);
+    CM = andn(cm, rst);
+}
+
+}  // namespace ocsw

@@ -122,9 +122,16 @@ class OvercookedBatch:
         capi.check(self.lib.oc_gen_actions(self._h, _ptr(actions), self.B, env_offset, step, seed, self._stream()))
         return actions
 
+    def checksum(self, state: torch.Tensor) -> torch.Tensor:
+        """[1] int64 device checksum of envs [0, B) (include/oc_engine.h oc_state_checksum)."""
+        self._check(state, self.layout.state_bytes)
+        out = torch.empty(1, dtype=torch.int64, device=self.device)
+        capi.check(self.lib.oc_state_checksum(self._h, _ptr(state), self.B, _ptr(out), self._stream()))
+        return out
+
     def reduce_stats(self, stats: torch.Tensor) -> torch.Tensor:
         """[OC_NSTATS] uint64 device totals of a partial-stats buffer."""
-        out = torch.empty(capi.OC_NSTATS, dtype=torch.uint64, device=self.device)
+        out = torch.empty(capi.OC_NSTATS, dtype=torch.int64, device=self.device)  # u64 sums < 2^63
         capi.check(self.lib.oc_stats_reduce(self._h, _ptr(stats), self.B, _ptr(out), self._stream()))
         return out
 

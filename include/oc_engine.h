@@ -154,6 +154,12 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
 int oc_gen_actions(const oc_handle* h, uint8_t* actions, int64_t B, int64_t env_offset,
                    int64_t step, uint64_t seed, void* stream);
 
+/* Order-sensitive 64-bit checksum of the state of envs [0, B) into *out (device uint64):
+ *   sum_e (2e+1) * sum_p (byte_p(e) + 1) * 0x9E3779B97F4A7C15 * (2p+1)   (mod 2^64),
+ * p over the byte planes (t as its low/high byte).  A size-independent parity probe for full
+ * batches (compare with a host computation without copying the batch back). */
+int oc_state_checksum(const oc_handle* h, const void* state, int64_t B, uint64_t* out, void* stream);
+
 /* Statistics: size of the partial buffer for B envs, and its reduction into OC_NSTATS
  * device uint64 totals. */
 int oc_stats_size(const oc_handle* h, int64_t B, int64_t* nbytes);

@@ -29,6 +29,28 @@ def planes_view(state: np.ndarray, A: int, K: int, pitch: int) -> Dict[str, np.n
     )
 
 
+def env_view(state: np.ndarray, A: int, K: int, pitch: int, B: int) -> np.ndarray:
+    """All state bytes of envs [0, B) as a [num_planes, B] array (the u16 t plane split into
+    its low/high bytes), independent of the pitch."""
+    P = capi.layout_planes(A, K)
+    s = state.reshape(P["num_planes"], pitch)
+    t = s[P["t"]:P["t"] + 2].reshape(-1).view(np.uint16)[:B]
+    rows = [s[:P["t"], :B], (t & 0xFF).astype(np.uint8)[None], (t >> 8).astype(np.uint8)[None],
+            s[P["flags"]:P["flags"] + 1, :B]]
+    return np.concatenate(rows, 0)
+
+
+def checksum(state: np.ndarray, A: int, K: int, pitch: int, B: int) -> int:
+    """Host twin of oc_state_checksum (include/oc_engine.h)."""
+    ev = env_view(state, A, K, pitch, B).astype(np.uint64)           # [planes, B]
+    p = np.arange(ev.shape[0], dtype=np.uint64)
+    M = np.uint64(0x9E3779B97F4A7C15) * (np.uint64(2) * p + np.uint64(1))
+    with np.errstate(over="ignore"):
+        h = ((ev + np.uint64(1)) * M[:, None]).sum(axis=0, dtype=np.uint64)
+        w = np.uint64(2) * np.arange(B, dtype=np.uint64) + np.uint64(1)
+        return int((h * w).sum(dtype=np.uint64))
+
+
 def canonical(state: np.ndarray, A: int, K: int, pitch: int, width: int, B: int):
     """SURVEY App. A.7 canonical form of the first B envs: t, flags, agents [B,4,3]
     (x, y, held mask), items [B,K,4] sorted (mask, x, y, held), PAD rows last."""

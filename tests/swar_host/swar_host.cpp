@@ -1,0 +1,83 @@
+// TEST INFRASTRUCTURE: host build of the device SWAR step (gym-cooking_amd/csrc/oc_swar.h)
+// so its logic can be checked against the CPU oracle without a GPU.  The two AMDGCN
+// intrinsics it uses are emulated bit-exactly below (v_perm_b32, v_bitop3_b32 semantics);
+// the product library never contains this file.
+#include <stdint.h>
+#include <string.h>
+
+static inline uint32_t host_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    const uint64_t src = ((uint64_t)hi << 32) | lo;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t s = (sel >> (8 * i)) & 0xFFu;
+        uint32_t b;
+        if (s < 8) b = (uint32_t)(src >> (8 * s)) & 0xFFu;
+        else if (s < 12) b = ((src >> (16 * (s - 8) + 15)) & 1u) ? 0xFFu : 0u;  // sign of a 16-bit half
+        else if (s == 12) b = 0u;
+        else b = 0xFFu;
+        r |= b << (8 * i);
+    }
+    return r;
+}
+static inline uint32_t host_bitop3(uint32_t a, uint32_t b, uint32_t c, uint32_t imm) {
+    uint32_t r = 0;
+    for (int i = 0; i < 8; ++i)
+        if (imm & (1u << i)) r |= ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
+    return r;
+}
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __builtin_amdgcn_perm host_perm
+#define __builtin_amdgcn_bitop3_b32 host_bitop3
+
+#include "../../gym-cooking_amd/csrc/oc_swar.h"
+#include "../../include/oc_engine.h"
+
+template <int A, int K>
+static void run(const oc_level_desc* lv, int max_T, const uint8_t* sin, uint8_t* sout, const uint8_t* act,
+                uint8_t* exo, uint8_t* coll, int64_t B, int64_t P) {
+    const int W = lv->width, H = lv->height;
+    uint64_t fm = 0, dm = 0, cmk = 0;
+    int done_cell = -1;
+    for (int c = 0; c < W * H; ++c) {
+        if (lv->tiles[c] == OC_TILE_FLOOR) fm |= 1ull << c;
+        if (lv->tiles[c] == OC_TILE_CUTBOARD) cmk |= 1ull << c;
+        if (lv->tiles[c] == OC_TILE_DELIVERY) { dm |= 1ull << c; if (done_cell < 0) done_cell = c; }
+    }
+    uint8_t cell[8], mask[8];
+    for (int j = 0; j < 8; ++j) { cell[j] = j < lv->num_items ? lv->item_cell[j] : 0xFF; mask[j] = j < lv->num_items ? lv->item_mask[j] : 0; }
+    ocsw::SwarLevel S;
+    ocsw::build_swar_level(S, W, H, done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y, A, cell, mask);
+    uint8_t tbl[256];
+    for (int c = 0; c < 256; ++c) tbl[c] = ocsw::tile_class(fm, dm, cmk, (uint32_t)c);
+    auto cls_of = [&](uint32_t cells) -> uint32_t {
+        return (uint32_t)tbl[cells & 0xFF] | ((uint32_t)tbl[(cells >> 8) & 0xFF] << 8) |
+               ((uint32_t)tbl[(cells >> 16) & 0xFF] << 16) | ((uint32_t)tbl[cells >> 24] << 24);
+    };
+    auto rd = [&](const uint8_t* base, int plane, int64_t g) { uint32_t v; memcpy(&v, base + plane * P + 4 * g, 4); return v; };
+    auto wr = [&](uint8_t* base, int plane, int64_t g, uint32_t v) { memcpy(base + plane * P + 4 * g, &v, 4); };
+    for (int64_t g = 0; g < (B + 3) / 4; ++g) {
+        uint32_t X[A], Y[A], Hh[A], Lc[K], M[K], AC[A], EX[A], T0, T1, F, CM;
+        for (int a = 0; a < A; ++a) { X[a] = rd(sin, a, g); Y[a] = rd(sin, A + a, g); Hh[a] = rd(sin, 2 * A + a, g); AC[a] = rd(act, a, g); }
+        for (int j = 0; j < K; ++j) { Lc[j] = rd(sin, 3 * A + j, g); M[j] = rd(sin, 3 * A + K + j, g); }
+        const int pt = 3 * A + 2 * K;
+        memcpy(&T0, sin + pt * P + 8 * g, 4);
+        memcpy(&T1, sin + pt * P + 8 * g + 4, 4);
+        F = rd(sin, pt + 2, g);
+        ocsw::step4<A, K>(S, X, Y, Hh, Lc, M, T0, T1, F, AC, EX, CM, cls_of);
+        for (int a = 0; a < A; ++a) { wr(sout, a, g, X[a]); wr(sout, A + a, g, Y[a]); wr(sout, 2 * A + a, g, Hh[a]); if (exo) wr(exo, a, g, EX[a]); }
+        for (int j = 0; j < K; ++j) { wr(sout, 3 * A + j, g, Lc[j]); wr(sout, 3 * A + K + j, g, M[j]); }
+        memcpy(sout + pt * P + 8 * g, &T0, 4);
+        memcpy(sout + pt * P + 8 * g + 4, &T1, 4);
+        wr(sout, pt + 2, g, F);
+        if (coll) memcpy(coll + 4 * g, &CM, 4);
+    }
+}
+
+extern "C" int swar_host_step(const oc_level_desc* lv, int A, int K, int max_T, const uint8_t* sin, uint8_t* sout,
+                              const uint8_t* act, uint8_t* exo, uint8_t* coll, int64_t B, int64_t P) {
+#define R(a, k) if (A == a && K == k) { run<a, k>(lv, max_T, sin, sout, act, exo, coll, B, P); return 0; }
+    R(1, 4) R(2, 4) R(3, 4) R(4, 4) R(1, 8) R(2, 8) R(3, 8) R(4, 8)
+    return -1;
+}

@@ -79,11 +79,11 @@ def _run_parity(level, A, B, steps, seed, max_T=100, check_every=1, nthreads=8):
         s_cpu, nxt_cpu = nxt_cpu, s_cpu
         v = tl.planes_view(s_cpu, A, ob.K, P)
         ended = ((fl_in & 1) == 0) & ((v["fl"][:B] & 1) == 1)
-        totals += [ended.sum(), (ended & ((v["fl"][:B] & 2) == 2)).sum(), v["t"][:B][ended].astype(np.int64).sum(),
-                   np.unpackbits(coll_cpu[:B]).sum(), (ended & ((v["fl"][:B] & 4) == 4)).sum()]
+        totals += np.array([ended.sum(), (ended & ((v["fl"][:B] & 2) == 2)).sum(), v["t"][:B][ended].astype(np.int64).sum(),
+                   np.unpackbits(coll_cpu[:B]).sum(), (ended & ((v["fl"][:B] & 4) == 4)).sum()], dtype=np.int64)
         if t % check_every == 0 or t == steps - 1:
-            g = s_gpu.cpu().numpy().reshape(-1, P)[:, :B]
-            c = s_cpu.reshape(-1, P)[:, :B]
+            g = tl.env_view(s_gpu.cpu().numpy(), A, ob.K, P, B)
+            c = tl.env_view(s_cpu, A, ob.K, P, B)
             if not np.array_equal(g, c):
                 bad = np.argwhere(g != c)
                 raise AssertionError("state mismatch at step %d: %d bytes differ, first (plane, env) %s"
@@ -172,3 +172,41 @@ def test_sharded_ids_match_single_batch(dev):
     ph = half.planes(sh)
     for k in pf:
         assert torch.equal(pf[k][..., 4096:8192], ph[k][..., :4096]), k
+
+
+def test_checksum_matches_host(dev):
+    eb = _batch("full-divider_tl", 3, 10000)
+    s, s2 = eb.new_state(), eb.new_state()
+    eb.reset(s)
+    act = eb.new_actions()
+    for t in range(37):
+        eb.gen_actions(act, t, 5)
+        eb.step(s, s2, act)
+        s, s2 = s2, s
+    host = s.cpu().numpy()
+    got = int(eb.checksum(s).item()) & (2**64 - 1)
+    assert got == tl.checksum(host, eb.A, eb.K, eb.pitch, eb.B)
+
+
+def test_metric_config_full_batch_parity(dev):
+    """BASELINE metric config (partial-divider_salad, 2 agents, B = 2^20) at full size:
+    GPU vs 16-thread oracle, checksum every 10 steps over 230 steps (two auto-resets),
+    then the complete state buffer bit-exact."""
+    B, A, seed = 1 << 20, 2, 77
+    eb = _batch("partial-divider_salad", A, B)
+    ob = oracle.OracleBatch(eb.level, A, 100, B)
+    s, s2 = eb.new_state(), eb.new_state()
+    eb.reset(s)
+    c, c2 = ob.new_state(), ob.new_state()
+    ob.reset(c)
+    act, cact = eb.new_actions(), ob.new_actions()
+    for t in range(230):
+        eb.gen_actions(act, t, seed)
+        ob.gen_actions(cact, 0, t, seed)
+        eb.step(s, s2, act)
+        ob.step(c, c2, cact, nthreads=16)
+        s, s2, c, c2 = s2, s, c2, c
+        if t % 10 == 9:
+            got = int(eb.checksum(s).item()) & (2**64 - 1)
+            assert got == tl.checksum(c, A, ob.K, ob.pitch, B), "checksum mismatch at step %d" % t
+    assert np.array_equal(s.cpu().numpy(), c)

@@ -1,0 +1,115 @@
+"""CPU check of the device SWAR step logic (gym-cooking_amd/csrc/oc_swar.h), compiled for the
+host by tests/swar_host/ with the two AMDGCN intrinsics emulated bit-exactly: replays the
+reference fixtures and random streams against the CPU oracle.  Catches logic errors in the
+kernel's step without a GPU; the GPU tests then check the real device build."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oc_testlib as tl
+from gym_cooking_amd import capi, levels
+
+from oracle import oracle
+
+HERE = os.path.join(tl.ROOT, "tests", "swar_host")
+LIB = os.path.join(HERE, "_build", "libswar_host.so")
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists("/opt/rocm/llvm/bin/clang++"):
+            pytest.skip("no clang++ for the host SWAR harness")
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+        L = ctypes.CDLL(LIB)
+        vp = ctypes.c_void_p
+        L.swar_host_step.restype = ctypes.c_int
+        L.swar_host_step.argtypes = [ctypes.POINTER(capi.OcLevelDesc), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     vp, vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int64]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+class SwarHostBatch(oracle.OracleBatch):
+    def step(self, sin, sout, actions, exec_out=None, coll=None, nthreads=1):
+        rc = _load().swar_host_step(ctypes.byref(self.desc), self.A, self.K, self.max_T, _p(sin), _p(sout),
+                                    _p(actions), _p(exec_out), _p(coll), self.B, self.pitch)
+        assert rc == 0
+
+
+def _step_fn(sb):
+    def fn(state, acts):
+        a = sb.new_actions()
+        a.reshape(sb.A, sb.pitch)[:, :sb.B] = acts
+        out = sb.new_state()
+        ex = np.zeros(sb.A * sb.pitch, np.uint8)
+        coll = np.zeros(sb.pitch, np.uint8)
+        sb.step(state, out, a, ex, coll)
+        return out, ex.reshape(sb.A, sb.pitch)[:, :sb.B], coll[:sb.B]
+    return fn
+
+
+@pytest.mark.parametrize("fixture", ["kat.npz", "streams.npz"])
+def test_swar_step_matches_reference_fixtures(fixture):
+    _load()
+    fx = tl.load_fixture(fixture)
+    for g in tl.episode_groups(fx):
+        sb = SwarHostBatch(g.level, g.A, g.max_T, g.B)
+        s = sb.new_state()
+        sb.reset(s)
+        g.relocate(s, sb.pitch)
+        errs = tl.compare_group(g, _step_fn(sb), s, sb.pitch, g.level.width)
+        assert not errs, "\n".join(errs[:10])
+
+
+@pytest.mark.parametrize("level", sorted(levels.BUILTIN_LEVELS))
+@pytest.mark.parametrize("A", [1, 2, 3, 4])
+def test_swar_step_matches_oracle_random(level, A):
+    _load()
+    B, steps, max_T = 1003, 130, 60
+    lv = levels.load_level(level)
+    ob = oracle.OracleBatch(lv, A, max_T, B)
+    sb = SwarHostBatch(lv, A, max_T, B)
+    s1, s2, n1, n2 = ob.new_state(), sb.new_state(), ob.new_state(), sb.new_state()
+    ob.reset(s1)
+    sb.reset(s2)
+    act = ob.new_actions()
+    e1, e2 = np.zeros(A * ob.pitch, np.uint8), np.zeros(A * ob.pitch, np.uint8)
+    c1, c2 = np.zeros(ob.pitch, np.uint8), np.zeros(ob.pitch, np.uint8)
+    for t in range(steps):
+        ob.gen_actions(act, 0, t, A * 131 + t % 3)
+        ob.step(s1, n1, act, e1, c1)
+        sb.step(s2, n2, act, e2, c2)
+        s1, n1, s2, n2 = n1, s1, n2, s2
+        v1, v2 = tl.env_view(s1, A, ob.K, ob.pitch, B), tl.env_view(s2, A, ob.K, ob.pitch, B)
+        if not np.array_equal(v1, v2):
+            bad = np.argwhere(v1 != v2)
+            raise AssertionError("step %d: %d bytes differ, first (plane, env) %s" % (t, len(bad), bad[:5].tolist()))
+        assert np.array_equal(e1.reshape(A, -1)[:, :B], e2.reshape(A, -1)[:, :B]), t
+        assert np.array_equal(c1[:B], c2[:B]), t
+
+
+def test_swar_invalid_action_codes():
+    _load()
+    lv = levels.load_level("open-divider_salad")
+    B = 512
+    ob = oracle.OracleBatch(lv, 2, 100, B)
+    sb = SwarHostBatch(lv, 2, 100, B)
+    s = ob.new_state()
+    ob.reset(s)
+    rng = np.random.default_rng(0)
+    for t in range(20):
+        act = rng.integers(0, 256, 2 * ob.pitch).astype(np.uint8)
+        o1, o2 = ob.new_state(), sb.new_state()
+        ob.step(s, o1, act)
+        sb.step(s, o2, act)
+        assert np.array_equal(tl.env_view(o1, 2, 4, ob.pitch, B), tl.env_view(o2, 2, 4, ob.pitch, B))
+        s = o1

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Workload for rocprofv3 --pmc passes (run under the profiler, one counter group per pass).
+
+Dispatches, on the bench workload (partial-divider_salad, 2 agents, 2^20 envs):
+  oc_reset_kernel     x3  -- writes exactly state_bytes with dword stores (WRITE_SIZE calibration)
+  oc_checksum_kernel  x3  -- reads exactly 17 planes x B bytes with oc_step's dword pattern
+                             (FETCH_SIZE calibration for this access width)
+  oc_step_kernel      x20 -- the measured kernel (eager launches)
+tools/pmc_report.py turns the counter CSVs into profiles/pmc_traffic.json.
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gym-cooking_amd"))
+
+import torch  # noqa: E402
+
+from gym_cooking_amd.engine import OvercookedBatch  # noqa: E402
+
+B = 1 << 20
+eb = OvercookedBatch("partial-divider_salad", 2, B, max_T=100, device="cuda:0")
+a, b = eb.new_state(), eb.new_state()
+acts = torch.empty((20, eb.A * eb.pitch), dtype=torch.uint8, device="cuda:0")
+for i in range(20):
+    eb.gen_actions(acts[i], step=i, seed=0)
+exe, coll, stats = eb.new_exec(), eb.new_coll(), eb.new_stats()
+for _ in range(3):
+    eb.reset(a)
+for _ in range(3):
+    eb.checksum(a)
+for i in range(20):
+    eb.step(a, b, acts[i], exe, coll, stats)
+    a, b = b, a
+torch.cuda.synchronize()
+print("pmc probe done")
