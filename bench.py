@@ -63,6 +63,38 @@ def cpu_baseline(level_name: str, A: int, B: int, max_T: int, budget_s: float, t
                       % (B, steps, level_name, A, threads)}
 
 
+def measure_fused(eb, acts, n, dev, world) -> dict:
+    """Secondary line: the same n steps as ONE oc_step_n call (state kept in registers between
+    steps), still writing every step's full state (trajectory), executed actions and collision
+    mask.  Algorithmic bytes per env-step: S/n (state in) + S (trajectory) + A (actions in) +
+    A (exec) + 1 (coll)."""
+    P, S, A = eb.pitch, eb.layout.state_bytes, eb.A
+    s0, out = eb.new_state(), eb.new_state()
+    eb.reset(s0)
+    traj = torch.empty(n * S, dtype=torch.uint8, device=dev)
+    ex = torch.empty(n * A * P, dtype=torch.uint8, device=dev)
+    coll = torch.empty(n * P, dtype=torch.uint8, device=dev)
+    stats = eb.new_stats()
+    flat = acts.reshape(-1)
+    eb.step_n(s0, out, flat, n, traj, ex, coll, stats)  # warm
+    torch.cuda.synchronize()
+    ocdist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    eb.step_n(s0, out, flat, n, traj, ex, coll, stats)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) * 1e-3, dev) * 1e3
+    nS = eb.layout.num_planes  # bytes per env of state = planes (t counts 2)
+    bytes_env_step = nS / n + nS + 2 * A + 1
+    gbs = bytes_env_step * eb.B * n / (ms * 1e-3) / 1e9
+    del traj, ex, coll
+    return {"value": world * eb.B * n / (ms * 1e-3), "unit": "env-steps/s", "steps": n, "ms_per_step": ms / n,
+            "kernel": "oc_step_n_kernel<%d,%d>" % (A, eb.K), "algorithmic_bytes_per_env_step": bytes_env_step,
+            "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS,
+            "outputs": "every step's state (trajectory), executed actions and collision mask written"}
+
+
 def load_traffic(path: str):
     try:
         with open(path) as f:
@@ -85,6 +117,7 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fused", action="store_true", help="skip the secondary oc_step_n measurement")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -206,6 +239,8 @@ def main() -> int:
         "gpu_ms_timed_region": gpu_ms,
         "episodes": summary,
     }
+    if not args.no_fused:
+        line["fused_multi_step"] = measure_fused(eb, acts, n_act, dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget, threads)

@@ -66,36 +66,54 @@ struct Chunk {
     uint32_t wf;
 };
 
+// Buffer resources of one launch: every plane access is a buffer load/store with the lane's
+// 32-bit byte offset in a VGPR and the plane offset (plane * pitch) in an SGPR, so no per-
+// access 64-bit address arithmetic is spent on the VALU.
+struct Bufs {
+    __amdgpu_buffer_rsrc_t sin, sout, act, ex, coll;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t bld32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ void bst32(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, 0);
+}
+
 template <int A, int K>
-__device__ __forceinline__ void load_chunk(Chunk<A, K>& c, const uint8_t* __restrict__ sin,
-                                           const uint8_t* __restrict__ actions, int64_t P, uint32_t g) {
+__device__ __forceinline__ void load_chunk(Chunk<A, K>& c, const Bufs& b, uint32_t P, uint32_t g) {
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
-    auto ld32 = [&](int plane) -> uint32_t { return reinterpret_cast<const uint32_t*>(sin + plane * P)[g]; };
+    const uint32_t vo = g * 4u;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-        c.wx[a] = ld32(a);
-        c.wy[a] = ld32(kPY + a);
-        c.wh[a] = ld32(kPH + a);
-        c.wa[a] = reinterpret_cast<const uint32_t*>(actions + a * P)[g];
+        c.wx[a] = bld32(b.sin, vo, a * P);
+        c.wy[a] = bld32(b.sin, vo, (kPY + a) * P);
+        c.wh[a] = bld32(b.sin, vo, (kPH + a) * P);
+        c.wa[a] = bld32(b.act, vo, a * P);
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        c.wl[j] = ld32(kPL + j);
-        c.wm[j] = ld32(kPM + j);
+        c.wl[j] = bld32(b.sin, vo, (kPL + j) * P);
+        c.wm[j] = bld32(b.sin, vo, (kPM + j) * P);
     }
-    c.wt = reinterpret_cast<const uint2*>(sin + kPT * P)[g];
-    c.wf = ld32(kPF);
+    const auto t = __builtin_amdgcn_raw_buffer_load_b64(b.sin, (int)(g * 8u), (int)(kPT * P), 0);
+    c.wt = make_uint2(t[0], t[1]);
+    c.wf = bld32(b.sin, vo, kPF * P);
 }
 
+// Per-lane episode counters; at the end of the kernel a wave sums them and lane 0 adds them
+// to the block's stats row with no-return 64-bit atomics.
 struct StepStats {
-    uint32_t eps = 0u, succ = 0u, steps = 0u, coll = 0u, err = 0u;
+    uint32_t eps = 0u, succ = 0u, err = 0u, coll = 0u, steps = 0u;
 };
 
 // Step the kEPL envs of chunk c (SWAR, oc_swar.h) and store every output plane word of lane g.
 template <int A, int K>
-__device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tbl, Chunk<A, K>& c,
-                                           uint8_t* __restrict__ sout, uint8_t* __restrict__ exec_out,
-                                           uint8_t* __restrict__ coll_out, int64_t P, uint32_t g, StepStats& st) {
+__device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tbl, Chunk<A, K>& c, const Bufs& b,
+                                           bool has_ex, bool has_coll, uint32_t P, uint32_t g, StepStats& st) {
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
     auto cls_of = [tbl](uint32_t cells) -> uint32_t {
         const uint32_t b0 = tbl[cells & 0xFFu], b1 = tbl[(cells >> 8) & 0xFFu], b2 = tbl[(cells >> 16) & 0xFFu],
@@ -114,30 +132,33 @@ __device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tb
     st.succ += __popc(c.wf & (ended << 1));
     st.err += __popc(c.wf & (ended << 2));
     st.coll += __popc(cm & vmask);
-    const uint32_t e16a = __builtin_amdgcn_perm(0u, ended * 0xFFu, 0x01010000u);  // env 0,1 -> u16 masks
-    const uint32_t e16b = __builtin_amdgcn_perm(0u, ended * 0xFFu, 0x03030202u);  // env 2,3
+    const uint32_t efull = ocsw::full80(ended << 7);
+    const uint32_t e16a = __builtin_amdgcn_perm(0u, efull, 0x01010000u);  // env 0,1 -> u16 masks
+    const uint32_t e16b = __builtin_amdgcn_perm(0u, efull, 0x03030202u);  // env 2,3
     const uint32_t sa = T0 & e16a, sb = T1 & e16b;
     st.steps += (sa & 0xFFFFu) + (sa >> 16) + (sb & 0xFFFFu) + (sb >> 16);
 
-    auto st32 = [&](int plane, uint32_t v) { reinterpret_cast<uint32_t*>(sout + plane * P)[g] = v; };
+    const uint32_t vo = g * 4u;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-        st32(a, c.wx[a]);
-        st32(kPY + a, c.wy[a]);
-        st32(kPH + a, c.wh[a]);
+        bst32(b.sout, c.wx[a], vo, a * P);
+        bst32(b.sout, c.wy[a], vo, (kPY + a) * P);
+        bst32(b.sout, c.wh[a], vo, (kPH + a) * P);
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        st32(kPL + j, c.wl[j]);
-        st32(kPM + j, c.wm[j]);
+        bst32(b.sout, c.wl[j], vo, (kPL + j) * P);
+        bst32(b.sout, c.wm[j], vo, (kPM + j) * P);
     }
-    reinterpret_cast<uint2*>(sout + kPT * P)[g] = make_uint2(T0, T1);
-    st32(kPF, c.wf);
-    if (exec_out != nullptr) {
+    typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+    const u32x2 tw = {T0, T1};
+    __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)(g * 8u), (int)(kPT * P), 0);
+    bst32(b.sout, c.wf, vo, kPF * P);
+    if (has_ex) {
 #pragma unroll
-        for (int a = 0; a < A; ++a) reinterpret_cast<uint32_t*>(exec_out + a * P)[g] = ex[a];
+        for (int a = 0; a < A; ++a) bst32(b.ex, ex[a], vo, a * P);
     }
-    if (coll_out != nullptr) reinterpret_cast<uint32_t*>(coll_out)[g] = cm;
+    if (has_coll) bst32(b.coll, cm, vo, 0u);
 }
 
 // Persistent, software-pipelined step: a grid of a few blocks per CU walks the batch in
@@ -152,8 +173,16 @@ __global__ __launch_bounds__(kBlock) void oc_step_kernel(LevelArgs L, const uint
                                                          uint8_t* __restrict__ exec_out,
                                                          uint8_t* __restrict__ coll_out,
                                                          uint64_t* __restrict__ stats) {
-    const int64_t P = L.pitch;
-    const uint32_t nlanes = (uint32_t)(P / kEPL);        // multiple of kBlock
+    const uint32_t P = (uint32_t)L.pitch;                 // state <= 4 GiB (checked on the host)
+    const uint32_t nlanes = P / kEPL;                     // multiple of kBlock
+    constexpr int NP = 3 * A + 2 * K + 3;
+    Bufs b;
+    b.sin = make_rsrc(sin, (int64_t)NP * P);
+    b.sout = make_rsrc(sout, (int64_t)NP * P);
+    b.act = make_rsrc(actions, (int64_t)A * P);
+    const bool has_ex = exec_out != nullptr, has_coll = coll_out != nullptr;
+    b.ex = make_rsrc(has_ex ? (const void*)exec_out : (const void*)sout, (int64_t)A * P);
+    b.coll = make_rsrc(has_coll ? (const void*)coll_out : (const void*)sout, (int64_t)P);
     // tile class per cell (bit7 Floor, bit6 Delivery, bit5 Cutboard); cells >= 64 read 0
     __shared__ uint8_t tbl[256];
     {
@@ -168,34 +197,141 @@ __global__ __launch_bounds__(kBlock) void oc_step_kernel(LevelArgs L, const uint
     // past the last chunk it re-reads the current one (an L2 hit, no HBM traffic).
     Chunk<A, K> ca, cb;
     if (g < nlanes) {  // block-uniform
-        load_chunk<A, K>(ca, sin, actions, P, g);
+        load_chunk<A, K>(ca, b, P, g);
         for (;;) {
-            load_chunk<A, K>(cb, sin, actions, P, g + stride < nlanes ? g + stride : g);
-            step_chunk<A, K>(L, tbl, ca, sout, exec_out, coll_out, P, g, st);
+            load_chunk<A, K>(cb, b, P, g + stride < nlanes ? g + stride : g);
+            step_chunk<A, K>(L, tbl, ca, b, has_ex, has_coll, P, g, st);
             g += stride;
             if (g >= nlanes) break;
-            load_chunk<A, K>(ca, sin, actions, P, g + stride < nlanes ? g + stride : g);
-            step_chunk<A, K>(L, tbl, cb, sout, exec_out, coll_out, P, g, st);
+            load_chunk<A, K>(ca, b, P, g + stride < nlanes ? g + stride : g);
+            step_chunk<A, K>(L, tbl, cb, b, has_ex, has_coll, P, g, st);
             g += stride;
             if (g >= nlanes) break;
         }
     }
 
-    if (stats != nullptr) {
-        __shared__ uint32_t red[kBlock / 64][OC_NSTATS];
-        const uint32_t v[OC_NSTATS] = {st.eps, st.succ, st.steps, st.coll, st.err};
-        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (stats != nullptr) {  // wave sums, then fire-and-forget 64-bit atomics into this block's row
+        const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
+                                       wave_sum(st.err)};
+        if ((threadIdx.x & 63u) == 0u) {
+            unsigned long long* row = (unsigned long long*)stats + (int64_t)blockIdx.x * OC_NSTATS;
 #pragma unroll
-        for (int c = 0; c < OC_NSTATS; ++c) {
-            const uint32_t r = wave_sum(v[c]);
-            if (lane == 0) red[wid][c] = r;
+            for (int c = 0; c < OC_NSTATS; ++c)
+                if (v[c]) atomicAdd(row + c, (unsigned long long)v[c]);
         }
-        __syncthreads();
-        if (threadIdx.x < OC_NSTATS) {
-            uint64_t s = 0;
+    }
+}
+
+// oc_step_n: n consecutive steps per launch.  Each lane loads its chunk's state once, then
+// for every step reads that step's actions (prefetched two steps ahead), steps in registers
+// and writes the step's outputs: the full state into traj[r] (when given), the executed
+// actions and the collision mask; the state after the last step goes to sout.  Outputs are
+// byte-identical to n oc_step launches with ping-pong buffers.
+template <int A, int K>
+__global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
+                                                           uint8_t* __restrict__ sout,
+                                                           const uint8_t* __restrict__ actions,
+                                                           uint8_t* __restrict__ traj, uint8_t* __restrict__ exec_out,
+                                                           uint8_t* __restrict__ coll_out,
+                                                           uint64_t* __restrict__ stats, int n) {
+    __shared__ uint8_t tbl[256];
+    tbl[threadIdx.x] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, threadIdx.x);
+    __syncthreads();
+    const uint32_t P = (uint32_t)L.pitch, nlanes = P / kEPL, stride = gridDim.x * (uint32_t)kBlock;
+    constexpr int NP = 3 * A + 2 * K + 3;
+    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+    auto cls_of = [&](uint32_t cells) -> uint32_t {
+        const uint32_t b0 = tbl[cells & 0xFFu], b1 = tbl[(cells >> 8) & 0xFFu], b2 = tbl[(cells >> 16) & 0xFFu],
+                       b3 = tbl[cells >> 24];
+        return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    };
+    Bufs b;
+    b.sin = make_rsrc(sin, (int64_t)NP * P);
+    b.sout = make_rsrc(sout, (int64_t)NP * P);
+    b.act = make_rsrc(actions, (int64_t)n * A * P);
+    const bool has_tr = traj != nullptr, has_ex = exec_out != nullptr, has_coll = coll_out != nullptr;
+    const __amdgpu_buffer_rsrc_t tr = make_rsrc(has_tr ? (const void*)traj : (const void*)sout, has_tr ? (int64_t)n * NP * P : 0);
+    b.ex = make_rsrc(has_ex ? (const void*)exec_out : (const void*)sout, has_ex ? (int64_t)n * A * P : 0);
+    b.coll = make_rsrc(has_coll ? (const void*)coll_out : (const void*)sout, has_coll ? (int64_t)n * P : 0);
+    StepStats st;
+    typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+    for (uint32_t g = blockIdx.x * (uint32_t)kBlock + threadIdx.x; g < nlanes; g += stride) {  // block-uniform
+        Chunk<A, K> c;
+        load_chunk<A, K>(c, b, P, g);
+        const uint32_t vo = g * 4u;
+        uint32_t T0 = c.wt.x, T1 = c.wt.y, nxt[A];
+        const int64_t rem = L.B - (int64_t)g * kEPL;
+        const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (rem <= 0 ? 0u : (1u << (8 * (uint32_t)rem)) - 1u);
 #pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
-            stats[(int64_t)blockIdx.x * OC_NSTATS + threadIdx.x] += s;  // block-private row
+        for (int a = 0; a < A; ++a) nxt[a] = n > 1 ? bld32(b.act, vo, (uint32_t)(A + a) * P) : 0u;
+        for (int r = 0; r < n; ++r) {
+            uint32_t act[A], ex[A], cm;
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                act[a] = c.wa[a];
+                c.wa[a] = nxt[a];
+            }
+            if (r + 2 < n) {
+#pragma unroll
+                for (int a = 0; a < A; ++a) nxt[a] = bld32(b.act, vo, (uint32_t)((r + 2) * A + a) * P);
+            }
+            const uint32_t f_in = c.wf;
+            ocsw::step4<A, K>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, act, ex, cm, cls_of);
+            const uint32_t ended = (c.wf & ~f_in & vmask) & ocsw::k01;
+            st.eps += __popc(ended);
+    st.succ += __popc(c.wf & (ended << 1));
+    st.err += __popc(c.wf & (ended << 2));
+            st.coll += __popc(cm & vmask);
+            const uint32_t efull = ocsw::full80(ended << 7);
+            const uint32_t sa = T0 & __builtin_amdgcn_perm(0u, efull, 0x01010000u);
+            const uint32_t sb2 = T1 & __builtin_amdgcn_perm(0u, efull, 0x03030202u);
+            st.steps += (sa & 0xFFFFu) + (sa >> 16) + (sb2 & 0xFFFFu) + (sb2 >> 16);
+            if (has_tr) {
+                const uint32_t base = (uint32_t)r * NP * P;
+#pragma unroll
+                for (int a = 0; a < A; ++a) {
+                    bst32(tr, c.wx[a], vo, base + a * P);
+                    bst32(tr, c.wy[a], vo, base + (kPY + a) * P);
+                    bst32(tr, c.wh[a], vo, base + (kPH + a) * P);
+                }
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    bst32(tr, c.wl[j], vo, base + (kPL + j) * P);
+                    bst32(tr, c.wm[j], vo, base + (kPM + j) * P);
+                }
+                const u32x2 tw = {T0, T1};
+                __builtin_amdgcn_raw_buffer_store_b64(tw, tr, (int)(g * 8u), (int)(base + kPT * P), 0);
+                bst32(tr, c.wf, vo, base + kPF * P);
+            }
+            if (has_ex) {
+#pragma unroll
+                for (int a = 0; a < A; ++a) bst32(b.ex, ex[a], vo, (uint32_t)(r * A + a) * P);
+            }
+            if (has_coll) bst32(b.coll, cm, vo, (uint32_t)r * P);
+        }
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            bst32(b.sout, c.wx[a], vo, a * P);
+            bst32(b.sout, c.wy[a], vo, (kPY + a) * P);
+            bst32(b.sout, c.wh[a], vo, (kPH + a) * P);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            bst32(b.sout, c.wl[j], vo, (kPL + j) * P);
+            bst32(b.sout, c.wm[j], vo, (kPM + j) * P);
+        }
+        const u32x2 tw = {T0, T1};
+        __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)(g * 8u), (int)(kPT * P), 0);
+        bst32(b.sout, c.wf, vo, kPF * P);
+    }
+    if (stats != nullptr) {
+        const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
+                                       wave_sum(st.err)};
+        if ((threadIdx.x & 63u) == 0u) {
+            unsigned long long* row = (unsigned long long*)stats + (int64_t)blockIdx.x * OC_NSTATS;
+#pragma unroll
+            for (int c = 0; c < OC_NSTATS; ++c)
+                if (v[c]) atomicAdd(row + c, (unsigned long long)v[c]);
         }
     }
 }
@@ -336,6 +472,13 @@ struct oc_handle {
     int32_t blocks_per_cu;  // persistent step grid: blocks per CU (OC_BLOCKS_PER_CU, default 2)
     LevelArgs args;
 };
+
+// Statistics rows: one per block of the larger of the oc_step / oc_step_n grids.
+int64_t stats_rows(const oc_handle* h, int64_t B) {
+    const int64_t P = pitch_for(B), need = P / kEnvsPerBlock, cap = (int64_t)kCUs * 5;
+    const int64_t a = step_grid(P, h->blocks_per_cu), b = need < cap ? need : cap;
+    return a > b ? a : b;
+}
 
 extern "C" {
 
@@ -480,6 +623,8 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
     LevelArgs L = h->args;
     L.pitch = pitch_for(B);
     L.B = B;
+    if ((int64_t)(3 * h->A + 2 * h->K + 3) * L.pitch >= (1ll << 31))
+        return fail(OC_EINVAL, "batch too large for one launch (state must be < 2 GiB)");
     const dim3 grid((unsigned)step_grid(L.pitch, h->blocks_per_cu));
     hipStream_t s = (hipStream_t)stream;
 #define OC_LAUNCH_STEP(A, K)                                                                          \
@@ -487,6 +632,44 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
                        (uint8_t*)state_out, actions, exec_actions, coll_mask, stats)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_STEP)
     return hip_check("oc_step launch");
+}
+
+int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions, void* traj,
+              uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, int64_t B, int32_t n, void* stream) {
+    if (h == nullptr || state_in == nullptr || state_out == nullptr || actions == nullptr || B < 0 || n < 0)
+        return fail(OC_EINVAL, "bad argument");
+    if (B == 0 || n == 0) return OC_OK;
+    if (((uintptr_t)state_in | (uintptr_t)state_out | (uintptr_t)actions | (uintptr_t)traj | (uintptr_t)exec_actions |
+         (uintptr_t)coll_mask) & 15u)
+        return fail(OC_EINVAL, "buffers must be 16-byte aligned");
+    if (state_in == state_out && n > 0 && traj == state_out) return fail(OC_EINVAL, "traj must not alias state_out");
+    LevelArgs L = h->args;
+    L.pitch = pitch_for(B);
+    L.B = B;
+    const int64_t NP = 3 * h->A + 2 * h->K + 3;
+    if (NP * L.pitch >= (1ll << 31)) return fail(OC_EINVAL, "batch too large for one launch (state must be < 2 GiB)");
+    // steps per launch so every per-launch buffer (trajectory, actions) stays < 2 GiB of offsets
+    int64_t per = ((1ll << 31) - 1) / (NP * L.pitch);
+    if (per > 4096) per = 4096;
+    const int64_t need = L.pitch / kEnvsPerBlock, cap = (int64_t)kCUs * 5;  // <= 5 waves/SIMD resident
+    const dim3 grid((unsigned)(need < cap ? need : cap));
+    hipStream_t s = (hipStream_t)stream;
+    const uint8_t* src = (const uint8_t*)state_in;
+    for (int64_t r0 = 0; r0 < n; r0 += per) {
+        const int m = (int)(n - r0 < per ? n - r0 : per);
+        const int64_t off = r0;
+        uint8_t* tr = traj ? (uint8_t*)traj + off * NP * L.pitch : nullptr;
+        uint8_t* ex = exec_actions ? exec_actions + off * h->A * L.pitch : nullptr;
+        uint8_t* cm = coll_mask ? coll_mask + off * L.pitch : nullptr;
+        const uint8_t* ac = actions + off * h->A * L.pitch;
+#define OC_LAUNCH_STEPN(A, K)                                                                                     \
+    hipLaunchKernelGGL((oc_step_n_kernel<A, K>), grid, dim3(kBlock), 0, s, L, src, (uint8_t*)state_out, ac, tr, ex, cm, \
+                       stats, m)
+        OC_DISPATCH(h->A, h->K, OC_LAUNCH_STEPN)
+        src = (const uint8_t*)state_out;
+        if (const int rc = hip_check("oc_step_n launch")) return rc;
+    }
+    return OC_OK;
 }
 
 int oc_gen_actions(const oc_handle* h, uint8_t* actions, int64_t B, int64_t env_offset, int64_t step,
@@ -524,13 +707,13 @@ int oc_state_checksum(const oc_handle* h, const void* state, int64_t B, uint64_t
 
 int oc_stats_size(const oc_handle* h, int64_t B, int64_t* nbytes) {
     if (h == nullptr || nbytes == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
-    *nbytes = step_grid(pitch_for(B), h->blocks_per_cu) * OC_NSTATS * (int64_t)sizeof(uint64_t);
+    *nbytes = stats_rows(h, B) * OC_NSTATS * (int64_t)sizeof(uint64_t);
     return OC_OK;
 }
 
 int oc_stats_reduce(const oc_handle* h, const uint64_t* stats, int64_t B, uint64_t* totals, void* stream) {
     if (h == nullptr || stats == nullptr || totals == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
-    const int64_t rows = step_grid(pitch_for(B), h->blocks_per_cu);
+    const int64_t rows = stats_rows(h, B);
     hipLaunchKernelGGL(oc_stats_reduce_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, stats, rows, totals);
     return hip_check("oc_stats_reduce launch");
 }

@@ -52,11 +52,9 @@ OC_SW uint32_t or3(uint32_t a, uint32_t b, uint32_t c) { return bop3<OC_LUT(a | 
 OC_SW uint32_t andn(uint32_t a, uint32_t b) { return bop3<OC_LUT(a & !b)>(a, b, 0u); }  // a & ~b
 OC_SW uint32_t perm(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_perm(hi, lo, s); }
 
-// h80 -> full mask: (h >> 7) * 0xFF per byte, carry-free
-OC_SW uint32_t full80(uint32_t h) {
-    const uint32_t s = h >> 7;
-    return (s << 8) - s;
-}
+// h80 -> full mask per byte: 0x80 -> 0xFF, carry-free.  Written as h | (h - (h >> 7)):
+// the equivalent (s << 8) - s is turned into a quarter-rate v_mul_lo_u32 by the compiler.
+OC_SW uint32_t full80(uint32_t h) { return h | (h - (h >> 7)); }
 // bytes <= 0x7F: h80 of (byte != 0) / (byte == 0)
 OC_SW uint32_t nz80(uint32_t x) { return (x + k7F) & k80; }
 OC_SW uint32_t z80(uint32_t x) { return andn(k80, x + k7F); }
@@ -245,12 +243,11 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         // scatter: target slot on merge / pick, held slot on reloc / merge / chop
         const uint32_t wo = merge | pick;
         const uint32_t oh = perm(0x80402010u, 0x08040201u, h);  // 1 << h per byte (h < 8)
-        const uint32_t wh01 = (and3(hold80, or3(reloc, merge, chop), k80)) >> 7;
+        const uint32_t wh80 = and3(hold80, or3(reloc, merge, chop), k80);
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const uint32_t eo = full80(at80[j] & wo);
-            const uint32_t eh01 = and3(oh >> j, wh01, k01);
-            const uint32_t eh = (eh01 << 8) - eh01;
+            const uint32_t eh = full80(and3(oh << (7 - j), wh80, k80));
             Lc[j] = sel(eh, newHl, sel(eo, newOl, Lc[j]));
             M[j] = sel(eh, newHm, sel(eo, newOm, M[j]));
         }

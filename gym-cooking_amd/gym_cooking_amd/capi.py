@@ -30,7 +30,7 @@ OC_STAT_NAMES = ("episodes", "successes", "steps", "collisions", "errors")
 # Every symbol include/oc_engine.h declares (tests check the library exports them all).
 EXPORTED_SYMBOLS = (
     "oc_abi_version", "oc_last_error", "oc_create", "oc_destroy", "oc_get_layout", "oc_reset",
-    "oc_step", "oc_gen_actions", "oc_state_checksum", "oc_stats_size", "oc_stats_reduce",
+    "oc_step", "oc_step_n", "oc_gen_actions", "oc_state_checksum", "oc_stats_size", "oc_stats_reduce",
 )
 
 
@@ -120,6 +120,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.oc_reset.argtypes = [vp, vp, i64, vp]
     lib.oc_step.restype = ctypes.c_int
     lib.oc_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, vp]
+    lib.oc_step_n.restype = ctypes.c_int
+    lib.oc_step_n.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]
     lib.oc_gen_actions.restype = ctypes.c_int
     lib.oc_gen_actions.argtypes = [vp, vp, i64, i64, i64, u64, vp]
     lib.oc_state_checksum.restype = ctypes.c_int

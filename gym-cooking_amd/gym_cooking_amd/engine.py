@@ -117,6 +117,25 @@ class OvercookedBatch:
                                     _ptr(coll), _ptr(stats), self.B, self._stream()))
         return state_out
 
+    def step_n(self, state_in: torch.Tensor, state_out: torch.Tensor, actions: torch.Tensor, n: int,
+               traj: Optional[torch.Tensor] = None, exec_out: Optional[torch.Tensor] = None,
+               coll: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """n consecutive steps in one launch (oc_step_n): identical outputs to n step() calls."""
+        self._check(state_in, self.layout.state_bytes)
+        self._check(state_out, self.layout.state_bytes)
+        self._check(actions, n * self.A * self.pitch)
+        if traj is not None:
+            self._check(traj, n * self.layout.state_bytes)
+        if exec_out is not None:
+            self._check(exec_out, n * self.A * self.pitch)
+        if coll is not None:
+            self._check(coll, n * self.pitch)
+        if stats is not None:
+            self._check(stats, self.stats_bytes)
+        capi.check(self.lib.oc_step_n(self._h, _ptr(state_in), _ptr(state_out), _ptr(actions), _ptr(traj),
+                                      _ptr(exec_out), _ptr(coll), _ptr(stats), self.B, n, self._stream()))
+        return state_out
+
     def gen_actions(self, actions: torch.Tensor, step: int, seed: int = 0, env_offset: int = 0) -> torch.Tensor:
         self._check(actions, self.A * self.pitch)
         capi.check(self.lib.oc_gen_actions(self._h, _ptr(actions), self.B, env_offset, step, seed, self._stream()))

@@ -8,7 +8,7 @@
  *   oc_create / oc_destroy   <- OvercookedEnvironment.load_level + run_recipes
  *                               (gym_cooking/envs/overcooked_environment.py:130-198, :396-473)
  *   oc_reset                 <- OvercookedEnvironment.reset      (overcooked_environment.py:201-250)
- *   oc_step                  <- OvercookedEnvironment.step       (overcooked_environment.py:255-306)
+ *   oc_step, oc_step_n       <- OvercookedEnvironment.step       (overcooked_environment.py:255-306)
  *                               = check_collisions (:724-762) + execute_navigation/interact
  *                               (:767-770, gym_cooking/utils/interact.py:4-89) + done/reward (:316-376)
  *   oc_gen_actions           <- synthetic action streams (the reference env has no RNG)
@@ -147,6 +147,17 @@ int oc_reset(const oc_handle* h, void* state, int64_t B, void* stream);
  * stepped (next-step auto-reset; its exec actions read OC_ACT_NOOP, coll 0). */
 int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
             uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, int64_t B, void* stream);
+
+/* n consecutive steps in one launch, identical to n oc_step calls with ping-pong buffers
+ * (state_in -> state_out after n steps).  The state stays in registers between steps, so the
+ * state is read from HBM once per launch instead of once per step.
+ *   actions      : n x u8 [A][pitch], step r at actions + r*A*pitch
+ *   traj         : nullable; n x [num_planes][pitch]: the state after every step (traj[r] equals
+ *                  the state_out of the r-th oc_step); must not alias state_in/state_out
+ *   exec_actions : nullable; n x u8 [A][pitch];  coll_mask : nullable; n x u8 [pitch]
+ *   stats        : accumulated over the n steps (same buffer as oc_step). */
+int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions, void* traj,
+              uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, int64_t B, int32_t n, void* stream);
 
 /* Synthetic i.i.d. uniform action codes 0..4 for B envs at step `step`:
  * code = splitmix64(seed ^ gid*0x9E3779B97F4A7C15 ^ step*0xC2B2AE3D27D4EB4F ^ agent) % 5,

@@ -210,3 +210,84 @@ def test_metric_config_full_batch_parity(dev):
             got = int(eb.checksum(s).item()) & (2**64 - 1)
             assert got == tl.checksum(c, A, ob.K, ob.pitch, B), "checksum mismatch at step %d" % t
     assert np.array_equal(s.cpu().numpy(), c)
+
+
+def _step_n_vs_steps(level, A, B, n, seed, max_T=100, with_traj=True, warm=0):
+    """oc_step_n over n steps == n oc_step calls: final state, every trajectory state, exec,
+    collision masks and statistics, byte for byte over the whole buffers."""
+    eb = _batch(level, A, B, max_T)
+    P, S = eb.pitch, eb.layout.state_bytes
+    s0 = eb.new_state()
+    eb.reset(s0)
+    if warm:  # move away from the template so episodes are mid-flight
+        a = eb.new_actions()
+        tmp = eb.new_state()
+        for t in range(warm):
+            eb.gen_actions(a, 10_000 + t, seed)
+            eb.step(s0, tmp, a)
+            s0, tmp = tmp, s0
+    acts = torch.empty(n * A * P, dtype=torch.uint8, device="cuda:0")
+    for r in range(n):
+        eb.gen_actions(acts[r * A * P:(r + 1) * A * P], r, seed)
+    # reference: n single steps
+    ref_states, ref_ex, ref_coll = [], [], []
+    stats_ref = eb.new_stats()
+    cur = s0.clone()
+    for r in range(n):
+        nxt, ex, coll = eb.new_state(), eb.new_exec(), eb.new_coll()
+        eb.step(cur, nxt, acts[r * A * P:(r + 1) * A * P], ex, coll, stats_ref)
+        ref_states.append(nxt)
+        ref_ex.append(ex)
+        ref_coll.append(coll)
+        cur = nxt
+    out = eb.new_state()
+    traj = torch.zeros(n * S, dtype=torch.uint8, device="cuda:0") if with_traj else None
+    ex_n = torch.zeros(n * A * P, dtype=torch.uint8, device="cuda:0")
+    coll_n = torch.zeros(n * P, dtype=torch.uint8, device="cuda:0")
+    stats_n = eb.new_stats()
+    eb.step_n(s0, out, acts, n, traj, ex_n, coll_n, stats_n)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref_states[-1])
+    for r in range(n):
+        if with_traj:
+            assert torch.equal(traj[r * S:(r + 1) * S], ref_states[r]), "trajectory step %d" % r
+        assert torch.equal(ex_n[r * A * P:(r + 1) * A * P], ref_ex[r]), "exec step %d" % r
+        assert torch.equal(coll_n[r * P:(r + 1) * P], ref_coll[r]), "coll step %d" % r
+    assert torch.equal(eb.reduce_stats(stats_n), eb.reduce_stats(stats_ref))
+    return eb.reduce_stats(stats_n)
+
+
+@pytest.mark.parametrize("level,A", [("partial-divider_salad", 2), ("full-divider_tl", 3),
+                                     ("open-divider_salad", 4), ("open-divider_tomato", 1)])
+def test_step_n_equals_single_steps(dev, level, A):
+    _step_n_vs_steps(level, A, 65536 + 17, 37, seed=A, max_T=20)
+
+
+def test_step_n_max_T_1_every_step_ends(dev):
+    """max_T=1: an episode ends every other step (timeout, then reset); stresses the counters."""
+    tot = _step_n_vs_steps("open-divider_salad", 2, 4096 * 64, 64, seed=3, max_T=1, with_traj=False)
+    assert int(tot[0]) == 4096 * 64 * 32
+
+
+def test_step_n_ragged_and_mid_episode(dev):
+    for B in (1, 5, 4099):
+        _step_n_vs_steps("full-divider_salad", 2, B, 9, seed=B, max_T=40, warm=13)
+
+
+def test_step_n_in_place_and_no_outputs(dev):
+    eb = _batch("partial-divider_salad", 2, 20000)
+    P = eb.pitch
+    s = eb.new_state()
+    eb.reset(s)
+    n = 25
+    acts = torch.empty(n * 2 * P, dtype=torch.uint8, device="cuda:0")
+    for r in range(n):
+        eb.gen_actions(acts[r * 2 * P:(r + 1) * 2 * P], r, 99)
+    ref = s.clone()
+    tmp = eb.new_state()
+    for r in range(n):
+        eb.step(ref, tmp, acts[r * 2 * P:(r + 1) * 2 * P])
+        ref, tmp = tmp, ref
+    eb.step_n(s, s, acts, n)  # in place, no trajectory / exec / coll / stats
+    torch.cuda.synchronize()
+    assert torch.equal(s, ref)

@@ -5,7 +5,8 @@ Dispatches, on the bench workload (partial-divider_salad, 2 agents, 2^20 envs):
   oc_reset_kernel     x3  -- writes exactly state_bytes with dword stores (WRITE_SIZE calibration)
   oc_checksum_kernel  x3  -- reads exactly 17 planes x B bytes with oc_step's dword pattern
                              (FETCH_SIZE calibration for this access width)
-  oc_step_kernel      x20 -- the measured kernel (eager launches)
+  oc_step_kernel      x20 -- the headline kernel (eager launches)
+  oc_step_n_kernel    x3  -- 16 fused steps each, trajectory + exec + coll written
 tools/pmc_report.py turns the counter CSVs into profiles/pmc_traffic.json.
 """
 import os
@@ -19,6 +20,7 @@ import torch  # noqa: E402
 from gym_cooking_amd.engine import OvercookedBatch  # noqa: E402
 
 B = 1 << 20
+NFUSED = 16
 eb = OvercookedBatch("partial-divider_salad", 2, B, max_T=100, device="cuda:0")
 a, b = eb.new_state(), eb.new_state()
 acts = torch.empty((20, eb.A * eb.pitch), dtype=torch.uint8, device="cuda:0")
@@ -32,5 +34,12 @@ for _ in range(3):
 for i in range(20):
     eb.step(a, b, acts[i], exe, coll, stats)
     a, b = b, a
+S = eb.layout.state_bytes
+traj = torch.empty(NFUSED * S, dtype=torch.uint8, device="cuda:0")
+exn = torch.empty(NFUSED * eb.A * eb.pitch, dtype=torch.uint8, device="cuda:0")
+colln = torch.empty(NFUSED * eb.pitch, dtype=torch.uint8, device="cuda:0")
+flat = acts[:NFUSED].reshape(-1)
+for _ in range(3):
+    eb.step_n(a, b, flat, NFUSED, traj, exn, colln, stats)
 torch.cuda.synchronize()
 print("pmc probe done")
