@@ -183,12 +183,6 @@ __global__ __launch_bounds__(kBlock) void oc_step_kernel(LevelArgs L, const uint
     const bool has_ex = exec_out != nullptr, has_coll = coll_out != nullptr;
     b.ex = make_rsrc(has_ex ? (const void*)exec_out : (const void*)sout, (int64_t)A * P);
     b.coll = make_rsrc(has_coll ? (const void*)coll_out : (const void*)sout, (int64_t)P);
-    // tile class per cell (bit7 Floor, bit6 Delivery, bit5 Cutboard); cells >= 64 read 0
-    __shared__ uint8_t tbl[256];
-    {
-        tbl[threadIdx.x] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, threadIdx.x);  // kBlock == 256
-        __syncthreads();
-    }
     const uint32_t stride = gridDim.x * (uint32_t)kBlock;
     uint32_t g = blockIdx.x * (uint32_t)kBlock + threadIdx.x;
     StepStats st;
@@ -196,8 +190,14 @@ __global__ __launch_bounds__(kBlock) void oc_step_kernel(LevelArgs L, const uint
     // loads).  The prefetch is unconditional so the compiler's counted vmcnt waits stay exact;
     // past the last chunk it re-reads the current one (an L2 hit, no HBM traffic).
     Chunk<A, K> ca, cb;
-    if (g < nlanes) {  // block-uniform
-        load_chunk<A, K>(ca, b, P, g);
+    const bool active = g < nlanes;  // block-uniform
+    if (active) load_chunk<A, K>(ca, b, P, g);  // in flight while the block builds its table
+    // tile class per cell (bit7 Floor, bit6 Delivery, bit5 Cutboard); cells >= 64 read 0
+    __shared__ uint8_t tbl[256];
+    tbl[threadIdx.x] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, threadIdx.x);  // kBlock == 256
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the LDS write, not the chunk loads
+    __builtin_amdgcn_s_barrier();
+    if (active) {
         for (;;) {
             load_chunk<A, K>(cb, b, P, g + stride < nlanes ? g + stride : g);
             step_chunk<A, K>(L, tbl, ca, b, has_ex, has_coll, P, g, st);

@@ -213,6 +213,66 @@ int main(int argc, char** argv) {
         float ms; CK(hipEventElapsedTime(&ms, a0, a1));
         printf("E1d hipGraph 16 steps     bpc %d: %7.2f us/step\n", bpc, ms * 1000.0 / 160);
     }
+    {  // E5: two half-batch chains on two streams (independent env ranges), as a graph
+        h->blocks_per_cu = 2;
+        for (int nsplit : {1, 2, 4}) {
+            hipStream_t s0, sx[4];
+            CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+            for (int i = 0; i < nsplit; ++i) CK(hipStreamCreateWithFlags(&sx[i], hipStreamNonBlocking));
+            hipEvent_t fork, join[4];
+            CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+            for (int i = 0; i < nsplit; ++i) CK(hipEventCreateWithFlags(&join[i], hipEventDisableTiming));
+            const int64_t Bh = B / nsplit;  // multiple of 4096: byte offsets stay 16-B aligned
+            oc_handle* hh;
+            oc_create(&lv, A, 100, 0, &hh);
+            hh->blocks_per_cu = 2;
+            oc_layout lh;
+            oc_get_layout(hh, Bh, &lh);
+            std::vector<uint8_t*> ha(nsplit), hb(nsplit), hact(nsplit), hex(nsplit), hco(nsplit);
+            for (int i = 0; i < nsplit; ++i) {
+                CK(hipMalloc(&ha[i], lh.state_bytes)); CK(hipMalloc(&hb[i], lh.state_bytes));
+                CK(hipMalloc(&hact[i], (int64_t)16 * A * lh.pitch)); CK(hipMalloc(&hex[i], A * lh.pitch));
+                CK(hipMalloc(&hco[i], lh.pitch));
+                oc_reset(hh, ha[i], Bh, nullptr);
+                for (int r = 0; r < 16; ++r) oc_gen_actions(hh, hact[i] + (int64_t)r * A * lh.pitch, Bh, i * Bh, r, 1, nullptr);
+            }
+            CK(hipDeviceSynchronize());
+            hipGraph_t gr;
+            hipGraphExec_t ge;
+            CK(hipStreamBeginCapture(s0, hipStreamCaptureModeGlobal));
+            CK(hipEventRecord(fork, s0));
+            for (int i = 0; i < nsplit; ++i) {
+                CK(hipStreamWaitEvent(sx[i], fork, 0));
+                for (int k = 0; k < 16; ++k)
+                    oc_step(hh, (k & 1) ? hb[i] : ha[i], (k & 1) ? ha[i] : hb[i], hact[i] + (int64_t)k * A * lh.pitch, hex[i],
+                            hco[i], stats, Bh, sx[i]);
+                CK(hipEventRecord(join[i], sx[i]));
+                CK(hipStreamWaitEvent(s0, join[i], 0));
+            }
+            CK(hipStreamEndCapture(s0, &gr));
+            CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+            hipEvent_t a0, a1;
+            CK(hipEventCreate(&a0)); CK(hipEventCreate(&a1));
+            for (int i = 0; i < 3; ++i) CK(hipGraphLaunch(ge, s0));
+            CK(hipEventRecord(a0, s0));
+            for (int i = 0; i < 10; ++i) CK(hipGraphLaunch(ge, s0));
+            CK(hipEventRecord(a1, s0));
+            CK(hipEventSynchronize(a1));
+            float ms; CK(hipEventElapsedTime(&ms, a0, a1));
+            printf("E5 graph, %d parallel chains of B/%d: %7.2f us/step (whole batch)\n", nsplit, nsplit, ms * 1000.0 / 160);
+            // eager: round-robin launches over the split streams
+            const double us = timeit([&] {
+                for (int k = 0; k < 16; ++k)
+                    for (int i = 0; i < nsplit; ++i)
+                        oc_step(hh, (k & 1) ? hb[i] : ha[i], (k & 1) ? ha[i] : hb[i], hact[i] + (int64_t)k * A * lh.pitch,
+                                hex[i], hco[i], stats, Bh, sx[i]);
+            }, 5) / 16;
+            printf("E5e eager, %d streams of B/%d:        %7.2f us/step (whole batch)\n", nsplit, nsplit, us);
+            CK(hipDeviceSynchronize());
+            for (int i = 0; i < nsplit; ++i) { hipFree(ha[i]); hipFree(hb[i]); hipFree(hact[i]); hipFree(hex[i]); hipFree(hco[i]); }
+            oc_destroy(hh);
+        }
+    }
     for (int grid : {256, 512, 1024}) {
         const double us = timeit([&] { hipLaunchKernelGGL((mem_only<2, 4>), dim3(grid), dim3(kBlock), 0, 0, L, sa, sb, act, ex, coll); }, 50);
         printf("E2 memory only           grid %4d: %7.2f us\n", grid, us);
