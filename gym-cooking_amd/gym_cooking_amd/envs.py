@@ -1,0 +1,539 @@
+"""gym surface of the engine: the reference ``OvercookedEnvironment`` class, drop-in, and a
+batched vector env.
+
+``OvercookedEnvironment`` mirrors gym_cooking/envs/overcooked_environment.py (class :37):
+the same constructor argument (``arglist`` with ``level``, ``num_agents``,
+``max_num_timesteps``, ``seed``, ``model1..4``), ``reset() -> env copy`` (:201-250),
+``step(action_dict) -> (obs_env, reward, done, info)`` (:255-306), ``done()`` (:316-363),
+``reward()`` (:365-376), ``close()`` (:252), ``get_repr()`` (:50-62), ``is_collision``
+(:671-722), and the attributes callers read (``t``, ``sim_agents``, ``world``, ``obs_tm1``,
+``agent_actions``, ``collisions``, ``termination_info``, ``successful``, ``filename``).
+One env is one batch row of the HIP engine (B = 1); every transition runs on the GPU
+through liboc_engine.so, and the host keeps a 17-byte-per-agent-count state copy from
+which the object views below are built.
+
+Differences from the reference, by design:
+  * stepping after ``done`` continues the episode like the reference (the engine's
+    next-step auto-reset is disabled for this single env by clearing DONE on upload);
+  * a step that the reference would crash in (two co-located agents both holding,
+    ``copy.copy`` at :289 -> world.py:417) raises ``RuntimeError`` here after updating
+    the state, as the reference raises after ``execute_navigation``;
+  * ``world.get_repr()`` lists only non-empty object groups: the reference keeps an empty
+    group for every object name that ever existed (a history artefact of
+    ``World.objects``' defaultdict, world.py:327-337), which the 17-byte state does not
+    record.  Object and agent reprs inside a group are identical.
+
+``OvercookedVecEnv`` is the batched surface (B envs on one GPU, torch tensors in and out).
+"""
+from __future__ import annotations
+
+import copy as _copy
+import types
+from collections import namedtuple
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import capi
+from . import levels as _levels
+
+CollisionRepr = namedtuple("CollisionRepr", "time agent_names agent_locations")   # overcooked_environment.py:34
+ObjectRepr = namedtuple("ObjectRepr", "name location is_held")                    # utils/core.py:128
+AgentRepr = namedtuple("AgentRepr", "name location holding")                      # utils/agent.py:22
+GridSquareRepr = namedtuple("GridSquareRepr", "name location holding")            # utils/core.py:16
+
+FLAG_DONE, FLAG_SUCCESS, FLAG_ERR = 0x01, 0x02, 0x04  # include/oc_engine.h flags plane
+COLORS = ["blue", "magenta", "yellow", "green"]  # utils/agent.py:25
+NAV_ACTIONS = [(0, 1), (0, -1), (-1, 0), (1, 0)]  # utils/world.py:16
+_TILE_NAMES = {_levels.TILE_FLOOR: "Floor", _levels.TILE_COUNTER: "Counter",
+               _levels.TILE_CUTBOARD: "Cutboard", _levels.TILE_DELIVERY: "Delivery"}
+_FOODS = (("Tomato", _levels.M_TOMATO), ("Lettuce", _levels.M_LETTUCE), ("Onion", _levels.M_ONION))
+
+
+def action_code(action) -> int:
+    """(dx, dy) -> engine action code (World.NAV_ACTIONS order, (0, 0) = no-op)."""
+    a = tuple(int(v) for v in action)
+    if a not in _levels.ACTION_CODE:
+        raise ValueError("not a navigation action: %r" % (action,))
+    return _levels.ACTION_CODE[a]
+
+
+# ---------------------------------------------------------------------------------------
+# Host views of one env's state (read-only snapshots of the engine state bytes)
+# ---------------------------------------------------------------------------------------
+class ItemView:
+    """An item slot as the reference ``Object`` (utils/core.py:130-241)."""
+
+    collidable = False
+    dynamic = False
+
+    def __init__(self, slot: int, mask: int, location: Tuple[int, int], is_held: bool):
+        self.slot, self.mask, self.location, self.is_held = slot, mask, location, is_held
+        parts = []
+        for name, bit in _FOODS:
+            if mask & bit:
+                parts.append((name, ("Chopped" if mask & _levels.chopped(bit) else "Fresh") + name))
+        if mask & _levels.M_PLATE:
+            parts.append(("Plate", "Plate"))
+        parts.sort()  # update_names: contents sorted by base name (core.py:161-171)
+        self.contents = [p[0] for p in parts]
+        self.name = "-".join(p[0] for p in parts)
+        self.full_name = "-".join(p[1] for p in parts)
+
+    def get_repr(self):
+        return ObjectRepr(name=self.full_name, location=self.location, is_held=self.is_held)
+
+    def contains(self, c_name: str) -> bool:
+        return c_name in self.contents
+
+    def needs_chopped(self) -> bool:  # core.py:176-178
+        foods = self.mask & _levels.M_FOODS
+        return len(self.contents) == 1 and foods != 0 and not (self.mask >> 4) & foods
+
+    def is_deliverable(self) -> bool:  # core.py:214-219
+        foods = self.mask & _levels.M_FOODS
+        return len(self.contents) >= 2 and ((self.mask >> 4) & foods) == foods
+
+    def __eq__(self, other):  # core.py:142-146
+        return (getattr(other, "name", None) == self.name and getattr(other, "full_name", None) == self.full_name
+                and len(getattr(other, "contents", ())) == len(self.contents))
+
+    def __hash__(self):
+        return hash((self.slot, self.mask, self.location))
+
+    def __str__(self):
+        return self.full_name
+
+    __repr__ = __str__
+
+
+class GridSquareView:
+    """A static tile as the reference ``GridSquare`` (utils/core.py:28-120)."""
+
+    def __init__(self, name: str, location: Tuple[int, int], holding):
+        self.name, self.location, self.holding = name, location, holding
+        self.collidable = name != "Floor"
+
+    def get_repr(self):
+        return GridSquareRepr(name=self.name, location=self.location, holding=self.holding)
+
+    def __eq__(self, other):
+        return isinstance(other, GridSquareView) and other.name == self.name
+
+    def __hash__(self):
+        return hash((self.name, self.location))
+
+
+class SimAgentView:
+    """An agent as the reference ``SimAgent`` (utils/agent.py:369-423)."""
+
+    def __init__(self, name: str, color: str, location: Tuple[int, int], holding: Optional[ItemView], action=None):
+        self.name, self.color, self.location, self.holding, self.action = name, color, location, holding, action
+
+    def get_repr(self):  # agent.py:393-394
+        return AgentRepr(name=self.name, location=self.location, holding=self.get_holding())
+
+    def get_holding(self) -> str:  # agent.py:396-399
+        return "None" if self.holding is None else self.holding.full_name
+
+
+class WorldView:
+    """The reference ``World`` queries (utils/world.py:285-436) over one env's state."""
+
+    NAV_ACTIONS = NAV_ACTIONS
+
+    def __init__(self, level: _levels.Level, items: Sequence[ItemView]):
+        self.level = level
+        self.width, self.height = level.width, level.height
+        self.perimeter = 2 * (self.width + self.height)  # overcooked_environment.py:198
+        self.items = list(items)
+        unheld = {it.location: it for it in self.items if not it.is_held}
+        self.objects: Dict[str, list] = {}
+        self._squares: Dict[Tuple[int, int], GridSquareView] = {}
+        for c, code in enumerate(level.tiles):
+            xy = level.xy(c)
+            name = _TILE_NAMES[code]
+            holding = None
+            if name == "Delivery":
+                holding = [it for it in self.items if not it.is_held and it.location == xy]
+            elif name != "Floor":
+                holding = unheld.get(xy)
+            gs = GridSquareView(name, xy, holding)
+            self._squares[xy] = gs
+            self.objects.setdefault(name, []).append(gs)
+        for it in sorted(self.items, key=lambda i: i.slot):
+            self.objects.setdefault(it.name, []).append(it)
+
+    def get_object_list(self) -> list:
+        out = []
+        for v in self.objects.values():
+            out += v
+        return out
+
+    def get_dynamic_objects(self):  # world.py:322-337 (non-empty groups, see module doc)
+        objs = []
+        for key in sorted(self.objects):
+            if key in ("Counter", "Floor", "Delivery", "Cutboard") or "Supply" in key:
+                continue
+            objs.append(tuple(o.get_repr() for o in self.objects[key]))
+        return tuple(objs)
+
+    get_repr = get_dynamic_objects
+
+    def is_occupied(self, location) -> bool:  # world.py:285-290
+        return any(it.location == tuple(location) and not it.is_held for it in self.items)
+
+    def is_collidable(self, location) -> bool:
+        return self.get_gridsquare_at(location).collidable
+
+    def get_collidable_object_locations(self) -> list:
+        return [o.location for o in self.get_object_list() if o.collidable]
+
+    def get_object_locs(self, obj, is_held: bool) -> list:  # world.py:339-363
+        if obj.name not in self.objects:
+            return []
+        if isinstance(obj, ItemView):
+            return [o.location for o in self.objects[obj.name] if obj == o and o.is_held == is_held]
+        return [o.location for o in self.objects[obj.name] if obj == o]
+
+    def get_all_object_locs(self, obj) -> list:  # world.py:365-376
+        return list(set(self.get_object_locs(obj, True) + self.get_object_locs(obj, False)))
+
+    def get_object_at(self, location, desired_obj, find_held_objects: bool):  # world.py:378-405
+        loc = tuple(location)
+        objs = [o for o in self.items if o.location == loc and o.is_held is find_held_objects
+                and (desired_obj is None or o.name == desired_obj.name)]
+        assert len(objs) == 1, "looking for {}, found {} at {}".format(desired_obj, len(objs), location)
+        return objs[0]
+
+    def get_gridsquare_at(self, location) -> GridSquareView:  # world.py:407-416
+        gs = self._squares.get((int(location[0]), int(location[1])))
+        assert gs is not None, "0 gridsquares at {}".format(location)
+        return gs
+
+    def inbounds(self, location):  # world.py:432-436
+        x, y = location
+        return min(max(x, 0), self.width - 1), min(max(y, 0), self.height - 1)
+
+
+def is_collision(world, agent1_loc, agent2_loc, agent1_action, agent2_action):
+    """OvercookedEnvironment.is_collision (overcooked_environment.py:671-722): [execute1,
+    execute2] for two agents' (location, action) on `world` (anything with get_gridsquare_at)."""
+    execute = [True, True]
+    l1, l2, a1, a2 = tuple(agent1_loc), tuple(agent2_loc), tuple(agent1_action), tuple(agent2_action)
+    n1 = (l1[0] + a1[0], l1[1] + a1[1])
+    if world.get_gridsquare_at(n1).collidable:
+        n1 = l1
+    n2 = (l2[0] + a2[0], l2[1] + a2[1])
+    if world.get_gridsquare_at(n2).collidable:
+        n2 = l2
+    if n1 == n2:
+        if n1 == l1 and a1 != (0, 0):
+            execute[1] = False
+        elif n2 == l2 and a2 != (0, 0):
+            execute[0] = False
+        else:
+            execute[0] = execute[1] = False
+    elif l1 == n2 and l2 == n1:
+        execute[0] = execute[1] = False
+    return execute
+
+
+def build_views(level: _levels.Level, A: int, K: int, env_bytes: np.ndarray, actions=None):
+    """(sim_agents, world, t, flags) of one env from its canonical state bytes
+    (oc_testlib.env_view order: ax[A] ay[A] ah[A] loc[K] mask[K] t_lo t_hi flags)."""
+    b = [int(v) for v in env_bytes]
+    ax, ay, ah = b[0:A], b[A:2 * A], b[2 * A:3 * A]
+    loc, mask = b[3 * A:3 * A + K], b[3 * A + K:3 * A + 2 * K]
+    t = b[3 * A + 2 * K] | (b[3 * A + 2 * K + 1] << 8)
+    flags = b[3 * A + 2 * K + 2]
+    held = {h: a for a, h in enumerate(ah) if h != _levels.HOLD_NONE}
+    items = {}
+    for j in range(K):
+        if loc[j] == _levels.LOC_DEAD:
+            continue
+        items[j] = ItemView(j, mask[j], level.xy(loc[j]), j in held)
+    agents = []
+    for a in range(A):
+        act = None if actions is None else actions[a]
+        agents.append(SimAgentView("agent-%d" % (a + 1), COLORS[a], (ax[a], ay[a]), items.get(ah[a]), act))
+    return agents, WorldView(level, list(items.values())), t, flags
+
+
+# ---------------------------------------------------------------------------------------
+# Single env: the reference class surface
+# ---------------------------------------------------------------------------------------
+class OvercookedEnvironment:
+    """Drop-in for gym_cooking.envs.OvercookedEnvironment, stepped by the HIP engine."""
+
+    def __init__(self, arglist=None, device="cuda:0", **kwargs):
+        if arglist is None:
+            arglist = types.SimpleNamespace(level=kwargs.pop("level"), num_agents=kwargs.pop("num_agents"),
+                                            max_num_timesteps=kwargs.pop("max_num_timesteps", 100),
+                                            seed=kwargs.pop("seed", 1), model1=None, model2=None,
+                                            model3=None, model4=None, record=False, with_image_obs=False)
+        self.arglist = arglist
+        self.t = 0
+        self.set_filename()
+        self.rep = []
+        self.collisions: List[CollisionRepr] = []
+        self.termination_info = ""
+        self.successful = False
+        self._device = device
+        self._engine = None
+        self._host = None
+
+    # -- reference bookkeeping ------------------------------------------------------------
+    def set_filename(self):  # overcooked_environment.py:116-128
+        a = self.arglist
+        self.filename = "{}_agents{}_seed{}".format(a.level, a.num_agents, getattr(a, "seed", 1))
+        for i in range(1, 5):
+            m = getattr(a, "model%d" % i, None)
+            if m is not None:
+                self.filename += "_model%d-%s" % (i, m)
+
+    def _ensure_engine(self):
+        if self._engine is None:
+            from .engine import OvercookedBatch  # raises without liboc_engine.so / a GPU
+            level = self.arglist.level
+            self.level = _levels.load_level(level) if isinstance(level, str) else level
+            self._engine = _Single(OvercookedBatch(self.level, self.arglist.num_agents, 1,
+                                                   max_T=self.arglist.max_num_timesteps, device=self._device))
+        return self._engine
+
+    def _refresh(self, actions=None):
+        eng = self._engine
+        self.sim_agents, self.world, self.t, self._flags = build_views(self.level, eng.A, eng.K, self._host, actions)
+
+    # -- gym API ----------------------------------------------------------------------------
+    def reset(self):  # :201-250
+        eng = self._ensure_engine()
+        self.agent_actions = {}
+        self.rep = []
+        self.collisions = []
+        self.termination_info = ""
+        self.successful = False
+        self.recipes = list(self.level.recipes)
+        self._host = eng.reset()
+        self._refresh()
+        self.obs_tm1 = _copy.copy(self)
+        return _copy.copy(self)
+
+    def close(self):  # :252-253
+        return
+
+    def step(self, action_dict):  # :255-306
+        eng = self._engine
+        if eng is None or self._host is None:
+            raise RuntimeError("call reset() before step()")
+        names = self.get_agent_names()
+        codes = [action_code(action_dict[n]) for n in names]
+        pre = self._host
+        new, ex, coll = eng.step(pre, codes)
+        t_now = self.t + 1
+        # collision log (check_collisions :724-757): pairs in combinations order
+        p = 0
+        for i in range(eng.A):
+            for j in range(i + 1, eng.A):
+                if (coll >> p) & 1:
+                    self.collisions.append(CollisionRepr(time=t_now, agent_names=[names[i], names[j]],
+                                                         agent_locations=[self.sim_agents[i].location,
+                                                                          self.sim_agents[j].location]))
+                p += 1
+        executed = [_levels.ACTIONS[c] for c in ex]
+        # obs_tm1: the state before execution, with the post-collision actions (:273)
+        self.obs_tm1 = _copy.copy(self)
+        self.obs_tm1.t = t_now  # the reference increments t before the copy (:257, :273)
+        for a, act in zip(self.obs_tm1.sim_agents, executed):
+            a.action = act
+        self._host = new
+        self._refresh(executed)
+        self.agent_actions = {n: act for n, act in zip(names, executed)}
+        if self._flags & FLAG_ERR:
+            raise RuntimeError("two co-located agents both hold items: the reference crashes in copy.copy "
+                               "(overcooked_environment.py:289 -> world.py:417)")
+        new_obs = _copy.copy(self)
+        done = self.done()
+        reward = self.reward()
+        info = {"t": self.t, "obs": new_obs, "image_obs": None, "done": done,
+                "termination_info": self.termination_info}
+        return new_obs, reward, done, info
+
+    def done(self):  # :316-363 (evaluated by the engine; timeout takes precedence)
+        mt = self.arglist.max_num_timesteps
+        if self.t >= mt and mt:
+            self.termination_info = "Terminating because passed {} timesteps".format(mt)
+            self.successful = False
+            return True
+        if self._flags & FLAG_SUCCESS:
+            self.termination_info = "Terminating because all deliveries were completed"
+            self.successful = True
+            return True
+        self.termination_info = ""
+        self.successful = False
+        return False
+
+    def reward(self):  # :365-376
+        return 1 if self.successful else 0
+
+    # -- queries the planners use ------------------------------------------------------------
+    def get_repr(self):  # :50-62
+        return self.world.get_repr() + tuple(a.get_repr() for a in self.sim_agents)
+
+    def __eq__(self, other):
+        return isinstance(other, OvercookedEnvironment) and self.get_repr() == other.get_repr()
+
+    def __hash__(self):
+        return hash(self.get_repr())
+
+    def __str__(self):
+        return "\n".join("".join(c + " " for c in row) for row in self._display_rows())
+
+    def _display_rows(self):
+        chars = {"Floor": " ", "Counter": "-", "Cutboard": "/", "Delivery": "*"}
+        rows = [[chars[_TILE_NAMES[self.level.tile_at(x, y)]] for x in range(self.world.width)]
+                for y in range(self.world.height)]
+        for it in self.world.items:
+            x, y = it.location
+            rows[y][x] = it.full_name[0].lower() if it.full_name else rows[y][x]
+        for a in self.sim_agents:
+            x, y = a.location
+            rows[y][x] = a.name[-1]
+        return rows
+
+    def __copy__(self):  # :100-114 -- a snapshot sharing the engine handle
+        new = object.__new__(OvercookedEnvironment)
+        new.__dict__ = self.__dict__.copy()
+        if self._host is not None:
+            new._host = self._host.copy()
+            new._refresh([a.action for a in self.sim_agents])
+        new.collisions = list(self.collisions)
+        return new
+
+    def get_agent_names(self) -> List[str]:
+        return [a.name for a in self.sim_agents]
+
+    def is_collision(self, agent1_loc, agent2_loc, agent1_action, agent2_action):  # :671-722
+        return is_collision(self.world, agent1_loc, agent2_loc, agent1_action, agent2_action)
+
+    def state_bytes(self) -> np.ndarray:
+        """The env's state bytes (ax[A] ay[A] ah[A] loc[K] mask[K] t_lo t_hi flags)."""
+        return self._host.copy()
+
+    def load_state(self, env_bytes) -> None:
+        """Set the env's state from state bytes (same order as :meth:`state_bytes`)."""
+        self._ensure_engine()
+        b = np.asarray(env_bytes, dtype=np.uint8).copy()
+        if b.shape != (self._engine.NP,):
+            raise ValueError("expected %d state bytes, got %s" % (self._engine.NP, b.shape))
+        self._host = b
+        self._refresh()
+
+
+class _Single:
+    """One env row of an OvercookedBatch(B=1): host canonical bytes in, host bytes out."""
+
+    def __init__(self, batch):
+        self.b = batch
+        self.A, self.K, self.P = batch.A, batch.K, batch.pitch
+        self.NP = batch.layout.num_planes
+        self.s_in, self.s_out = batch.new_state(), batch.new_state()
+        self.act, self.ex, self.coll = batch.new_actions(), batch.new_exec(), batch.new_coll()
+        self._t = batch.layout.plane_t
+
+    def _download(self, buf) -> np.ndarray:
+        host = buf.view(self.NP, self.P)[:, :2].cpu().numpy()  # env 0 of every plane (+ t's high byte)
+        out = host[:, 0].copy()
+        out[self._t + 1] = host[self._t, 1]  # t is u16 at byte 0..1 of the two t planes' row
+        return out
+
+    def _upload(self, env_bytes: np.ndarray, buf):
+        rows = np.zeros((self.NP, 2), np.uint8)
+        rows[:, 0] = env_bytes
+        rows[self._t, 0], rows[self._t, 1] = env_bytes[self._t], env_bytes[self._t + 1]
+        rows[self._t + 1, :] = 0
+        buf.view(self.NP, self.P)[:, :2].copy_(torch.from_numpy(rows))
+
+    def reset(self) -> np.ndarray:
+        self.b.reset(self.s_in)
+        return self._download(self.s_in)
+
+    def step(self, env_bytes: np.ndarray, codes: Sequence[int]):
+        cur = env_bytes.copy()
+        cur[-1] &= ~np.uint8(FLAG_DONE)  # no auto-reset for the single env: the reference keeps stepping
+        self._upload(cur, self.s_in)
+        self.act.view(self.A, self.P)[:, 0].copy_(torch.tensor(list(codes), dtype=torch.uint8))
+        self.b.step(self.s_in, self.s_out, self.act, self.ex, self.coll)
+        new = self._download(self.s_out)
+        ex = self.ex.view(self.A, self.P)[:, 0].cpu().tolist()
+        coll = int(self.coll[0].item())
+        return new, ex, coll
+
+
+# ---------------------------------------------------------------------------------------
+# Batched vector env
+# ---------------------------------------------------------------------------------------
+class OvercookedVecEnv:
+    """B kitchens on one GPU with the gym vector-env shape of API.
+
+    ``reset()`` returns the state buffer; ``step(actions)`` takes ``uint8 [A, B]`` action
+    codes (or ``[A, pitch]``) and returns ``(state, reward[B] int8, done[B] bool, info)``
+    where ``info`` holds the executed actions ``[A, B]`` and the collision-pair masks ``[B]``.
+    Envs that were done at the input are reset to the level template by the engine in the
+    same launch (next-step auto-reset).  All tensors stay on the GPU.
+    """
+
+    def __init__(self, level, num_agents: int, num_envs: int, max_num_timesteps: int = 100, device="cuda:0"):
+        from .engine import OvercookedBatch
+        self.batch = OvercookedBatch(level, num_agents, num_envs, max_T=max_num_timesteps, device=device)
+        self.num_envs, self.A, self.P = num_envs, num_agents, self.batch.pitch
+        self._s = [self.batch.new_state(), self.batch.new_state()]
+        self._i = 0
+        self._act = self.batch.new_actions()
+        self.ex, self.coll = self.batch.new_exec(), self.batch.new_coll()
+        self.stats = self.batch.new_stats()
+        self._fl = self.batch.layout.plane_flags
+
+    @property
+    def state(self) -> torch.Tensor:
+        return self._s[self._i]
+
+    def planes(self) -> Dict[str, torch.Tensor]:
+        return self.batch.planes(self.state)
+
+    def reset(self) -> torch.Tensor:
+        self.batch.reset(self.state)
+        return self.state
+
+    def step(self, actions: torch.Tensor):
+        B, P = self.num_envs, self.P
+        if actions.shape[-1] == P and actions.is_contiguous():
+            act = actions.reshape(-1)
+        else:
+            self._act.view(self.A, P)[:, :B].copy_(actions.view(self.A, B))
+            act = self._act
+        src, dst = self._s[self._i], self._s[self._i ^ 1]
+        self.batch.step(src, dst, act, self.ex, self.coll, self.stats)
+        self._i ^= 1
+        fl = dst.view(-1, P)[self._fl, :B]
+        done = (fl & FLAG_DONE) != 0
+        reward = ((fl & FLAG_SUCCESS) != 0).to(torch.int8)
+        info = {"exec_actions": self.ex.view(self.A, P)[:, :B], "collisions": self.coll[:B],
+                "error": (fl & FLAG_ERR) != 0}
+        return dst, reward, done, info
+
+    def episode_stats(self) -> torch.Tensor:
+        """int64 [episodes, successes, steps, collisions, errors] since construction."""
+        return self.batch.reduce_stats(self.stats)
+
+
+def register(env_id: str = "overcookedEnv-v0") -> bool:
+    """Register the shim with gym under the reference's id (gym_cooking/__init__.py:3-6)
+    when gym is importable; returns whether it did."""
+    try:
+        from gym.envs.registration import register as _reg
+    except ImportError:
+        return False
+    _reg(id=env_id, entry_point="gym_cooking_amd.envs:OvercookedEnvironment")
+    return True

@@ -78,8 +78,10 @@ def canonical(state: np.ndarray, A: int, K: int, pitch: int, width: int, B: int)
     return dict(t=v["t"][:B].copy(), flags=v["fl"][:B].copy(), agents=agents, items=items[:, :4])
 
 
-def load_fixture(name: str):
-    return np.load(os.path.join(GOLDEN, name))
+def load_fixture(name: str) -> Dict[str, np.ndarray]:
+    """All arrays of a golden .npz, materialised (NpzFile re-reads an array on every index)."""
+    with np.load(os.path.join(GOLDEN, name)) as z:
+        return {k: z[k] for k in z.files}
 
 
 class EpisodeGroup:
