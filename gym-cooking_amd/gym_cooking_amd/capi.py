@@ -56,6 +56,38 @@ class OcLayout(ctypes.Structure):
     ]
 
 
+SUB_NONE, SUB_CHOP, SUB_MERGE, SUB_DELIVER = 0, 1, 2, 3
+ROLL_LEGAL, ROLL_GOAL, ROLL_ASSERT = 0x01, 0x02, 0x04
+MAX_SUBTASKS = 64
+
+
+class OcSubtask(ctypes.Structure):
+    """oc_subtask (include/oc_engine.h): one navigation-planner configuration."""
+    _fields_ = [("kind", ctypes.c_int32), ("num_agents", ctypes.c_int32), ("agent", ctypes.c_uint8 * 2),
+                ("start_mask", ctypes.c_uint8 * 2), ("goal_mask", ctypes.c_uint8),
+                ("goal_count", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 2)]
+
+
+def subtask(kind: int, agents, start_masks, goal_mask: int, goal_count: int = 0) -> OcSubtask:
+    s = OcSubtask()
+    s.kind = kind
+    s.num_agents = len(agents)
+    for i, a in enumerate(agents):
+        s.agent[i] = a
+    for i, m in enumerate(start_masks):
+        s.start_mask[i] = m
+    s.goal_mask = goal_mask
+    s.goal_count = goal_count
+    return s
+
+
+def subtask_array(subtasks):
+    arr = (OcSubtask * len(subtasks))()
+    for i, s in enumerate(subtasks):
+        arr[i] = s
+    return arr
+
+
 def level_desc(level: "_lv.Level", num_agents: int) -> OcLevelDesc:
     """Pack a :class:`levels.Level` into the C struct (validates it first)."""
     level.validate(num_agents)

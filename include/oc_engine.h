@@ -177,6 +177,58 @@ int oc_stats_size(const oc_handle* h, int64_t B, int64_t* nbytes);
 int oc_stats_reduce(const oc_handle* h, const uint64_t* stats, int64_t B, uint64_t* totals,
                     void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Navigation-planner rollout: what E2E_BRTDP evaluates per (state,
+ * subtask allocation, action).  Replaces, per row:
+ *   _configure_planner_level, Level 0   navigation_planner/planners/e2e_brtdp.py:383-406
+ *     (agents outside the subtask become collidable AgentCounters, utils/core.py:79-93,
+ *      and the items they hold leave the world)
+ *   get_actions / get_single_actions    e2e_brtdp.py:151-206, navigation_planner/utils.py:55-90
+ *   T(state_repr, action)               e2e_brtdp.py:103-149 (interact per subtask agent in
+ *                                       order, no collision pass, joint co-location assert)
+ *   is_goal_state                       e2e_brtdp.py:435-566
+ *   get_lower_bound_for_subtask_given_objs  gym_cooking/envs/overcooked_environment.py:480-664
+ *     -> World.get_lower_bound_between(_helper), check_bound   gym_cooking/utils/world.py:115-283
+ *     over the static reachability graph            world.py:67-108 (BFS table built in oc_create)
+ * ------------------------------------------------------------------------------------- */
+#define OC_MAX_SUBTASKS 64
+#define OC_SUB_NONE 0    /* subtask None: every state is a goal state */
+#define OC_SUB_CHOP 1    /* Chop(food)     gym_cooking/recipe_planner/utils.py:128 */
+#define OC_SUB_MERGE 2   /* Merge(a, b)    recipe_planner/utils.py:142 */
+#define OC_SUB_DELIVER 3 /* Deliver(dish)  recipe_planner/utils.py:157 */
+
+/* One planner configuration (set_settings(env, subtask, subtask_agent_names)). */
+typedef struct {
+    int32_t kind;          /* OC_SUB_* */
+    int32_t num_agents;    /* 1 or 2 (is_joint) */
+    uint8_t agent[2];      /* subtask agent indices, ascending (sim_agents order) */
+    uint8_t start_mask[2]; /* start_obj content mask (Chop, Deliver: [0]); Merge: start_obj[0], [1] */
+    uint8_t goal_mask;     /* goal_obj content mask (navigation_planner/utils.py:181-246) */
+    uint8_t goal_count;    /* cur_obj_count of _define_goal_state at set_settings */
+    uint8_t reserved[2];
+} oc_subtask;
+
+/* rollout flags (per row) */
+#define OC_ROLL_LEGAL 0x01  /* the action is in get_actions(state) (joint: both single-legal and
+                               is_collision all True) */
+#define OC_ROLL_GOAL 0x02   /* is_goal_state(T(state, action)); 0 on OC_ROLL_ASSERT rows */
+#define OC_ROLL_ASSERT 0x04 /* joint: the two agents end co-located (the reference's
+                               AssertionError at e2e_brtdp.py:143; state_out still written) */
+
+/* One rollout transition per row e < B:
+ *   state_in   : states in the oc_layout (real or already Level-0 states)
+ *   state_out  : the Level-0 next state: agents outside the subtask keep their location with
+ *                hold = OC_HOLD_NONE and their held items dead; t and flags copied
+ *   actions    : u8 [A][pitch] codes; only the subtask agents' rows are read
+ *   alloc      : nullable u8 [pitch] index into subtasks per row (NULL: subtasks[0])
+ *   subtasks   : host array of num_subtasks (<= OC_MAX_SUBTASKS) planner configurations
+ *   out_flags  : u8 [pitch] OC_ROLL_* ;  lower_bound : f32 [pitch], the lower bound of the
+ *                next state before the planner's cost factor (value_init: v_l = 1.1*lb - 1.09,
+ *                v_u = 6.05*lb; goal states have value 0) */
+int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
+               const uint8_t* alloc, const oc_subtask* subtasks, int32_t num_subtasks,
+               uint8_t* out_flags, float* lower_bound, int64_t B, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,6 +16,7 @@
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <math.h>
 #include <string.h>
 
 #include "../include/oc_engine.h"
@@ -49,6 +50,10 @@ typedef struct {
     int t;
     Obj objs[OC_MAX_ITEMS];
     Agent agents[OC_MAX_AGENTS];
+    /* planner Level-0 view (e2e_brtdp.py:389-406): agents outside the subtask are removed
+     * from sim_agents and their Floor becomes an AgentCounter; 0 / all-active on the env step */
+    uint64_t agent_counter;
+    int active[OC_MAX_AGENTS];
 } Env;
 
 static const Loc NAV[5] = {{0, 1}, {0, -1}, {-1, 0}, {1, 0}, {0, 0}};
@@ -66,7 +71,9 @@ static int action_code(Loc a) {
  * reference asserts when there is none (off-grid); level validation excludes that. */
 static int gridsquare_at(const Env* e, Loc l) {
     if (l.x < 0 || l.y < 0 || l.x >= e->L->width || l.y >= e->L->height) abort();
-    return e->L->tiles[l.y * e->L->width + l.x];
+    const int c = l.y * e->L->width + l.x;
+    if ((e->agent_counter >> c) & 1u) return OC_TILE_COUNTER; /* AgentCounter (core.py:79-93) */
+    return e->L->tiles[c];
 }
 
 /* GridSquare.collidable: only Floor is walkable (core.py:34, 64) */
@@ -340,6 +347,8 @@ static void unpack(const Cfg* c, const uint8_t* s, int64_t e, Env* env, int* fla
     }
     for (int a = 0; a < A; ++a)
         if (env->agents[a].holding >= 0) env->objs[env->agents[a].holding].is_held = 1;
+    env->agent_counter = 0;
+    for (int a = 0; a < OC_MAX_AGENTS; ++a) env->active[a] = 1;
 }
 
 static void pack(const Cfg* c, const Env* env, int flags, uint8_t* s, int64_t e) {
@@ -400,6 +409,7 @@ static void template_env(const Cfg* c, Env* env) {
         env->agents[a].holding = -1;
         env->agents[a].action = NAV[OC_ACT_NOOP];
     }
+    for (int a = 0; a < OC_MAX_AGENTS; ++a) env->active[a] = 1;
 }
 
 /* step() (overcooked_environment.py:255-306) for env e. */
@@ -510,4 +520,341 @@ int oco_gen_actions(int A, uint8_t* act, int64_t B, int64_t pitch, int64_t env_o
         for (int64_t e = 0; e < B; ++e)
             act[a * pitch + e] = oco_action_code(seed, (uint64_t)(env_offset + e), (uint64_t)step, (uint64_t)a);
     return OC_OK;
+}
+
+/* =========================================================================================
+ * Navigation-planner rollout, restated from the reference planner.
+ * ========================================================================================= */
+
+static int obj_mask(const Obj* o) {
+    int m = o->plates ? OC_M_PLATE : 0;
+    for (int f = 0; f < NFOOD; ++f)
+        if (o->food_present[f]) m |= (1 << f) | (o->food_state[f] << (f + OC_M_CHOPPED_SHIFT));
+    return m;
+}
+
+static int cell_of(const Env* e, Loc l) { return l.y * e->L->width + l.x; }
+
+/* E2E_BRTDP._configure_planner_level, LEVEL0 branch (e2e_brtdp.py:389-406): every agent
+ * not in the subtask leaves sim_agents, the object it holds leaves the world, and its Floor
+ * is replaced by an AgentCounter. */
+static void level0_view(Env* e, const oc_subtask* s) {
+    for (int a = 0; a < e->A; ++a) {
+        int in = 0;
+        for (int i = 0; i < s->num_agents; ++i) in |= s->agent[i] == a;
+        if (in) continue;
+        Agent* ag = &e->agents[a];
+        e->active[a] = 0;
+        if (ag->holding >= 0) {
+            e->objs[ag->holding].alive = 0; /* env.world.remove(agent.holding) */
+            ag->holding = -1;
+        }
+        e->agent_counter |= 1ull << cell_of(e, ag->location); /* Floor -> AgentCounter */
+    }
+}
+
+/* gs.holding of a non-Floor square: the un-held object on it (Counter / Cutboard /
+ * AgentCounter hold at most one; core.py:41-56) or -1 */
+static int square_holding(const Env* e, Loc l) {
+    for (int i = 0; i < e->K; ++i)
+        if (e->objs[i].alive && !e->objs[i].is_held && loc_eq(e->objs[i].location, l)) return i;
+    return -1;
+}
+
+/* nav_utils.get_single_actions (navigation_planner/utils.py:55-90): is `code` in the list */
+static int single_action_legal(const Env* e, int a, int code) {
+    if (code == OC_ACT_NOOP) return 1; /* (0, 0) is always appended (:89) */
+    const Agent* ag = &e->agents[a];
+    Loc nl = inbounds(e, loc_add(ag->location, NAV[code]));
+    for (int b = 0; b < e->A; ++b) /* new_loc not in agent_locs (sim_agents of the Level-0 env) */
+        if (e->active[b] && loc_eq(e->agents[b].location, nl)) return 0;
+    int gs = gridsquare_at(e, nl);
+    if (!collidable(gs)) return 1;
+    if (gs == OC_TILE_DELIVERY) return 1;
+    int o = square_holding(e, nl);
+    if (o < 0 && ag->holding >= 0) return 1;
+    if (o >= 0 && ag->holding < 0) return 1;
+    if (o >= 0 && ag->holding >= 0 && mergeable(&e->objs[ag->holding], &e->objs[o])) return 1;
+    return 0;
+}
+
+/* E2E_BRTDP.get_actions (e2e_brtdp.py:151-206): is the (joint) action in the list */
+static int action_legal(const Env* e, const oc_subtask* s, const int* codes) {
+    if (s->kind == OC_SUB_NONE) return codes[0] == OC_ACT_NOOP && (s->num_agents < 2 || codes[1] == OC_ACT_NOOP);
+    for (int i = 0; i < s->num_agents; ++i)
+        if (!single_action_legal(e, s->agent[i], codes[i])) return 0;
+    if (s->num_agents == 2) {
+        int ex[2];
+        is_collision(e, e->agents[s->agent[0]].location, e->agents[s->agent[1]].location, NAV[codes[0]],
+                     NAV[codes[1]], ex);
+        if (!(ex[0] && ex[1])) return 0;
+    }
+    return 1;
+}
+
+/* E2E_BRTDP.T (e2e_brtdp.py:103-149): interact for each subtask agent in order, no
+ * collision pass; returns 1 where the joint co-location assert (:143) fails. */
+static int rollout_T(Env* e, const oc_subtask* s, const int* codes) {
+    for (int i = 0; i < s->num_agents; ++i) e->agents[s->agent[i]].action = NAV[codes[i]];
+    for (int i = 0; i < s->num_agents; ++i) interact(e, &e->agents[s->agent[i]]);
+    if (s->num_agents == 2 && loc_eq(e->agents[s->agent[0]].location, e->agents[s->agent[1]].location)) return 1;
+    return 0;
+}
+
+/* is_goal_state (e2e_brtdp.py:435-566) */
+static int is_goal_state(const Env* e, const oc_subtask* s) {
+    if (s->kind == OC_SUB_NONE) return 1;
+    int count = 0;
+    if (s->kind == OC_SUB_DELIVER) { /* un-held goal objects on a Delivery square */
+        for (int i = 0; i < e->K; ++i) {
+            const Obj* o = &e->objs[i];
+            if (o->alive && !o->is_held && obj_mask(o) == s->goal_mask &&
+                gridsquare_at(e, o->location) == OC_TILE_DELIVERY)
+                ++count;
+        }
+    } else { /* len(get_all_object_locs(goal_obj)): distinct locations, held or not */
+        Loc seen[OC_MAX_ITEMS];
+        for (int i = 0; i < e->K; ++i) {
+            const Obj* o = &e->objs[i];
+            if (!o->alive || obj_mask(o) != s->goal_mask) continue;
+            int dup = 0;
+            for (int j = 0; j < count; ++j) dup |= loc_eq(seen[j], o->location);
+            if (!dup) seen[count++] = o->location;
+        }
+    }
+    return count > s->goal_count;
+}
+
+/* World.make_reachability_graph (world.py:67-108) over the STATIC level (the graph is built
+ * at reset and shared by every copy, world.py:38), as an all-pairs BFS table.  Node id =
+ * cell * 5 + d, d = NAV index of the approach direction, 4 = (0, 0) on a Floor. */
+#define RG_N (OC_MAX_CELLS * 5)
+typedef struct {
+    int exists[RG_N];
+    int16_t dist[RG_N][RG_N]; /* -1: no path */
+} Reach;
+
+static void build_reach(const oc_level_desc* L, Reach* R) {
+    const int W = L->width, H = L->height, N = W * H;
+    static const int opp[4] = {1, 0, 3, 2};
+    int adj[RG_N][8], deg[RG_N];
+    memset(R->exists, 0, sizeof(R->exists));
+    memset(deg, 0, sizeof(deg));
+    for (int c = 0; c < N; ++c) {
+        const int x = c % W, y = c / W, coll = L->tiles[c] != OC_TILE_FLOOR;
+        if (!coll) R->exists[c * 5 + 4] = 1;
+        for (int d = 0; d < 4; ++d) {
+            int nx = x + NAV[d].x, ny = y + NAV[d].y;
+            nx = nx < 0 ? 0 : (nx > W - 1 ? W - 1 : nx);
+            ny = ny < 0 ? 0 : (ny > H - 1 ? H - 1 : ny);
+            const int nc = ny * W + nx, ncoll = L->tiles[nc] != OC_TILE_FLOOR;
+            if (coll && !ncoll) R->exists[c * 5 + d] = 1;
+            (void)opp;
+        }
+    }
+    for (int c = 0; c < N; ++c) { /* edges (undirected; the reference's insertion order does not matter) */
+        const int x = c % W, y = c / W, coll = L->tiles[c] != OC_TILE_FLOOR;
+        for (int d = 0; d < 4; ++d) {
+            int nx = x + NAV[d].x, ny = y + NAV[d].y;
+            nx = nx < 0 ? 0 : (nx > W - 1 ? W - 1 : nx);
+            ny = ny < 0 ? 0 : (ny > H - 1 ? H - 1 : ny);
+            const int nc = ny * W + nx, ncoll = L->tiles[nc] != OC_TILE_FLOOR;
+            int u = -1, v = -1;
+            if (coll && !ncoll) { u = c * 5 + d; v = nc * 5 + 4; }            /* :96-100 */
+            else if (!coll && ncoll) { u = c * 5 + 4; v = nc * 5 + opp[d]; }  /* :101-104 */
+            else if (!coll && !ncoll) { u = c * 5 + 4; v = nc * 5 + 4; }      /* :105-107 */
+            if (u < 0 || !R->exists[u] || !R->exists[v] || u == v) continue;
+            int dup = 0;
+            for (int k = 0; k < deg[u]; ++k) dup |= adj[u][k] == v;
+            if (!dup) { adj[u][deg[u]++] = v; adj[v][deg[v]++] = u; }
+        }
+    }
+    for (int s0 = 0; s0 < RG_N; ++s0) {
+        for (int t0 = 0; t0 < RG_N; ++t0) R->dist[s0][t0] = -1;
+        if (!R->exists[s0]) continue;
+        int q[RG_N], qh = 0, qt = 0;
+        R->dist[s0][s0] = 0;
+        q[qt++] = s0;
+        while (qh < qt) {
+            const int u = q[qh++];
+            for (int k = 0; k < deg[u]; ++k) {
+                const int v = adj[u][k];
+                if (R->dist[s0][v] < 0) { R->dist[s0][v] = (int16_t)(R->dist[s0][u] + 1); q[qt++] = v; }
+            }
+        }
+    }
+}
+
+/* nx.shortest_path_length; -1 where the reference raises (node missing or no path) */
+static int rg_dist(const Reach* R, Loc a, int da, Loc b, int db, int W) {
+    const int u = (a.y * W + a.x) * 5 + da, v = (b.y * W + b.x) * 5 + db;
+    if (!R->exists[u] || !R->exists[v]) return -1;
+    return R->dist[u][v];
+}
+
+/* World.get_lower_bound_between_helper (world.py:148-264) + check_bound (:266-283) */
+static double lb_helper(const Env* e, const Reach* R, const oc_subtask* s, const Loc* agent_locs, Loc A, Loc B) {
+    const int W = e->L->width;
+    const double perimeter = 2.0 * (e->L->width + e->L->height);
+    double lower = perimeter + 1;
+    const int Acoll = collidable(gridsquare_at(e, A)), Bcoll = collidable(gridsquare_at(e, B));
+    const int nA = Acoll ? 4 : 1, nB = Bcoll ? 4 : 1;
+    for (int ia = 0; ia < nA; ++ia)
+        for (int ib = 0; ib < nB; ++ib) {
+            const int da = Acoll ? ia : 4, db = Bcoll ? ib : 4;
+            double bound;
+            if (s->num_agents == 1) {
+                const int b1 = rg_dist(R, agent_locs[0], 4, A, da, W);
+                const int b2 = rg_dist(R, A, da, B, db, W);
+                if (b1 < 0 || b2 < 0) continue; /* except: continue */
+                bound = b1 + b2 - 1;
+            } else {
+                int t;
+                const double b1A = (t = rg_dist(R, agent_locs[0], 4, A, da, W)) < 0 ? perimeter : t;
+                const double b2A = (t = rg_dist(R, agent_locs[1], 4, A, da, W)) < 0 ? perimeter : t;
+                double minA = b1A < b2A ? b1A : b2A;
+                const double man = fabs((double)A.x - B.x) + fabs((double)A.y - B.y); /* manhattan_dist -> float */
+                const double b1B = (t = rg_dist(R, agent_locs[0], 4, B, db, W)) < 0 ? perimeter : t;
+                const double b2B = (t = rg_dist(R, agent_locs[1], 4, B, db, W)) < 0 ? perimeter : t;
+                double minB = b1B < b2B ? b1B : b2B;
+                if (s->kind == OC_SUB_CHOP || s->kind == OC_SUB_DELIVER) {
+                    bound = minA + man - 1;
+                } else { /* Merge */
+                    if ((b1A == minA && b1B == minB) || (b2A == minA && b2B == minB)) {
+                        minA *= 2;
+                        minB *= 2;
+                    }
+                    bound = (minA > minB ? minA : minB) + (man - 1) / 2;
+                }
+            }
+            if (bound < lower) lower = bound;
+        }
+    return lower > 1 ? lower : 1;
+}
+
+/* get_lower_bound_for_subtask_given_objs (overcooked_environment.py:594-664) with
+ * get_AB_locs_given_objs (:480-589) and World.get_lower_bound_between (world.py:115-146) */
+static double lower_bound(const Env* e, const Reach* R, const oc_subtask* s) {
+    double penalty = 0.0;
+    Loc agent_locs[2];
+    int na = 0;
+    for (int a = 0; a < e->A; ++a) { /* sim_agents order */
+        int in = 0;
+        for (int i = 0; i < s->num_agents; ++i) in |= s->agent[i] == a;
+        if (!in || !e->active[a]) continue;
+        agent_locs[na++] = e->agents[a].location;
+        const int h = e->agents[a].holding;
+        if (h >= 0 && s->kind != OC_SUB_MERGE) {
+            const int m = obj_mask(&e->objs[h]);
+            if (m != s->start_mask[0] && m != s->goal_mask) penalty += 1.0;
+        }
+    }
+    if (penalty > 1) penalty = 1;
+    Loc Al[OC_MAX_ITEMS + 2], Bl[OC_MAX_CELLS];
+    int nAl = 0, nBl = 0;
+    /* get_object_locs(obj, is_held=False) + subtask agents holding obj */
+#define OBJ_LOCS(mask, out, n)                                                                    \
+    do {                                                                                          \
+        for (int i = 0; i < e->K; ++i)                                                            \
+            if (e->objs[i].alive && !e->objs[i].is_held && obj_mask(&e->objs[i]) == (mask))       \
+                out[n++] = e->objs[i].location;                                                   \
+        for (int a = 0; a < e->A; ++a) {                                                          \
+            int in = 0;                                                                           \
+            for (int q = 0; q < s->num_agents; ++q) in |= s->agent[q] == a;                       \
+            if (in && e->active[a] && e->agents[a].holding >= 0 &&                                \
+                obj_mask(&e->objs[e->agents[a].holding]) == (mask))                               \
+                out[n++] = e->agents[a].location;                                                 \
+        }                                                                                         \
+    } while (0)
+    if (s->kind == OC_SUB_CHOP || s->kind == OC_SUB_DELIVER) {
+        const int want = s->kind == OC_SUB_CHOP ? OC_TILE_CUTBOARD : OC_TILE_DELIVERY;
+        for (int c = 0; c < e->L->width * e->L->height; ++c) /* get_all_object_locs(Cutboard|Delivery) */
+            if (e->L->tiles[c] == want) { Bl[nBl].x = c % e->L->width; Bl[nBl].y = c / e->L->width; ++nBl; }
+        OBJ_LOCS(s->start_mask[0], Al, nAl);
+        if (s->kind == OC_SUB_DELIVER) { /* A_locs not already on a Delivery square */
+            int k = 0;
+            for (int i = 0; i < nAl; ++i) {
+                int in = 0;
+                for (int j = 0; j < nBl; ++j) in |= loc_eq(Al[i], Bl[j]);
+                if (!in) Al[k++] = Al[i];
+            }
+            nAl = k;
+        }
+    } else if (s->kind == OC_SUB_MERGE) {
+        OBJ_LOCS(s->start_mask[0], Al, nAl);
+        OBJ_LOCS(s->start_mask[1], Bl, nBl);
+    }
+#undef OBJ_LOCS
+    double lower = 2.0 * (e->L->width + e->L->height) + 1;
+    for (int i = 0; i < nAl; ++i)
+        for (int j = 0; j < nBl; ++j) {
+            const double b = lb_helper(e, R, s, agent_locs, Al[i], Bl[j]);
+            if (b < lower) lower = b;
+        }
+    return lower + penalty;
+}
+
+typedef struct {
+    Cfg c;
+    const Reach* R;
+    const uint8_t *sin, *act, *alloc;
+    uint8_t *sout, *flags;
+    const oc_subtask* subs;
+    float* lb;
+    int64_t b0, b1;
+} RollJob;
+
+static void* run_roll(void* p) {
+    RollJob* j = (RollJob*)p;
+    const int64_t P = j->c.pitch;
+    for (int64_t e = j->b0; e < j->b1; ++e) {
+        const oc_subtask* s = &j->subs[j->alloc ? j->alloc[e] : 0];
+        Env env;
+        int fl;
+        unpack(&j->c, j->sin, e, &env, &fl);
+        level0_view(&env, s);
+        int codes[2] = {OC_ACT_NOOP, OC_ACT_NOOP};
+        for (int i = 0; i < s->num_agents; ++i) {
+            const int c = j->act[s->agent[i] * P + e];
+            codes[i] = c > OC_ACT_NOOP ? OC_ACT_NOOP : c;
+        }
+        if (s->kind == OC_SUB_NONE) codes[0] = codes[1] = OC_ACT_NOOP; /* get_actions -> [(0, 0)] */
+        int out = action_legal(&env, s, codes) ? OC_ROLL_LEGAL : 0;
+        if (rollout_T(&env, s, codes)) out |= OC_ROLL_ASSERT; /* the reference raised: no goal test */
+        else if (is_goal_state(&env, s)) out |= OC_ROLL_GOAL;
+        j->lb[e] = (float)lower_bound(&env, j->R, s);
+        j->flags[e] = (uint8_t)out;
+        pack(&j->c, &env, fl, j->sout, e);
+    }
+    return NULL;
+}
+
+int oco_rollout(const oc_level_desc* L, int A, int K, const uint8_t* sin, uint8_t* sout, const uint8_t* act,
+                const uint8_t* alloc, const oc_subtask* subs, int nsub, uint8_t* flags, float* lb, int64_t B,
+                int64_t pitch, int nthreads) {
+    if (nsub < 1) return -1;
+    for (int i = 0; i < nsub; ++i) {
+        if (subs[i].num_agents < 1 || subs[i].num_agents > 2) return -1;
+        for (int q = 0; q < subs[i].num_agents; ++q)
+            if (subs[i].agent[q] >= A) return -1;
+        if (subs[i].num_agents == 2 && subs[i].agent[0] >= subs[i].agent[1]) return -1;
+    }
+    Reach* R = (Reach*)malloc(sizeof(Reach));
+    build_reach(L, R);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    pthread_t th[64];
+    RollJob jobs[64];
+    for (int t = 0; t < nthreads; ++t) {
+        RollJob* j = &jobs[t];
+        j->c.L = L; j->c.A = A; j->c.K = K; j->c.max_T = 0; j->c.pitch = pitch;
+        j->R = R; j->sin = sin; j->act = act; j->alloc = alloc; j->sout = sout; j->flags = flags;
+        j->subs = subs; j->lb = lb;
+        j->b0 = B * t / nthreads;
+        j->b1 = B * (t + 1) / nthreads;
+        pthread_create(&th[t], NULL, run_roll, j);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    free(R);
+    return 0;
 }

@@ -40,6 +40,9 @@ def lib() -> ctypes.CDLL:
         L.oco_reset.argtypes = [ctypes.POINTER(capi.OcLevelDesc), i32, i32, vp, i64, i64]
         L.oco_gen_actions.restype = ctypes.c_int
         L.oco_gen_actions.argtypes = [i32, vp, i64, i64, i64, i64, u64]
+        L.oco_rollout.restype = ctypes.c_int
+        L.oco_rollout.argtypes = [ctypes.POINTER(capi.OcLevelDesc), i32, i32, vp, vp, vp, vp,
+                                  ctypes.POINTER(capi.OcSubtask), i32, vp, vp, i64, i64, i32]
         L.oco_action_code.restype = ctypes.c_uint8
         L.oco_action_code.argtypes = [u64, u64, u64, u64]
         _lib = L
@@ -77,6 +80,16 @@ class OracleBatch:
         rc = lib().oco_step(ctypes.byref(self.desc), self.A, self.K, self.max_T, _p(sin), _p(sout),
                             _p(actions), _p(exec_out), _p(coll), self.B, self.pitch, nthreads)
         assert rc == 0
+
+    def rollout(self, sin, sout, actions, subtasks, alloc=None, nthreads=8):
+        """Planner rollout rows (oco_rollout): returns (flags u8 [B], lower bound f32 [B])."""
+        subs = capi.subtask_array(subtasks)
+        flags = np.zeros(self.pitch, np.uint8)
+        lb = np.zeros(self.pitch, np.float32)
+        rc = lib().oco_rollout(ctypes.byref(self.desc), self.A, self.K, _p(sin), _p(sout), _p(actions),
+                               _p(alloc), subs, len(subtasks), _p(flags), _p(lb), self.B, self.pitch, nthreads)
+        assert rc == 0, rc
+        return flags[:self.B], lb[:self.B]
 
     def gen_actions(self, actions, env_offset, step, seed) -> None:
         rc = lib().oco_gen_actions(self.A, _p(actions), self.B, self.pitch, env_offset, step, seed)

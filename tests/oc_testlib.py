@@ -187,3 +187,103 @@ def compare_group(group: EpisodeGroup, step_fn, init_state: np.ndarray, pitch: i
 def _eq(c, b, exp) -> bool:
     return (int(c["t"][b]) == int(exp["t"]) and int(c["flags"][b]) == int(exp["flags"])
             and np.array_equal(c["agents"][b], exp["agents"]) and np.array_equal(c["items"][b], exp["items"]))
+
+
+def state_from_canonical(level, A: int, K: int, pitch: int, agents: np.ndarray, items: np.ndarray,
+                         t: np.ndarray) -> np.ndarray:
+    """Engine-layout state buffer whose env b has the canonical state (agents [B,4,3], items
+    [B,4,4], t [B]): items take slots in canonical order, and each holding agent holds the
+    held item at its location with its held mask."""
+    B = len(agents)
+    P = capi.layout_planes(A, K)
+    s = np.zeros(P["num_planes"] * pitch, np.uint8)
+    v = planes_view(s, A, K, pitch)
+    v["il"][:] = 0xFF
+    v["ah"][:] = 0xFF
+    W = level.width
+    for b in range(B):
+        held_slots = []
+        for j in range(4):
+            m, x, y, h = (int(c) for c in items[b, j])
+            if m == PAD:
+                continue
+            v["il"][j, b], v["im"][j, b] = y * W + x, m
+            if h:
+                held_slots.append((j, x, y, m))
+        for a in range(A):
+            x, y, hm = (int(c) for c in agents[b, a])
+            v["ax"][a, b], v["ay"][a, b] = x, y
+            if hm not in (0, PAD):
+                for i, (j, ix, iy, m) in enumerate(held_slots):
+                    if (ix, iy, m) == (x, y, hm):
+                        v["ah"][a, b] = j
+                        held_slots.pop(i)
+                        break
+                else:
+                    raise AssertionError("no held item for agent %d of env %d" % (a, b))
+        v["t"][b] = t[b]
+    return s
+
+
+class RolloutRows:
+    """Rows of tests/golden/rollout.npz for one (level, A) config, with their subtask table."""
+
+    def __init__(self, fx, cfg: int, limit=None):
+        sel = np.nonzero(fx["cfg"] == cfg)[0]
+        if limit is not None and len(sel) > limit:
+            sel = sel[np.linspace(0, len(sel) - 1, limit).astype(int)]
+        self.idx = sel
+        self.level = levels.load_level(str(fx["cfg_level"][cfg]))
+        self.A = int(fx["cfg_A"][cfg])
+        self.K = capi.item_slots(self.level)
+        st = fx["state"][sel]
+        self.agents, self.items, self.t = fx["st_agents"][st], fx["st_items"][st], fx["st_t"][st]
+        self.B = len(sel)
+        keys, self.alloc = {}, np.zeros(self.B, np.uint8)
+        self.subtasks = []
+        for r, i in enumerate(sel):
+            n = int((fx["agents"][i] != PAD).sum())
+            key = (int(fx["kind"][i]), tuple(int(a) for a in fx["agents"][i][:n]),
+                   tuple(int(m) for m in fx["start"][i]), int(fx["goal_mask"][i]), int(fx["goal_count"][i]))
+            if key not in keys:
+                keys[key] = len(self.subtasks)
+                self.subtasks.append(capi.subtask(key[0], key[1], key[2], key[3], key[4]))
+            self.alloc[r] = keys[key]
+        self.sub_agents = [tuple(int(a) for a in fx["agents"][i] if a != PAD) for i in sel]
+        self.codes = fx["action"][sel]
+        self.exp_flags = (fx["legal"][sel] * capi.ROLL_LEGAL | fx["goal"][sel] * capi.ROLL_GOAL
+                          | fx["assert_"][sel] * capi.ROLL_ASSERT).astype(np.uint8)
+        self.exp_lb = fx["lb"][sel]
+        self.exp_next = fx["next"][sel]
+        self.exp_vl, self.exp_vu = fx["v_l"][sel], fx["v_u"][sel]
+
+    def actions(self, pitch: int) -> np.ndarray:
+        a = np.full((self.A, pitch), 4, np.uint8)
+        for r in range(self.B):
+            for q, ag in enumerate(self.sub_agents[r]):
+                a[ag, r] = self.codes[r, q]
+        return a.reshape(-1)
+
+    def compare(self, sout: np.ndarray, flags: np.ndarray, lb: np.ndarray, pitch: int):
+        """Mismatch descriptions of a rollout output against the reference rows."""
+        errs = []
+        c = canonical(sout, self.A, self.K, pitch, self.level.width, self.B)
+        for r in range(self.B):
+            if flags[r] != self.exp_flags[r]:
+                errs.append("row %d: flags %d vs %d" % (self.idx[r], flags[r], self.exp_flags[r]))
+                continue
+            if self.exp_flags[r] & capi.ROLL_ASSERT:
+                continue
+            if float(lb[r]) != float(self.exp_lb[r]):
+                errs.append("row %d: lb %r vs %r" % (self.idx[r], float(lb[r]), float(self.exp_lb[r])))
+            exp_ag = self.exp_next[r][:12].reshape(4, 3)
+            exp_it = self.exp_next[r][12:].reshape(4, 4)
+            for a in self.sub_agents[r]:
+                if not np.array_equal(c["agents"][r, a], exp_ag[a]):
+                    errs.append("row %d: agent %d %s vs %s" % (self.idx[r], a, c["agents"][r, a].tolist(),
+                                                               exp_ag[a].tolist()))
+            if not np.array_equal(c["items"][r], exp_it):
+                errs.append("row %d: items %s vs %s" % (self.idx[r], c["items"][r].tolist(), exp_it.tolist()))
+            if len(errs) > 20:
+                break
+        return errs
