@@ -95,6 +95,62 @@ def measure_fused(eb, acts, n, dev, world) -> dict:
             "outputs": "every step's state (trajectory), executed actions and collision mask written"}
 
 
+# Salad recipe subtasks (recipe_planner: Chop x2, Merge x6, Deliver) as oc_subtask masks:
+# (kind, start masks, goal mask); agents are filled in per allocation.
+SALAD_SUBTASKS = [(1, (0x01, 0), 0x11), (1, (0x02, 0), 0x22),
+                  (2, (0x11, 0x22), 0x33), (2, (0x11, 0x08), 0x19), (2, (0x22, 0x08), 0x2A),
+                  (2, (0x33, 0x08), 0x3B), (2, (0x19, 0x22), 0x3B), (2, (0x2A, 0x11), 0x3B),
+                  (3, (0x3B, 0), 0x3B)]
+
+
+def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 20) -> dict:
+    """Secondary line, config C5: navigation-planner rollout rows (oc_rollout) on
+    full-divider_salad with 4 agents.  Row states are mid-episode random-play states; each
+    row gets a random (subtask, 1-2 agent) allocation out of the Salad subtasks x every agent
+    set, and a random joint action.  Algorithmic bytes per row: 2S(4) + 4 actions
+    + 1 alloc id + 4 f32 bound = 55 (+1 flags byte written)."""
+    import itertools
+    from gym_cooking_amd import capi
+    from gym_cooking_amd.engine import OvercookedBatch
+    A = 4
+    eb = OvercookedBatch("full-divider_salad", A, rows, max_T=100, device=dev)
+    s, s2 = eb.new_state(), eb.new_state()
+    eb.reset(s)
+    a = eb.new_actions()
+    for t in range(37):
+        eb.gen_actions(a, t, 11)
+        eb.step(s, s2, a)
+        s, s2 = s2, s
+    agent_sets = [(i,) for i in range(A)] + list(itertools.combinations(range(A), 2))
+    table = [capi.subtask(k, ags, st, g, 0) for (k, st, g) in SALAD_SUBTASKS for ags in agent_sets]
+    table = table[:capi.MAX_SUBTASKS]
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    alloc = torch.randint(0, len(table), (eb.pitch,), dtype=torch.uint8, device=dev, generator=gen)
+    eb.gen_actions(a, 99, 12)
+    out = eb.new_state()
+    flags = torch.empty(eb.pitch, dtype=torch.uint8, device=dev)
+    lb = torch.empty(eb.pitch, dtype=torch.float32, device=dev)
+    for _ in range(2):
+        eb.rollout(s, out, a, table, alloc, flags, lb)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        eb.rollout(s, out, a, table, alloc, flags, lb)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
+    nbytes = 55 * rows
+    legal = int((flags[:rows] & capi.ROLL_LEGAL).ne(0).sum())
+    return {"value": world * rows / (ms * 1e-3), "unit": "rollout rows/s", "rows_per_gpu": rows,
+            "ms_per_launch": ms, "kernel": "oc_rollout_kernel<4,4>",
+            "workload": "C5: full-divider_salad 4 agents, %d Salad (subtask, agents) configs, random joint actions"
+                        % len(table),
+            "algorithmic_bytes_per_row": 55, "achieved_GBs": nbytes / (ms * 1e-3) / 1e9,
+            "frac_hbm": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "legal_rows": legal}
+
+
 def load_traffic(path: str):
     try:
         with open(path) as f:
@@ -118,6 +174,7 @@ def main() -> int:
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="skip the secondary oc_step_n measurement")
+    ap.add_argument("--no-rollout", action="store_true", help="skip the secondary oc_rollout (C5) measurement")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -241,6 +298,8 @@ def main() -> int:
     }
     if not args.no_fused:
         line["fused_multi_step"] = measure_fused(eb, acts, n_act, dev, world)
+    if not args.no_rollout:
+        line["rollout"] = measure_rollout(dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget, threads)

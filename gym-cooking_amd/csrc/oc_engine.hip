@@ -22,6 +22,7 @@
 #include <string>
 
 #include "../../include/oc_engine.h"
+#include "oc_rollout.h"
 #include "oc_swar.h"
 
 namespace {
@@ -336,6 +337,80 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
     }
 }
 
+// Planner rollout (oc_rollout): one row per lane, scalar (oc_rollout.h).  Each block stages
+// the level's reachability distances, its tables and the subtask configurations in LDS, then
+// walks rows with a grid stride.  Rows are independent; byte-plane loads of 64 contiguous
+// bytes per wave instruction.
+struct RollArgs {
+    ocro::RollLevel L;
+    ocro::Sub subs[OC_MAX_SUBTASKS];
+    int32_t nsub;
+    int64_t pitch, B;
+};
+
+template <int A, int K>
+__global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const uint8_t* __restrict__ sin,
+                                                            uint8_t* __restrict__ sout,
+                                                            const uint8_t* __restrict__ act,
+                                                            const uint8_t* __restrict__ alloc,
+                                                            const uint8_t* __restrict__ dist_g,
+                                                            uint8_t* __restrict__ out_flags,
+                                                            float* __restrict__ lb) {
+    __shared__ uint32_t dist_w[ocro::kMaxNodes * ocro::kMaxNodes / 4];
+    __shared__ ocro::RollLevel Ls;
+    __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
+    const int nwords = R.L.nnodes * ocro::kMaxNodes / 4;  // rows 0..nnodes-1 of the table
+    for (int i = threadIdx.x; i < nwords; i += kBlock) dist_w[i] = ((const uint32_t*)dist_g)[i];
+    if (threadIdx.x == 0) {
+        Ls = R.L;
+        for (int i = 0; i < R.nsub; ++i) subs[i] = R.subs[i];
+    }
+    __syncthreads();
+    const uint8_t* dist = (const uint8_t*)dist_w;
+    const int64_t P = R.pitch;
+    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
+        ocro::Row r;
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            r.x |= (uint32_t)sin[a * P + e] << (8 * a);
+            r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
+            r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            r.loc |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
+            r.mask |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
+        }
+        const uint16_t t = ((const uint16_t*)(sin + kPT * P))[e];
+        const uint8_t fl_in = sin[kPF * P + e];
+        const int ai = alloc != nullptr ? alloc[e] : 0;
+        float bound = 0.0f;
+        int f = OC_ROLL_BADALLOC;  // an alloc id past num_subtasks: the row is copied unchanged
+        if (ai < R.nsub) {
+            const ocro::Sub& s = subs[ai];
+            const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
+            ocro::RowOps<A, K> ops(Ls, dist);
+            f = ops.run(r, s, c0, c1, bound);
+        }
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            sout[a * P + e] = (uint8_t)r.ax(a);
+            sout[(kPY + a) * P + e] = (uint8_t)r.ay(a);
+            sout[(kPH + a) * P + e] = (uint8_t)r.ah(a);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            sout[(kPL + j) * P + e] = (uint8_t)r.il(j);
+            sout[(kPM + j) * P + e] = (uint8_t)r.im(j);
+        }
+        ((uint16_t*)(sout + kPT * P))[e] = t;
+        sout[kPF * P + e] = fl_in;
+        out_flags[e] = (uint8_t)f;
+        lb[e] = bound;
+    }
+}
+
 // reset(): broadcast the level template (overcooked_environment.py:201-250).
 template <int A, int K>
 __global__ __launch_bounds__(kBlock) void oc_reset_kernel(LevelArgs L, uint8_t* __restrict__ s) {
@@ -471,6 +546,8 @@ struct oc_handle {
     int32_t A, K, max_T, device;
     int32_t blocks_per_cu;  // persistent step grid: blocks per CU (OC_BLOCKS_PER_CU, default 2)
     LevelArgs args;
+    ocro::RollLevel roll;       // planner rollout tables (nnodes < 0: graph too large)
+    uint8_t* roll_dist = nullptr;  // device: reachability distances [kMaxNodes][kMaxNodes]
 };
 
 // Statistics rows: one per block of the larger of the oc_step / oc_step_n grids.
@@ -559,11 +636,27 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
         if (v >= 1 && v <= 16) h->blocks_per_cu = v;
     }
     h->args = L;
+    // planner rollout: the static reachability graph's BFS table (world.py:67-108)
+    {
+        static uint8_t dist[ocro::kMaxNodes * ocro::kMaxNodes];
+        const int n = ocro::build_roll_level(h->roll, dist, W, H, lv->tiles);
+        if (n < 0) {
+            h->roll.nnodes = -1;
+        } else {
+            if (hipSetDevice(device) != hipSuccess ||
+                hipMalloc(&h->roll_dist, sizeof(dist)) != hipSuccess ||
+                hipMemcpy(h->roll_dist, dist, sizeof(dist), hipMemcpyHostToDevice) != hipSuccess) {
+                h->roll_dist = nullptr;  // no device (e.g. a CPU-only build check): rollout unavailable
+                (void)hipGetLastError();
+            }
+        }
+    }
     *out = h;
     return OC_OK;
 }
 
 int oc_destroy(oc_handle* h) {
+    if (h != nullptr && h->roll_dist != nullptr) (void)hipFree(h->roll_dist);
     delete h;
     return OC_OK;
 }
@@ -670,6 +763,52 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
         if (const int rc = hip_check("oc_step_n launch")) return rc;
     }
     return OC_OK;
+}
+
+int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
+               const uint8_t* alloc, const oc_subtask* subtasks, int32_t num_subtasks, uint8_t* out_flags,
+               float* lower_bound, int64_t B, void* stream) {
+    if (h == nullptr || state_in == nullptr || state_out == nullptr || actions == nullptr || subtasks == nullptr ||
+        out_flags == nullptr || lower_bound == nullptr || B < 0)
+        return fail(OC_EINVAL, "bad argument");
+    if (num_subtasks < 1 || num_subtasks > OC_MAX_SUBTASKS) return fail(OC_EINVAL, "num_subtasks %d", num_subtasks);
+    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes", ocro::kMaxNodes);
+    if (h->roll_dist == nullptr) return fail(OC_EHIP, "rollout tables not on the device");
+    if (state_in == state_out) return fail(OC_EINVAL, "oc_rollout is out of place");
+    if (((uintptr_t)lower_bound & 3u) || ((uintptr_t)state_in & 1u) || ((uintptr_t)state_out & 1u))
+        return fail(OC_EINVAL, "misaligned buffer");
+    RollArgs R;
+    R.L = h->roll;
+    R.nsub = num_subtasks;
+    R.pitch = pitch_for(B);
+    R.B = B;
+    for (int i = 0; i < num_subtasks; ++i) {
+        const oc_subtask& s = subtasks[i];
+        if (s.kind < OC_SUB_NONE || s.kind > OC_SUB_DELIVER) return fail(OC_EINVAL, "subtask %d kind %d", i, s.kind);
+        if (s.num_agents < 1 || s.num_agents > 2) return fail(OC_EINVAL, "subtask %d: %d agents", i, s.num_agents);
+        for (int q = 0; q < s.num_agents; ++q)
+            if (s.agent[q] >= h->A) return fail(OC_EINVAL, "subtask %d: agent %d", i, s.agent[q]);
+        if (s.num_agents == 2 && s.agent[0] >= s.agent[1]) return fail(OC_EINVAL, "subtask %d: agents not ascending", i);
+        ocro::Sub& d = R.subs[i];
+        d.kind = s.kind;
+        d.n = s.num_agents;
+        d.agent[0] = s.agent[0];
+        d.agent[1] = s.num_agents == 2 ? s.agent[1] : s.agent[0];
+        d.start[0] = s.start_mask[0];
+        d.start[1] = s.start_mask[1];
+        d.goal = s.goal_mask;
+        d.count = s.goal_count;
+        d.pad[0] = d.pad[1] = 0;
+    }
+    if (B == 0) return OC_OK;
+    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)kCUs * 8;
+    const dim3 grid((unsigned)(need < cap ? need : cap));
+    hipStream_t st = (hipStream_t)stream;
+#define OC_LAUNCH_ROLL(A, K)                                                                                 \
+    hipLaunchKernelGGL((oc_rollout_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state_in,  \
+                       (uint8_t*)state_out, actions, alloc, h->roll_dist, out_flags, lower_bound)
+    OC_DISPATCH(h->A, h->K, OC_LAUNCH_ROLL)
+    return hip_check("oc_rollout launch");
 }
 
 int oc_gen_actions(const oc_handle* h, uint8_t* actions, int64_t B, int64_t env_offset, int64_t step,

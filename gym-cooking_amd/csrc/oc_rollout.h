@@ -1,0 +1,397 @@
+// oc_rollout.h -- one navigation-planner rollout row, scalar per lane.
+//
+// A row is (state, planner configuration, action).  Everything here follows the reference
+// planner as restated in include/oc_engine.h's rollout section:
+//   level0()        E2E_BRTDP._configure_planner_level, LEVEL0   e2e_brtdp.py:389-406
+//   interact()      utils/interact.py:4-89 (the same rules as ocsw::step4, one env)
+//   action_legal()  get_actions / get_single_actions      e2e_brtdp.py:151-206, nav utils.py:55-90
+//   is_goal()       _define_goal_state                   e2e_brtdp.py:435-566
+//   lower_bound()   get_lower_bound_for_subtask_given_objs  overcooked_environment.py:480-664,
+//                   World.get_lower_bound_between(_helper), check_bound  world.py:115-283
+// The reachability graph of the static level (world.py:67-108) is precomputed by
+// build_roll_level() as a compact all-pairs distance table (u8, 0xFF = no path); the kernel
+// stages it in LDS.  Distances and bounds are exact in fp32 (integers and halves < 2^8).
+//
+// The includer defines __host__ / __device__ (HIP, or empty for the host test harness).
+#pragma once
+
+#include <stdint.h>
+
+#define OC_RH __host__ __device__ inline
+
+namespace ocro {
+
+constexpr int kMaxNodes = 160;  // compact reachability-graph nodes (LDS table kMaxNodes^2 bytes)
+constexpr uint8_t kNone = 0xFF;
+constexpr int kFloor = 0, kCounter = 1, kCutboard = 2, kDelivery = 3;  // OC_TILE_*
+constexpr int kNoop = 4;
+constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NAV_ACTIONS + (0, 0)
+
+struct RollLevel {
+    int32_t W, H, perimeter, nnodes;
+    uint64_t cut_cells, deliv_cells;  // static Cutboard / Delivery squares
+    uint8_t tile[64];                 // static tile class per cell
+    uint8_t node[64 * 5];             // cell * 5 + approach direction (4 = (0, 0)) -> compact node or kNone
+};
+
+struct Sub {  // oc_subtask, device copy
+    int32_t kind, n;
+    uint8_t agent[2], start[2], goal, count, pad[2];
+};
+
+// One row's state, packed so that run-time slot / agent indices are shifts, not memory:
+// agent a in byte a of x, y, h (h = held slot or kNone); slot j in byte j of loc, mask.
+struct Row {
+    uint32_t x = 0, y = 0, h = 0;
+    uint64_t loc = 0, mask = 0;
+    static OC_RH uint32_t b32(uint32_t w, int i) { return (w >> (8 * i)) & 0xFFu; }
+    static OC_RH uint32_t b64(uint64_t w, int i) { return (uint32_t)(w >> (8 * i)) & 0xFFu; }
+    static OC_RH void s32(uint32_t& w, int i, uint32_t v) { w = (w & ~(0xFFu << (8 * i))) | (v << (8 * i)); }
+    static OC_RH void s64(uint64_t& w, int i, uint32_t v) {
+        w = (w & ~(0xFFull << (8 * i))) | ((uint64_t)v << (8 * i));
+    }
+    OC_RH int ax(int a) const { return (int)b32(x, a); }
+    OC_RH int ay(int a) const { return (int)b32(y, a); }
+    OC_RH int ah(int a) const { return (int)b32(h, a); }
+    OC_RH int il(int j) const { return (int)b64(loc, j); }
+    OC_RH int im(int j) const { return (int)b64(mask, j); }
+};
+
+// ---- host: level tables --------------------------------------------------------------------
+// Builds the reachability graph of make_reachability_graph (world.py:67-108) and its BFS
+// distances.  Returns the node count, or -1 when it exceeds kMaxNodes.
+inline int build_roll_level(RollLevel& L, uint8_t* dist /* kMaxNodes^2 */, int W, int H, const uint8_t* tiles) {
+    L.W = W;
+    L.H = H;
+    L.perimeter = 2 * (W + H);
+    L.cut_cells = L.deliv_cells = 0;
+    for (int c = 0; c < 64; ++c) {
+        L.tile[c] = c < W * H ? tiles[c] : (uint8_t)kCounter;
+        if (c < W * H && tiles[c] == kCutboard) L.cut_cells |= 1ull << c;
+        if (c < W * H && tiles[c] == kDelivery) L.deliv_cells |= 1ull << c;
+    }
+    for (int i = 0; i < 64 * 5; ++i) L.node[i] = kNone;
+    int n = 0;
+    auto clampx = [&](int v) { return v < 0 ? 0 : (v > W - 1 ? W - 1 : v); };
+    auto clampy = [&](int v) { return v < 0 ? 0 : (v > H - 1 ? H - 1 : v); };
+    for (int c = 0; c < W * H; ++c) {
+        const int x = c % W, y = c / W;
+        const bool coll = tiles[c] != kFloor;
+        if (!coll) {
+            if (n >= kMaxNodes) return -1;
+            L.node[c * 5 + 4] = (uint8_t)n++;
+        }
+        for (int d = 0; d < 4; ++d) {
+            const int nc = clampy(y + kDY[d]) * W + clampx(x + kDX[d]);
+            if (coll && tiles[nc] == kFloor) {
+                if (n >= kMaxNodes) return -1;
+                L.node[c * 5 + d] = (uint8_t)n++;
+            }
+        }
+    }
+    L.nnodes = n;
+    // adjacency (undirected): floor-floor, and a collidable square's approach node with the
+    // floor it is approached from
+    static const int opp[4] = {1, 0, 3, 2};
+    uint8_t adj[kMaxNodes][8];
+    int deg[kMaxNodes] = {0};
+    auto link = [&](int u, int v) {
+        if (u == kNone || v == kNone || u == v) return;
+        for (int k = 0; k < deg[u]; ++k)
+            if (adj[u][k] == v) return;
+        adj[u][deg[u]++] = (uint8_t)v;
+        adj[v][deg[v]++] = (uint8_t)u;
+    };
+    for (int c = 0; c < W * H; ++c) {
+        const int x = c % W, y = c / W;
+        const bool coll = tiles[c] != kFloor;
+        for (int d = 0; d < 4; ++d) {
+            const int nc = clampy(y + kDY[d]) * W + clampx(x + kDX[d]);
+            const bool ncoll = tiles[nc] != kFloor;
+            if (coll && !ncoll) link(L.node[c * 5 + d], L.node[nc * 5 + 4]);
+            else if (!coll && ncoll) link(L.node[c * 5 + 4], L.node[nc * 5 + opp[d]]);
+            else if (!coll && !ncoll) link(L.node[c * 5 + 4], L.node[nc * 5 + 4]);
+        }
+    }
+    for (int s = 0; s < n; ++s) {
+        uint8_t* row = dist + s * kMaxNodes;
+        for (int t = 0; t < kMaxNodes; ++t) row[t] = kNone;
+        int q[kMaxNodes], qh = 0, qt = 0;
+        row[s] = 0;
+        q[qt++] = s;
+        while (qh < qt) {
+            const int u = q[qh++];
+            for (int k = 0; k < deg[u]; ++k) {
+                const int v = adj[u][k];
+                if (row[v] == kNone) {
+                    row[v] = (uint8_t)(row[u] + 1);
+                    q[qt++] = v;
+                }
+            }
+        }
+    }
+    return n;
+}
+
+// ---- row logic ----------------------------------------------------------------------------
+template <int A, int K>
+struct RowOps {
+    const RollLevel& L;
+    const uint8_t* dist;  // LDS on the device
+    uint64_t ac = 0;      // AgentCounter cells of this row's Level-0 view
+    uint32_t active = 0;  // bit a: agent a is a subtask agent
+
+    OC_RH RowOps(const RollLevel& l, const uint8_t* d) : L(l), dist(d) {}
+
+    OC_RH int tile(int cell) const { return (ac >> cell) & 1u ? kCounter : L.tile[cell]; }
+    OC_RH int cell(int x, int y) const { return y * L.W + x; }
+    OC_RH int agent_cell(const Row& r, int a) const { return cell(r.ax(a), r.ay(a)); }
+
+    // level0: agents outside the subtask freeze into AgentCounters; their items leave
+    OC_RH void level0(Row& r, const Sub& s) {
+        active = 0;
+        for (int i = 0; i < s.n; ++i) active |= 1u << s.agent[i];
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            if ((active >> a) & 1u) continue;
+            const int hh = r.ah(a);
+            if (hh != kNone) {
+                Row::s64(r.loc, hh, kNone);
+                Row::s64(r.mask, hh, 0);
+                Row::s32(r.h, a, kNone);
+            }
+            ac |= 1ull << agent_cell(r, a);
+        }
+    }
+
+    // the un-held item on a non-Floor square (at most one off Delivery), or -1
+    OC_RH int item_at(const Row& r, int c) const {
+        int o = -1;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (r.il(j) == c) o = j;
+        return o;
+    }
+
+    static OC_RH int ncontents(int m) { return __builtin_popcount((unsigned)m & 0x0Fu); }
+    static OC_RH bool deliverable(int m) { return ncontents(m) >= 2 && ((m & 7) & ~(m >> 4)) == 0; }
+    static OC_RH bool mergeable(int a, int b) {
+        const int u = a | b;
+        return !(a & b & 8) && ((u & 7) & ~(u >> 4)) == 0;
+    }
+    static OC_RH bool needs_chopped(int m) { return ncontents(m) == 1 && (m & 0x78) == 0; }
+
+    // interact(agent, world), play = False (utils/interact.py:4-89)
+    OC_RH void interact(Row& r, int a, int code) const {
+        if (code == kNoop) return;
+        int tx = r.ax(a) + kDX[code], ty = r.ay(a) + kDY[code];
+        tx = tx < 0 ? 0 : (tx > L.W - 1 ? L.W - 1 : tx);
+        ty = ty < 0 ? 0 : (ty > L.H - 1 ? L.H - 1 : ty);
+        const int tc = cell(tx, ty), t = tile(tc), h = r.ah(a);
+        if (t == kFloor) {  // move_to: the held item follows
+            Row::s32(r.x, a, (uint32_t)tx);
+            Row::s32(r.y, a, (uint32_t)ty);
+            if (h != kNone) Row::s64(r.loc, h, (uint32_t)tc);
+        } else if (h != kNone) {
+            const int hm = r.im(h);
+            if (t == kDelivery) {
+                if (deliverable(hm)) {
+                    Row::s64(r.loc, h, (uint32_t)tc);
+                    Row::s32(r.h, a, kNone);
+                }
+            } else {
+                const int o = item_at(r, tc);
+                if (o >= 0) {
+                    if (mergeable(hm, r.im(o))) {  // the holder's item absorbs o
+                        Row::s64(r.mask, h, (uint32_t)(hm | r.im(o)));
+                        Row::s64(r.loc, o, kNone);
+                        Row::s64(r.mask, o, 0);
+                    }
+                } else if (t == kCutboard && needs_chopped(hm)) {
+                    Row::s64(r.mask, h, (uint32_t)(hm | ((hm << 4) & 0x70)));
+                } else {  // put down
+                    Row::s64(r.loc, h, (uint32_t)tc);
+                    Row::s32(r.h, a, kNone);
+                }
+            }
+        } else if (t != kDelivery) {
+            const int o = item_at(r, tc);
+            if (o >= 0) {  // pick up: the item moves onto the agent
+                Row::s32(r.h, a, (uint32_t)o);
+                Row::s64(r.loc, o, (uint32_t)agent_cell(r, a));
+            }
+        }
+    }
+
+    // OvercookedEnvironment.is_collision (overcooked_environment.py:671-722): both execute
+    OC_RH bool no_collision(const Row& r, int i, int j, int ci, int cj) const {
+        const int lix = r.ax(i), liy = r.ay(i), ljx = r.ax(j), ljy = r.ay(j);
+        int nix = lix + kDX[ci], niy = liy + kDY[ci], njx = ljx + kDX[cj], njy = ljy + kDY[cj];
+        if (tile(cell(nix, niy)) != kFloor) { nix = lix; niy = liy; }
+        if (tile(cell(njx, njy)) != kFloor) { njx = ljx; njy = ljy; }
+        if (nix == njx && niy == njy) return false;  // every same-target branch blocks someone
+        return !(lix == njx && liy == njy && ljx == nix && ljy == niy);
+    }
+
+    // nav_utils.get_single_actions membership
+    OC_RH bool single_legal(const Row& r, int a, int code) const {
+        if (code == kNoop) return true;
+        int nx = r.ax(a) + kDX[code], ny = r.ay(a) + kDY[code];
+        nx = nx < 0 ? 0 : (nx > L.W - 1 ? L.W - 1 : nx);
+        ny = ny < 0 ? 0 : (ny > L.H - 1 ? L.H - 1 : ny);
+#pragma unroll
+        for (int b = 0; b < A; ++b)
+            if (((active >> b) & 1u) && r.ax(b) == nx && r.ay(b) == ny) return false;
+        const int c = cell(nx, ny), t = tile(c);
+        if (t == kFloor || t == kDelivery) return true;
+        const int o = item_at(r, c);
+        const int h = r.ah(a);
+        if (o < 0) return h != kNone;
+        return h == kNone || mergeable(r.im(h), r.im(o));
+    }
+
+    OC_RH bool action_legal(const Row& r, const Sub& s, int c0, int c1) const {
+        if (s.kind == 0) return c0 == kNoop && (s.n < 2 || c1 == kNoop);
+        if (!single_legal(r, s.agent[0], c0)) return false;
+        if (s.n < 2) return true;
+        return single_legal(r, s.agent[1], c1) && no_collision(r, s.agent[0], s.agent[1], c0, c1);
+    }
+
+    OC_RH bool is_goal(const Row& r, const Sub& s) const {
+        if (s.kind == 0) return true;
+        int count = 0;
+        uint64_t seen = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int c = r.il(j);
+            if (c == kNone || r.im(j) != s.goal) continue;
+            if (s.kind == 3) {  // un-held goal items on a Delivery square
+                count += (L.deliv_cells >> c) & 1u ? 1 : 0;
+            } else {  // distinct locations of goal items, held or not
+                count += (seen >> c) & 1u ? 0 : 1;
+                seen |= 1ull << c;
+            }
+        }
+        return count > s.count;
+    }
+
+    OC_RH int rg(int c1, int d1, int c2, int d2) const {  // nx.shortest_path_length or -1
+        const int u = L.node[c1 * 5 + d1], v = L.node[c2 * 5 + d2];
+        if (u == kNone || v == kNone) return -1;
+        const int d = dist[u * kMaxNodes + v];
+        return d == kNone ? -1 : d;
+    }
+
+    // World.get_lower_bound_between_helper (world.py:148-264) with check_bound (:266-283)
+    OC_RH float helper(const Sub& s, int ag0, int ag1, int Ac, int Bc) const {
+        const float per = (float)L.perimeter;
+        float lower = per + 1.0f;
+        const bool Acoll = tile(Ac) != kFloor, Bcoll = tile(Bc) != kFloor;
+        const int nA = Acoll ? 4 : 1, nB = Bcoll ? 4 : 1;
+        const int dx = Ac % L.W - Bc % L.W, dy = Ac / L.W - Bc / L.W;
+        const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
+        for (int ia = 0; ia < nA; ++ia)
+            for (int ib = 0; ib < nB; ++ib) {
+                const int da = Acoll ? ia : 4, db = Bcoll ? ib : 4;
+                float bound;
+                if (s.n == 1) {
+                    const int b1 = rg(ag0, 4, Ac, da), b2 = rg(Ac, da, Bc, db);
+                    if (b1 < 0 || b2 < 0) continue;
+                    bound = (float)(b1 + b2 - 1);
+                } else {
+                    int t;
+                    const float b1A = (t = rg(ag0, 4, Ac, da)) < 0 ? per : (float)t;
+                    const float b2A = (t = rg(ag1, 4, Ac, da)) < 0 ? per : (float)t;
+                    const float b1B = (t = rg(ag0, 4, Bc, db)) < 0 ? per : (float)t;
+                    const float b2B = (t = rg(ag1, 4, Bc, db)) < 0 ? per : (float)t;
+                    float mA = b1A < b2A ? b1A : b2A, mB = b1B < b2B ? b1B : b2B;
+                    if (s.kind == 1 || s.kind == 3) {
+                        bound = mA + man - 1.0f;
+                    } else {
+                        if ((b1A == mA && b1B == mB) || (b2A == mA && b2B == mB)) {
+                            mA *= 2.0f;
+                            mB *= 2.0f;
+                        }
+                        bound = (mA > mB ? mA : mB) + (man - 1.0f) * 0.5f;
+                    }
+                }
+                if (bound < lower) lower = bound;
+            }
+        return lower > 1.0f ? lower : 1.0f;
+    }
+
+    // Locations of `m` as get_AB_locs_given_objs lists them: un-held items (slot order) then
+    // subtask agents holding one; `skip_deliv` drops Delivery squares (Deliver's A_locs).
+    template <class F>
+    OC_RH void visit_objs(const Row& r, int m, bool skip_deliv, F&& f) const {
+        uint32_t held = 0;
+#pragma unroll
+        for (int a = 0; a < A; ++a)
+            if (r.ah(a) != kNone) held |= 1u << r.ah(a);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int c = r.il(j);
+            if (c == kNone || r.im(j) != m || ((held >> j) & 1u)) continue;
+            if (skip_deliv && ((L.deliv_cells >> c) & 1u)) continue;
+            f(c);
+        }
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            const int h = r.ah(a);
+            if (!((active >> a) & 1u) || h == kNone || r.im(h) != m) continue;
+            const int c = agent_cell(r, a);
+            if (skip_deliv && ((L.deliv_cells >> c) & 1u)) continue;
+            f(c);
+        }
+    }
+
+    // get_lower_bound_for_subtask_given_objs (overcooked_environment.py:594-664)
+    OC_RH float lower_bound(const Row& r, const Sub& s) const {
+        float pen = 0.0f;
+        int ag0 = 0, ag1 = 0, na = 0;
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            if (!((active >> a) & 1u)) continue;
+            if (na == 0) ag0 = agent_cell(r, a); else ag1 = agent_cell(r, a);
+            ++na;
+            const int h = r.ah(a);
+            if (h != kNone && s.kind != 2 && r.im(h) != s.start[0] && r.im(h) != s.goal) pen = 1.0f;
+        }
+        float lower = (float)L.perimeter + 1.0f;
+        if (s.kind == 1 || s.kind == 3) {
+            const uint64_t bset = s.kind == 1 ? L.cut_cells : L.deliv_cells;
+            visit_objs(r, s.start[0], s.kind == 3, [&](int Ac) {
+                for (uint64_t m = bset; m; m &= m - 1) {
+                    const float b = helper(s, ag0, ag1, Ac, __builtin_ctzll(m));
+                    if (b < lower) lower = b;
+                }
+            });
+        } else if (s.kind == 2) {
+            visit_objs(r, s.start[0], false, [&](int Ac) {
+                visit_objs(r, s.start[1], false, [&](int Bc) {
+                    const float b = helper(s, ag0, ag1, Ac, Bc);
+                    if (b < lower) lower = b;
+                });
+            });
+        }
+        return lower + pen;
+    }
+
+    // The whole row: returns OC_ROLL_* flags; r becomes the Level-0 next state.
+    OC_RH int run(Row& r, const Sub& s, int c0, int c1, float& lb) {
+        level0(r, s);
+        if (s.kind == 0) c0 = c1 = kNoop;
+        c0 = c0 > kNoop ? kNoop : c0;
+        c1 = c1 > kNoop ? kNoop : c1;
+        int fl = action_legal(r, s, c0, c1) ? 1 : 0;
+        interact(r, s.agent[0], c0);
+        if (s.n == 2) interact(r, s.agent[1], c1);
+        const bool asserted = s.n == 2 && agent_cell(r, s.agent[0]) == agent_cell(r, s.agent[1]);
+        if (asserted) fl |= 4;
+        else if (is_goal(r, s)) fl |= 2;
+        lb = lower_bound(r, s);
+        return fl;
+    }
+};
+
+}  // namespace ocro

@@ -136,6 +136,24 @@ class OvercookedBatch:
                                       _ptr(exec_out), _ptr(coll), _ptr(stats), self.B, n, self._stream()))
         return state_out
 
+    def rollout(self, state_in: torch.Tensor, state_out: torch.Tensor, actions: torch.Tensor, subtasks,
+                alloc: Optional[torch.Tensor] = None, flags: Optional[torch.Tensor] = None,
+                lower_bound: Optional[torch.Tensor] = None):
+        """Navigation-planner rollout rows (oc_rollout): the Level-0 next state of every row
+        under its subtask configuration, and (flags u8 [pitch], lower bound f32 [pitch])."""
+        self._check(state_in, self.layout.state_bytes)
+        self._check(state_out, self.layout.state_bytes)
+        self._check(actions, self.A * self.pitch)
+        if alloc is not None:
+            self._check(alloc, self.pitch)
+        flags = torch.empty(self.pitch, dtype=torch.uint8, device=self.device) if flags is None else flags
+        lower_bound = (torch.empty(self.pitch, dtype=torch.float32, device=self.device)
+                       if lower_bound is None else lower_bound)
+        subs = capi.subtask_array(subtasks)
+        capi.check(self.lib.oc_rollout(self._h, _ptr(state_in), _ptr(state_out), _ptr(actions), _ptr(alloc), subs,
+                                       len(subtasks), _ptr(flags), _ptr(lower_bound), self.B, self._stream()))
+        return flags, lower_bound
+
     def gen_actions(self, actions: torch.Tensor, step: int, seed: int = 0, env_offset: int = 0) -> torch.Tensor:
         self._check(actions, self.A * self.pitch)
         capi.check(self.lib.oc_gen_actions(self._h, _ptr(actions), self.B, env_offset, step, seed, self._stream()))

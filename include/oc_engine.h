@@ -214,6 +214,7 @@ typedef struct {
 #define OC_ROLL_GOAL 0x02   /* is_goal_state(T(state, action)); 0 on OC_ROLL_ASSERT rows */
 #define OC_ROLL_ASSERT 0x04 /* joint: the two agents end co-located (the reference's
                                AssertionError at e2e_brtdp.py:143; state_out still written) */
+#define OC_ROLL_BADALLOC 0x80 /* alloc id >= num_subtasks: row copied unchanged, bound 0 */
 
 /* One rollout transition per row e < B:
  *   state_in   : states in the oc_layout (real or already Level-0 states)

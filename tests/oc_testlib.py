@@ -257,6 +257,22 @@ class RolloutRows:
         self.exp_next = fx["next"][sel]
         self.exp_vl, self.exp_vu = fx["v_l"][sel], fx["v_u"][sel]
 
+    def split(self, max_sub: int = 64) -> List["RolloutRows"]:
+        """The rows as chunks of at most `max_sub` subtask configurations (one oc_rollout call each)."""
+        out = []
+        for c0 in range(0, len(self.subtasks), max_sub):
+            sel = np.nonzero((self.alloc >= c0) & (self.alloc < c0 + max_sub))[0]
+            part = object.__new__(RolloutRows)
+            part.__dict__ = dict(self.__dict__)
+            for k in ("idx", "agents", "items", "t", "codes", "exp_flags", "exp_lb", "exp_next", "exp_vl", "exp_vu"):
+                setattr(part, k, getattr(self, k)[sel])
+            part.sub_agents = [self.sub_agents[i] for i in sel]
+            part.alloc = (self.alloc[sel] - c0).astype(np.uint8)
+            part.subtasks = self.subtasks[c0:c0 + max_sub]
+            part.B = len(sel)
+            out.append(part)
+        return out
+
     def actions(self, pitch: int) -> np.ndarray:
         a = np.full((self.A, pitch), 4, np.uint8)
         for r in range(self.B):

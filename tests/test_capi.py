@@ -14,7 +14,8 @@ HEADER = os.path.join(tl.ROOT, "include", "oc_engine.h")
 
 def _declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(oc_[a-z_]+)\s*\(", src)))
+    decl = r"^(?:int|void|const char\s*\*)\s*\*?\s*(oc_[a-z_]+)\s*\("  # function declarations
+    return sorted(set(re.findall(decl, src, re.M)))
 
 
 def test_header_declarations_match_binding():
