@@ -3,11 +3,17 @@
 
 Workload (BASELINE configs[1]/[3]): partial-divider_salad, 2 agents, 2^20 envs per GPU,
 synthetic i.i.d. uniform actions from the counter RNG (materialised in HBM before the timed
-region, one buffer per step), max_T = 100 with next-step auto-reset.  A "step" = one
-oc_step launch over the whole per-GPU batch: reads the 17-B state + 2 action bytes per env,
-writes the next state, the executed actions, the collision mask and per-block episode
-statistics.  The K timed steps are replayed from a hipGraph (launch-bound loop), bracketed by
-a barrier + synchronize; the episode summaries are all-gathered (RCCL) inside the window.
+region, one buffer per step), max_T = 100 with next-step auto-reset.
+
+A "step" is one pass of the env transition over the whole per-GPU batch.  Every step reads
+that step's actions and writes the step's full next state, executed actions and collision
+mask to HBM, and accumulates the episode statistics.  The headline runs the K timed steps as
+multi-step launches (oc_step_n, <= 100 steps per launch; the state stays in registers
+between the steps of a launch, SURVEY 8(d) "a multi-step launch that still writes every
+step's state"), with its own algorithmic bytes per env-step S*launches/K + S + 2A + 1.
+The one-launch-per-step path (oc_step in a hipGraph, 2S + 2A + 1 bytes) is reported beside it
+as "per_step_launch".  The timed region is bracketed by a barrier + synchronize on both
+sides; the per-GPU episode summaries are all-gathered (RCCL) inside it.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -61,38 +67,6 @@ def cpu_baseline(level_name: str, A: int, B: int, max_T: int, budget_s: float, t
     return {"value": B * steps / t_step, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": "%d envs x %d steps of %s %d-agent (oracle/oc_oracle.c, %d threads)"
                       % (B, steps, level_name, A, threads)}
-
-
-def measure_fused(eb, acts, n, dev, world) -> dict:
-    """Secondary line: the same n steps as ONE oc_step_n call (state kept in registers between
-    steps), still writing every step's full state (trajectory), executed actions and collision
-    mask.  Algorithmic bytes per env-step: S/n (state in) + S (trajectory) + A (actions in) +
-    A (exec) + 1 (coll)."""
-    P, S, A = eb.pitch, eb.layout.state_bytes, eb.A
-    s0, out = eb.new_state(), eb.new_state()
-    eb.reset(s0)
-    traj = torch.empty(n * S, dtype=torch.uint8, device=dev)
-    ex = torch.empty(n * A * P, dtype=torch.uint8, device=dev)
-    coll = torch.empty(n * P, dtype=torch.uint8, device=dev)
-    stats = eb.new_stats()
-    flat = acts.reshape(-1)
-    eb.step_n(s0, out, flat, n, traj, ex, coll, stats)  # warm
-    torch.cuda.synchronize()
-    ocdist.barrier()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    eb.step_n(s0, out, flat, n, traj, ex, coll, stats)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) * 1e-3, dev) * 1e3
-    nS = eb.layout.num_planes  # bytes per env of state = planes (t counts 2)
-    bytes_env_step = nS / n + nS + 2 * A + 1
-    gbs = bytes_env_step * eb.B * n / (ms * 1e-3) / 1e9
-    del traj, ex, coll
-    return {"value": world * eb.B * n / (ms * 1e-3), "unit": "env-steps/s", "steps": n, "ms_per_step": ms / n,
-            "kernel": "oc_step_n_kernel<%d,%d>" % (A, eb.K), "algorithmic_bytes_per_env_step": bytes_env_step,
-            "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS,
-            "outputs": "every step's state (trajectory), executed actions and collision mask written"}
 
 
 # Salad recipe subtasks (recipe_planner: Chop x2, Merge x6, Deliver) as oc_subtask masks:
@@ -151,13 +125,57 @@ def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 20) -> dict:
             "frac_hbm": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "legal_rows": legal}
 
 
-def load_traffic(path: str):
+def load_traffic(path: str, kernel: str = "oc_step_n_kernel"):
+    """Calibrated HBM bytes per launch of `kernel` from tools/pmc_report.py's output."""
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
-    except (OSError, ValueError):
+        return d[kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    except (OSError, ValueError, KeyError):
         return None, None
+
+
+def per_step_launch(eb, acts, n_act, W, dev, world, use_graph=True) -> dict:
+    """Secondary line: one oc_step launch per step, K steps replayed from a hipGraph (or eager),
+    ping-pong state buffers; kernel duration = event window / K on the launch stream."""
+    s_a, s_b = eb.new_state(), eb.new_state()
+    eb.reset(s_a)
+    exe, coll, stats = eb.new_exec(), eb.new_coll(), eb.new_stats()
+
+    def run_steps(n):
+        for i in range(n):
+            src, dst = (s_a, s_b) if i % 2 == 0 else (s_b, s_a)
+            eb.step(src, dst, acts[i % n_act], exe, coll, stats)
+
+    run_steps(W + (W % 2))
+    torch.cuda.synchronize()
+    graph = None
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(device=dev)
+        cap.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.graph(graph, stream=cap):
+            run_steps(n_act)
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+    ocdist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    if graph is not None:
+        graph.replay()
+    else:
+        run_steps(n_act)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) * 1e-3, dev) * 1e3
+    bytes_step = algorithmic_bytes_per_env_step(eb.A, eb.K)
+    gbs = bytes_step * eb.B / (ms / n_act * 1e-3) / 1e9
+    return {"value": world * eb.B * n_act / (ms * 1e-3), "unit": "env-steps/s", "steps": n_act,
+            "ms_per_step": ms / n_act, "launch": "hipGraph of %d oc_step launches" % n_act if graph else "eager",
+            "kernel": "oc_step_kernel<%d,%d>" % (eb.A, eb.K), "algorithmic_bytes_per_env_step": bytes_step,
+            "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
 
 
 def main() -> int:
@@ -170,10 +188,11 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=1 << 20, help="envs per GPU")
     ap.add_argument("--max-T", type=int, default=100)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a hipGraph")
+    ap.add_argument("--steps-per-launch", type=int, default=100, help="oc_step_n launch length (headline)")
+    ap.add_argument("--no-graph", action="store_true", help="per-step line: eager launches instead of a hipGraph")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-fused", action="store_true", help="skip the secondary oc_step_n measurement")
+    ap.add_argument("--no-per-step", action="store_true", help="skip the secondary one-launch-per-step line")
     ap.add_argument("--no-rollout", action="store_true", help="skip the secondary oc_rollout (C5) measurement")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
@@ -189,40 +208,40 @@ def main() -> int:
     sh = ocdist.shard(args.batch, rank, world, local)
     eb = OvercookedBatch(args.level, args.agents, sh.batch, max_T=args.max_T, device=dev)
     K, W = args.steps, args.warmup
-    s_a, s_b = eb.new_state(), eb.new_state()
-    eb.reset(s_a)
-    exe, coll, stats = eb.new_exec(), eb.new_coll(), eb.new_stats()
-    n_act = K + (K % 2)  # even ring: the graph ends on the buffer it started from
-    acts = torch.empty((n_act, eb.A * eb.pitch), dtype=torch.uint8, device=dev)
-    for i in range(n_act):
+    P, A, S = eb.pitch, eb.A, eb.layout.state_bytes
+    # pre-materialised synthetic actions, one buffer per step (untimed)
+    acts = torch.empty((K, A * P), dtype=torch.uint8, device=dev)
+    for i in range(K):
         eb.gen_actions(acts[i], step=i, seed=args.seed, env_offset=sh.env_offset)
+    # launch plan: equal launches of <= steps_per_launch steps
+    n_launch = -(-K // max(1, args.steps_per_launch))
+    n_per = -(-K // n_launch)
+    segs = [(i, min(n_per, K - i)) for i in range(0, K, n_per)]
+    # outputs of one launch (every step's state, executed actions, collision mask), reused per launch
+    traj = torch.empty(n_per * S, dtype=torch.uint8, device=dev)
+    ex_all = torch.empty(n_per * A * P, dtype=torch.uint8, device=dev)
+    coll_all = torch.empty(n_per * P, dtype=torch.uint8, device=dev)
+    s_a, s_b = eb.new_state(), eb.new_state()
+    stats = eb.new_stats()
 
-    def run_steps(n, events=None):
-        for i in range(n):
-            src, dst = (s_a, s_b) if i % 2 == 0 else (s_b, s_a)
-            if events is not None:
-                events[i][0].record()
-            eb.step(src, dst, acts[i % n_act], exe, coll, stats)
-            if events is not None:
-                events[i][1].record()
+    def run(n_steps_total, first=0):
+        src, dst = s_a, s_b
+        done = 0
+        while done < n_steps_total:
+            n = min(n_per, n_steps_total - done)
+            i0 = (first + done) % K
+            n = min(n, K - i0)
+            eb.step_n(src, dst, acts[i0:i0 + n].reshape(-1), n, traj, ex_all, coll_all, stats)
+            src, dst = dst, src
+            done += n
+        return src
 
-    # warmup (eager), even count so the state is back in s_a
-    run_steps(W + (W % 2))
-    torch.cuda.synchronize()
-
-    graph = None
-    if not args.no_graph:
-        graph = torch.cuda.CUDAGraph()
-        cap = torch.cuda.Stream(device=dev)
-        cap.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.graph(graph, stream=cap):
-            run_steps(n_act)
-        torch.cuda.synchronize()
-        graph.replay()  # one untimed replay
-        torch.cuda.synchronize()
-    # warm the summary path (reduce kernel + all-gather) so no first-use cost lands in the window
+    # warmup: W untimed steps (plus the summary path: reduce kernel + all-gather)
+    eb.reset(s_a)
+    run(max(W, 1))
     ocdist.gather_summaries(eb.reduce_stats(stats))
     torch.cuda.synchronize()
+    eb.reset(s_a)
     stats.zero_()
 
     # ---------------- timed region ----------------
@@ -231,10 +250,7 @@ def main() -> int:
     ev0, ev1, ev2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
     t0 = time.perf_counter()
     ev0.record()
-    if graph is not None:
-        graph.replay()
-    else:
-        run_steps(n_act)
+    run(K)
     ev1.record()
     totals = eb.reduce_stats(stats)
     gathered = ocdist.gather_summaries(totals)
@@ -244,36 +260,26 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     # ----------------------------------------------
     elapsed_max = ocdist.max_over_ranks(elapsed, dev)
-    gpu_ms = ev0.elapsed_time(ev2)
     steps_ms = ev0.elapsed_time(ev1)
     summary = ocdist.summarize(gathered)
 
-    # Dominant-kernel duration, live: HIP events on the launch stream bracket the K step
-    # kernels of the timed window (graph replay: kernels back to back, no host gaps), so
-    # window / K is the mean oc_step_kernel duration.  Eager mode also reports per-launch
-    # event pairs (which add the event packets' own ~2 us).
-    kern_ms = steps_ms / n_act
-    kern_ms_pairs = None
-    if graph is None:
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_act)]
-        run_steps(n_act, evs)
-        torch.cuda.synchronize()
-        durs = sorted(a.elapsed_time(b) for a, b in evs)
-        kern_ms_pairs = durs[len(durs) // 2]
-
-    steps_done = n_act
-    value = world * sh.batch * steps_done / elapsed_max
-    bytes_step = algorithmic_bytes_per_env_step(args.agents, eb.K)
-    achieved_gbs = bytes_step * sh.batch / (kern_ms * 1e-3) / 1e9
+    # Dominant kernel: oc_step_n_kernel; HIP events on its launch stream bracket the timed
+    # launches (back to back), so window / launches = its mean duration.
+    kern_ms = steps_ms / len(segs)
+    nS = eb.layout.num_planes  # state bytes per env (the u16 t counts 2)
+    bytes_launch = (nS + n_per * (nS + 2 * A + 1)) * sh.batch
+    bytes_env_step = bytes_launch / (n_per * sh.batch)
+    achieved_gbs = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(args.traffic_json)
+    value = world * sh.batch * K / elapsed_max
     line = {
         "metric": METRIC,
         "value": value,
         "unit": "env-steps/s",
         "n_gpus": world,
-        "steps": steps_done,
+        "steps": K,
         "warmup": W,
-        "ms_per_step": elapsed_max * 1e3 / steps_done,
+        "ms_per_step": elapsed_max * 1e3 / K,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -284,20 +290,23 @@ def main() -> int:
                         % (args.level, args.agents, sh.batch, args.max_T),
             "level": args.level, "num_agents": args.agents, "batch_per_gpu": sh.batch,
             "global_batch": world * sh.batch, "parallelism": "dp%d (env shards, no data-path collective)" % world,
-            "launch": "eager" if graph is None else "hipGraph of %d steps" % n_act,
+            "launch": "oc_step_n: %d launches x %d steps; every step's state, executed actions and collision "
+                      "mask written to HBM" % (len(segs), n_per),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "oc_step_kernel<2,4>", "algorithmic_bytes_per_env_step": bytes_step,
-            "kernel_ms_mean": kern_ms, "kernel_ms_event_pairs_median": kern_ms_pairs,
-            "traffic_source": traffic_src,
+            "kernel": "oc_step_n_kernel<%d,%d>" % (A, eb.K), "steps_per_launch": n_per,
+            "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_env_step": bytes_env_step,
+            "kernel_ms_mean": kern_ms, "traffic_source": traffic_src,
         },
-        "gpu_ms_timed_region": gpu_ms,
+        "gpu_ms_timed_region": ev0.elapsed_time(ev2),
         "episodes": summary,
     }
-    if not args.no_fused:
-        line["fused_multi_step"] = measure_fused(eb, acts, n_act, dev, world)
+    if not args.no_per_step:
+        n_ps = K if K % 2 == 0 or K == 1 else K - 1  # even: the replayed graph ends on its start buffer
+        line["per_step_launch"] = per_step_launch(eb, acts, n_ps, W, dev, world, use_graph=not args.no_graph)
+        line["per_step_launch"]["traffic"] = load_traffic(args.traffic_json, "oc_step_kernel")[0]
     if not args.no_rollout:
         line["rollout"] = measure_rollout(dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -735,7 +735,7 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
     if (((uintptr_t)state_in | (uintptr_t)state_out | (uintptr_t)actions | (uintptr_t)traj | (uintptr_t)exec_actions |
          (uintptr_t)coll_mask) & 15u)
         return fail(OC_EINVAL, "buffers must be 16-byte aligned");
-    if (state_in == state_out && n > 0 && traj == state_out) return fail(OC_EINVAL, "traj must not alias state_out");
+    if (traj != nullptr && (traj == state_in || traj == state_out)) return fail(OC_EINVAL, "traj must not alias the state");
     LevelArgs L = h->args;
     L.pitch = pitch_for(B);
     L.B = B;
@@ -744,6 +744,7 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
     // steps per launch so every per-launch buffer (trajectory, actions) stays < 2 GiB of offsets
     int64_t per = ((1ll << 31) - 1) / (NP * L.pitch);
     if (per > 4096) per = 4096;
+    per = (n + (n + per - 1) / per - 1) / ((n + per - 1) / per);  // equal launches
     const int64_t need = L.pitch / kEnvsPerBlock, cap = (int64_t)kCUs * 5;  // <= 5 waves/SIMD resident
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t s = (hipStream_t)stream;

@@ -6,7 +6,7 @@ Dispatches, on the bench workload (partial-divider_salad, 2 agents, 2^20 envs):
   oc_checksum_kernel  x3  -- reads exactly 17 planes x B bytes with oc_step's dword pattern
                              (FETCH_SIZE calibration for this access width)
   oc_step_kernel      x20 -- the headline kernel (eager launches)
-  oc_step_n_kernel    x3  -- 16 fused steps each, trajectory + exec + coll written
+  oc_step_n_kernel    x3  -- 100 steps each (bench.py's launch), trajectory + exec + coll written
 tools/pmc_report.py turns the counter CSVs into profiles/pmc_traffic.json.
 """
 import os
@@ -20,11 +20,11 @@ import torch  # noqa: E402
 from gym_cooking_amd.engine import OvercookedBatch  # noqa: E402
 
 B = 1 << 20
-NFUSED = 16
+NFUSED = 100  # bench.py's headline launch length
 eb = OvercookedBatch("partial-divider_salad", 2, B, max_T=100, device="cuda:0")
 a, b = eb.new_state(), eb.new_state()
-acts = torch.empty((20, eb.A * eb.pitch), dtype=torch.uint8, device="cuda:0")
-for i in range(20):
+acts = torch.empty((NFUSED, eb.A * eb.pitch), dtype=torch.uint8, device="cuda:0")
+for i in range(NFUSED):
     eb.gen_actions(acts[i], step=i, seed=0)
 exe, coll, stats = eb.new_exec(), eb.new_coll(), eb.new_stats()
 for _ in range(3):

@@ -20,7 +20,7 @@ import sys
 
 B, NP, A = 1 << 20, 17, 2  # tools/pmc_probe.py workload
 PITCH = B
-NFUSED = 16
+NFUSED = 100
 
 
 def per_kernel(d, counter):
@@ -60,7 +60,6 @@ def main():
     alg = (2 * NP + 2 * A + 1) * B
     res["oc_step_kernel"] = {"read_bytes": f_step, "write_bytes": w_step, "hbm_bytes_per_launch": f_step + w_step,
                              "algorithmic_bytes_per_launch": alg, "ratio": (f_step + w_step) / alg}
-    res["hbm_bytes_per_launch"] = f_step + w_step
     if "oc_step_n_kernel" in fetch:
         fn, wn = mean_tail(fetch["oc_step_n_kernel"]) * 1024 * rf, mean_tail(write["oc_step_n_kernel"]) * 1024 * wf
         algn = (NP + NFUSED * (NP + 2 * A + 1)) * B
