@@ -236,9 +236,11 @@ def main() -> int:
             done += n
         return src
 
-    # warmup: W untimed steps (plus the summary path: reduce kernel + all-gather)
+    # warmup: W untimed steps, rounded up to whole launches of the timed length so that every
+    # oc_step_n launch a profiler sees has the timed shape (plus the summary path: reduce + all-gather)
+    warm_steps = -(-max(W, 1) // n_per) * n_per
     eb.reset(s_a)
-    run(max(W, 1))
+    run(warm_steps)
     ocdist.gather_summaries(eb.reduce_stats(stats))
     torch.cuda.synchronize()
     eb.reset(s_a)
@@ -292,6 +294,7 @@ def main() -> int:
             "global_batch": world * sh.batch, "parallelism": "dp%d (env shards, no data-path collective)" % world,
             "launch": "oc_step_n: %d launches x %d steps; every step's state, executed actions and collision "
                       "mask written to HBM" % (len(segs), n_per),
+            "warmup_steps_run": warm_steps,
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -1,18 +1,23 @@
 // oc_engine.hip -- MI355X (gfx950) batched Overcooked step engine + its C-ABI (include/oc_engine.h).
 //
-// One fused kernel steps a batch of independent kitchens.  The state is structure-of-arrays
-// byte planes; each lane owns EPL consecutive envs, so every plane is read
-// and written with one coalesced EPL-byte access per lane (EPL = 4: one dword, 256 B per
-// wave-instruction).  The static level (7x7 tile classes) lives in three 64-bit cell masks
-// in SGPRs, so a tile lookup is a 64-bit shift: no LDS, no table loads.  Per env the kernel
-// runs, branch-free (selects, no divergent control flow):
-//   pairwise collision resolution  <- check_collisions / is_collision
-//                                     (gym_cooking/envs/overcooked_environment.py:671-762)
-//   sequential per-agent interact  <- execute_navigation + interact
-//                                     (overcooked_environment.py:767-770, gym_cooking/utils/interact.py:4-89)
-//   the copy-crash (ERR) condition <- new_obs = copy.copy(self) (overcooked_environment.py:289, :108-113)
-//   done() / reward()              <- overcooked_environment.py:316-376
-// and accumulates per-block episode statistics for the all-gather of summaries.
+// Kernels:
+//   oc_step_kernel    one env transition over the batch.  The state is structure-of-arrays byte
+//                     planes; a lane owns 4 consecutive envs (one dword per
+//                     plane, 256 B per wave-instruction) and steps them as SWAR (oc_swar.h):
+//                       pairwise collision resolution  <- check_collisions / is_collision
+//                                                         (gym_cooking/envs/overcooked_environment.py:671-762)
+//                       sequential per-agent interact  <- execute_navigation + interact
+//                                                         (overcooked_environment.py:767-770, utils/interact.py:4-89)
+//                       the copy-crash (ERR) condition <- new_obs = copy.copy(self) (:289, :108-113)
+//                       done() / reward()              <- overcooked_environment.py:316-376
+//                     Tile classes come from a 256-byte LDS table per block; the grid is
+//                     persistent and software-pipelined (next chunk's loads before this step).
+//   oc_step_n_kernel  n steps per launch with the state in registers; every step's state,
+//                     executed actions and collision mask are still written.
+//   oc_rollout_kernel navigation-planner rollout rows (oc_rollout.h).
+//   reset / gen_actions / checksum / stats_reduce helpers.
+// All of them accumulate nothing on the host; statistics are per-block rows of no-return
+// 64-bit atomics reduced by oc_stats_reduce for the all-gather of episode summaries.
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -133,7 +138,7 @@ __device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tb
     st.succ += __popc(c.wf & (ended << 1));
     st.err += __popc(c.wf & (ended << 2));
     st.coll += __popc(cm & vmask);
-    const uint32_t efull = ocsw::full80(ended << 7);
+    const uint32_t efull = (0x80808080u - ended) ^ 0x80808080u;  // 0x01 -> 0xFF per byte, no multiply
     const uint32_t e16a = __builtin_amdgcn_perm(0u, efull, 0x01010000u);  // env 0,1 -> u16 masks
     const uint32_t e16b = __builtin_amdgcn_perm(0u, efull, 0x03030202u);  // env 2,3
     const uint32_t sa = T0 & e16a, sb = T1 & e16b;
@@ -283,7 +288,7 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
     st.succ += __popc(c.wf & (ended << 1));
     st.err += __popc(c.wf & (ended << 2));
             st.coll += __popc(cm & vmask);
-            const uint32_t efull = ocsw::full80(ended << 7);
+            const uint32_t efull = (0x80808080u - ended) ^ 0x80808080u;  // no multiply
             const uint32_t sa = T0 & __builtin_amdgcn_perm(0u, efull, 0x01010000u);
             const uint32_t sb2 = T1 & __builtin_amdgcn_perm(0u, efull, 0x03030202u);
             st.steps += (sa & 0xFFFFu) + (sa >> 16) + (sb2 & 0xFFFFu) + (sb2 >> 16);

@@ -273,6 +273,20 @@ int main(int argc, char** argv) {
             oc_destroy(hh);
         }
     }
+    {  // E6: product oc_step_n, 100 steps per launch, full trajectory + exec + coll + stats
+        const int N6 = 100;
+        uint8_t *act6, *traj6, *ex6, *co6;
+        CK(hipMalloc(&act6, (int64_t)N6 * A * P));
+        CK(hipMalloc(&traj6, (int64_t)N6 * NP * P));
+        CK(hipMalloc(&ex6, (int64_t)N6 * A * P));
+        CK(hipMalloc(&co6, (int64_t)N6 * P));
+        for (int r = 0; r < N6; ++r) oc_gen_actions(h, act6 + (int64_t)r * A * P, B, 0, r, 1, nullptr);
+        const double us = timeit([&] { oc_step_n(h, sa, sb, act6, traj6, ex6, co6, stats, B, N6, nullptr); }, 5) / N6;
+        printf("E6 product oc_step_n x%d + traj      : %7.2f us/step\n", N6, us);
+        const double us2 = timeit([&] { oc_step_n(h, sa, sb, act6, nullptr, nullptr, nullptr, nullptr, B, N6, nullptr); }, 5) / N6;
+        printf("E6b oc_step_n x%d, no outputs        : %7.2f us/step\n", N6, us2);
+        hipFree(act6); hipFree(traj6); hipFree(ex6); hipFree(co6);
+    }
     for (int grid : {256, 512, 1024}) {
         const double us = timeit([&] { hipLaunchKernelGGL((mem_only<2, 4>), dim3(grid), dim3(kBlock), 0, 0, L, sa, sb, act, ex, coll); }, 50);
         printf("E2 memory only           grid %4d: %7.2f us\n", grid, us);
