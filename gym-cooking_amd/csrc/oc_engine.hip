@@ -353,6 +353,36 @@ struct RollArgs {
     int64_t pitch, B;
 };
 
+// Stage the reachability distances, the level tables and the subtask configurations in LDS.
+__device__ __forceinline__ void stage_roll_tables(const RollArgs& R, const uint8_t* dist_g, uint32_t* dist_w,
+                                                  ocro::RollLevel& Ls, ocro::Sub* subs) {
+    const int nwords = R.L.nnodes * ocro::kMaxNodes / 4;  // rows 0..nnodes-1 of the table
+    for (int i = threadIdx.x; i < nwords; i += kBlock) dist_w[i] = ((const uint32_t*)dist_g)[i];
+    if (threadIdx.x == 0) {
+        Ls = R.L;
+        for (int i = 0; i < R.nsub; ++i) subs[i] = R.subs[i];
+    }
+    __syncthreads();
+}
+
+template <int A, int K>
+__device__ __forceinline__ ocro::Row load_row(const uint8_t* __restrict__ sin, int64_t P, int64_t e) {
+    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
+    ocro::Row r;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        r.x |= (uint32_t)sin[a * P + e] << (8 * a);
+        r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
+        r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        r.loc |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
+        r.mask |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
+    }
+    return r;
+}
+
 template <int A, int K>
 __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                             uint8_t* __restrict__ sout,
@@ -364,29 +394,12 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
     __shared__ uint32_t dist_w[ocro::kMaxNodes * ocro::kMaxNodes / 4];
     __shared__ ocro::RollLevel Ls;
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
-    const int nwords = R.L.nnodes * ocro::kMaxNodes / 4;  // rows 0..nnodes-1 of the table
-    for (int i = threadIdx.x; i < nwords; i += kBlock) dist_w[i] = ((const uint32_t*)dist_g)[i];
-    if (threadIdx.x == 0) {
-        Ls = R.L;
-        for (int i = 0; i < R.nsub; ++i) subs[i] = R.subs[i];
-    }
-    __syncthreads();
+    stage_roll_tables(R, dist_g, dist_w, Ls, subs);
     const uint8_t* dist = (const uint8_t*)dist_w;
     const int64_t P = R.pitch;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-        ocro::Row r;
-#pragma unroll
-        for (int a = 0; a < A; ++a) {
-            r.x |= (uint32_t)sin[a * P + e] << (8 * a);
-            r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
-            r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
-        }
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            r.loc |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
-            r.mask |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
-        }
+        ocro::Row r = load_row<A, K>(sin, P, e);
         const uint16_t t = ((const uint16_t*)(sin + kPT * P))[e];
         const uint8_t fl_in = sin[kPF * P + e];
         const int ai = alloc != nullptr ? alloc[e] : 0;
@@ -413,6 +426,38 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
         sout[kPF * P + e] = fl_in;
         out_flags[e] = (uint8_t)f;
         lb[e] = bound;
+    }
+}
+
+// Bayesian-delegation likelihood (oc_nav_likelihood): one row per lane; every candidate action
+// of the row is a rollout (interact + goal + lower bound) evaluated in registers.
+template <int A, int K>
+__global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const uint8_t* __restrict__ sin,
+                                                               const uint8_t* __restrict__ taken_p,
+                                                               const uint8_t* __restrict__ alloc,
+                                                               const uint8_t* __restrict__ dist_g, int self_agent,
+                                                               double beta, double nap, double* __restrict__ out,
+                                                               uint8_t* __restrict__ out_flags) {
+    __shared__ uint32_t dist_w[ocro::kMaxNodes * ocro::kMaxNodes / 4];
+    __shared__ ocro::RollLevel Ls;
+    __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
+    stage_roll_tables(R, dist_g, dist_w, Ls, subs);
+    const uint8_t* dist = (const uint8_t*)dist_w;
+    const int64_t P = R.pitch;
+    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
+        const int ai = alloc != nullptr ? alloc[e] : 0;
+        double v = 0.0;
+        int f = OC_LIK_BADALLOC;
+        if (ai < R.nsub) {
+            const ocro::Row r = load_row<A, K>(sin, P, e);
+            uint32_t taken = 0;
+#pragma unroll
+            for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
+            ocro::RowOps<A, K> ops(Ls, dist);
+            f = ops.likelihood(r, subs[ai], taken, self_agent, beta, nap, v);
+        }
+        out[e] = f == OC_LIK_OK ? v : 0.0;
+        out_flags[e] = (uint8_t)f;
     }
 }
 
@@ -771,19 +816,11 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
     return OC_OK;
 }
 
-int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
-               const uint8_t* alloc, const oc_subtask* subtasks, int32_t num_subtasks, uint8_t* out_flags,
-               float* lower_bound, int64_t B, void* stream) {
-    if (h == nullptr || state_in == nullptr || state_out == nullptr || actions == nullptr || subtasks == nullptr ||
-        out_flags == nullptr || lower_bound == nullptr || B < 0)
-        return fail(OC_EINVAL, "bad argument");
+// Shared argument block of oc_rollout / oc_nav_likelihood: level tables + validated subtasks.
+static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num_subtasks, int64_t B, RollArgs& R) {
     if (num_subtasks < 1 || num_subtasks > OC_MAX_SUBTASKS) return fail(OC_EINVAL, "num_subtasks %d", num_subtasks);
     if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes", ocro::kMaxNodes);
     if (h->roll_dist == nullptr) return fail(OC_EHIP, "rollout tables not on the device");
-    if (state_in == state_out) return fail(OC_EINVAL, "oc_rollout is out of place");
-    if (((uintptr_t)lower_bound & 3u) || ((uintptr_t)state_in & 1u) || ((uintptr_t)state_out & 1u))
-        return fail(OC_EINVAL, "misaligned buffer");
-    RollArgs R;
     R.L = h->roll;
     R.nsub = num_subtasks;
     R.pitch = pitch_for(B);
@@ -806,6 +843,20 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
         d.count = s.goal_count;
         d.pad[0] = d.pad[1] = 0;
     }
+    return OC_OK;
+}
+
+int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
+               const uint8_t* alloc, const oc_subtask* subtasks, int32_t num_subtasks, uint8_t* out_flags,
+               float* lower_bound, int64_t B, void* stream) {
+    if (h == nullptr || state_in == nullptr || state_out == nullptr || actions == nullptr || subtasks == nullptr ||
+        out_flags == nullptr || lower_bound == nullptr || B < 0)
+        return fail(OC_EINVAL, "bad argument");
+    if (state_in == state_out) return fail(OC_EINVAL, "oc_rollout is out of place");
+    if (((uintptr_t)lower_bound & 3u) || ((uintptr_t)state_in & 1u) || ((uintptr_t)state_out & 1u))
+        return fail(OC_EINVAL, "misaligned buffer");
+    RollArgs R;
+    if (const int rc = roll_args(h, subtasks, num_subtasks, B, R)) return rc;
     if (B == 0) return OC_OK;
     const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)kCUs * 8;
     const dim3 grid((unsigned)(need < cap ? need : cap));
@@ -815,6 +866,27 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
                        (uint8_t*)state_out, actions, alloc, h->roll_dist, out_flags, lower_bound)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_ROLL)
     return hip_check("oc_rollout launch");
+}
+
+int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* taken, const uint8_t* alloc,
+                      const oc_subtask* subtasks, int32_t num_subtasks, int32_t self_agent, double beta,
+                      double none_action_prob, double* likelihood, uint8_t* out_flags, int64_t B, void* stream) {
+    if (h == nullptr || state == nullptr || taken == nullptr || subtasks == nullptr || likelihood == nullptr ||
+        out_flags == nullptr || B < 0)
+        return fail(OC_EINVAL, "bad argument");
+    if (self_agent < 0 || self_agent >= h->A) return fail(OC_EINVAL, "self_agent %d", self_agent);
+    if (((uintptr_t)likelihood & 7u) || ((uintptr_t)state & 1u)) return fail(OC_EINVAL, "misaligned buffer");
+    RollArgs R;
+    if (const int rc = roll_args(h, subtasks, num_subtasks, B, R)) return rc;
+    if (B == 0) return OC_OK;
+    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)kCUs * 8;
+    const dim3 grid((unsigned)(need < cap ? need : cap));
+    hipStream_t st = (hipStream_t)stream;
+#define OC_LAUNCH_LIK(A, K)                                                                                     \
+    hipLaunchKernelGGL((oc_likelihood_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state, taken, \
+                       alloc, h->roll_dist, self_agent, beta, none_action_prob, likelihood, out_flags)
+    OC_DISPATCH(h->A, h->K, OC_LAUNCH_LIK)
+    return hip_check("oc_nav_likelihood launch");
 }
 
 int oc_gen_actions(const oc_handle* h, uint8_t* actions, int64_t B, int64_t env_offset, int64_t step,

@@ -147,9 +147,12 @@ struct RowOps {
     OC_RH int cell(int x, int y) const { return y * L.W + x; }
     OC_RH int agent_cell(const Row& r, int a) const { return cell(r.ax(a), r.ay(a)); }
 
-    // level0: agents outside the subtask freeze into AgentCounters; their items leave
-    OC_RH void level0(Row& r, const Sub& s) {
+    // level0: agents outside the subtask freeze into AgentCounters; their items leave.
+    // Returns true where the reference raises: a second removed agent on an already replaced
+    // Floor (World.remove asserts, world.py:307-315).
+    OC_RH bool level0(Row& r, const Sub& s) {
         active = 0;
+        bool raised = false;
         for (int i = 0; i < s.n; ++i) active |= 1u << s.agent[i];
 #pragma unroll
         for (int a = 0; a < A; ++a) {
@@ -160,8 +163,11 @@ struct RowOps {
                 Row::s64(r.mask, hh, 0);
                 Row::s32(r.h, a, kNone);
             }
-            ac |= 1ull << agent_cell(r, a);
+            const uint64_t bit = 1ull << agent_cell(r, a);
+            raised |= (ac & bit) != 0;
+            ac |= bit;
         }
+        return raised;
     }
 
     // the un-held item on a non-Floor square (at most one off Delivery), or -1
@@ -377,9 +383,15 @@ struct RowOps {
         return lower + pen;
     }
 
-    // The whole row: returns OC_ROLL_* flags; r becomes the Level-0 next state.
+    // The whole row: returns OC_ROLL_* flags; r becomes the Level-0 next state (unchanged when
+    // the configuration raises).
     OC_RH int run(Row& r, const Sub& s, int c0, int c1, float& lb) {
-        level0(r, s);
+        const Row r_in = r;
+        if (level0(r, s)) {
+            r = r_in;
+            lb = 0.0f;
+            return 8;  // OC_ROLL_RAISES
+        }
         if (s.kind == 0) c0 = c1 = kNoop;
         c0 = c0 > kNoop ? kNoop : c0;
         c1 = c1 > kNoop ? kNoop : c1;
@@ -391,6 +403,78 @@ struct RowOps {
         else if (is_goal(r, s)) fl |= 2;
         lb = lower_bound(r, s);
         return fl;
+    }
+
+    // E2E_BRTDP.Q(state, action, v_l) with value_init's values (e2e_brtdp.py:736-760, :678-729);
+    // false where T raises (joint co-location)
+    OC_RH bool q_value(const Row& r0, const Sub& s, int c0, int c1, double& q) const {
+        Row r = r0;
+        interact(r, s.agent[0], c0);
+        if (s.n == 2) {
+            interact(r, s.agent[1], c1);
+            if (agent_cell(r, s.agent[0]) == agent_cell(r, s.agent[1])) return false;
+        }
+        double cost = 1.0;  // time_cost + action_cost per moving agent (:816-826)
+        if (c0 != kNoop) cost += 0.1;
+        if (s.n == 2 && c1 != kNoop) cost += 0.1;
+        double v = 0.0;
+        if (!is_goal(r, s)) v = (double)lower_bound(r, s) * (1.0 + 0.1) - 1.09;
+        q = cost + 1.0 * v;
+        return true;
+    }
+
+    // BayesianDelegator.prob_nav_actions(..., no_level_1=True) (bayesian_delegator.py:461-689).
+    // taken: agent a's executed action in byte a.  Returns OC_LIK_* flags.
+    OC_RH int likelihood(Row r, const Sub& s, uint32_t taken, int self_agent, double beta, double nap,
+                         double& out) {
+        out = 0.0;
+        if (s.kind == 0) {  // None: one agent, the self agent's movable actions in the full state
+            if (s.n != 1) return 4;
+            active = (1u << A) - 1u;
+            ac = 0;
+            int n = 0;
+            for (int c = 0; c < 4; ++c) n += single_legal(r, self_agent, c) ? 1 : 0;
+            if (n == 0) return 8;
+            const double ap = (1.0 - nap) / n, x0 = beta * nap, x1 = beta * ap, m = x0 > x1 ? x0 : x1;
+            double S = exp(x0 - m);
+            for (int k = 0; k < n; ++k) S += exp(x1 - m);
+            const bool moved = ((taken >> (8 * s.agent[0])) & 0xFFu) != kNoop;
+            out = (moved ? exp(x1 - m) : exp(x0 - m)) / S;
+            return 1;
+        }
+        if (level0(r, s)) return 4;
+        int t0 = (int)((taken >> (8 * s.agent[0])) & 0xFFu), t1 = kNoop;
+        if (s.n == 2) t1 = (int)((taken >> (8 * s.agent[1])) & 0xFFu);
+        t0 = t0 > kNoop ? kNoop : t0;
+        t1 = t1 > kNoop ? kNoop : t1;
+        double old_q;
+        if (!q_value(r, s, t0, t1, old_q)) return 4;
+        if (!action_legal(r, s, t0, t1)) return 4;  // assert action in valid_nav_actions
+        const int other = s.n == 2 ? (s.agent[0] == self_agent ? 1 : (s.agent[1] == self_agent ? 0 : -1)) : -1;
+        // pass 1: max of beta * (old_q - Q) over the valid actions; pass 2: softmax sum
+        double m = -1.0e300, S = 0.0, xt = 0.0;
+        bool found = false;
+        for (int pass = 0; pass < 2; ++pass) {
+            for (int a0 = 0; a0 < 5; ++a0)
+                for (int a1 = 0; a1 < (s.n == 2 ? 5 : 1); ++a1) {
+                    const int c1 = s.n == 2 ? a1 : kNoop;
+                    if (!action_legal(r, s, a0, c1)) continue;
+                    if (other == 0 && a0 != t0) continue;
+                    if (other == 1 && c1 != t1) continue;
+                    double q;
+                    if (!q_value(r, s, a0, c1, q)) return 4;
+                    const double x = beta * (old_q - q);
+                    if (pass == 0) {
+                        m = x > m ? x : m;
+                        if (a0 == t0 && c1 == t1) { found = true; xt = x; }
+                    } else {
+                        S += exp(x - m);
+                    }
+                }
+        }
+        if (!found) return 4;
+        out = exp(xt - m) / S;
+        return 1;
     }
 };
 

@@ -30,7 +30,7 @@ OC_STAT_NAMES = ("episodes", "successes", "steps", "collisions", "errors")
 # Every symbol include/oc_engine.h declares (tests check the library exports them all).
 EXPORTED_SYMBOLS = (
     "oc_abi_version", "oc_last_error", "oc_create", "oc_destroy", "oc_get_layout", "oc_reset",
-    "oc_step", "oc_step_n", "oc_rollout", "oc_gen_actions", "oc_state_checksum", "oc_stats_size", "oc_stats_reduce",
+    "oc_step", "oc_step_n", "oc_rollout", "oc_nav_likelihood", "oc_gen_actions", "oc_state_checksum", "oc_stats_size", "oc_stats_reduce",
 )
 
 
@@ -59,6 +59,8 @@ class OcLayout(ctypes.Structure):
 SUB_NONE, SUB_CHOP, SUB_MERGE, SUB_DELIVER = 0, 1, 2, 3
 ROLL_LEGAL, ROLL_GOAL, ROLL_ASSERT, ROLL_BADALLOC = 0x01, 0x02, 0x04, 0x80
 MAX_SUBTASKS = 64
+LIK_OK, LIK_RAISES, LIK_ZERODIV, LIK_BADALLOC = 0x01, 0x04, 0x08, 0x80
+ROLL_RAISES = 0x08
 
 
 class OcSubtask(ctypes.Structure):
@@ -154,6 +156,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.oc_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, vp]
     lib.oc_rollout.restype = ctypes.c_int
     lib.oc_rollout.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(OcSubtask), i32, vp, vp, i64, vp]
+    lib.oc_nav_likelihood.restype = ctypes.c_int
+    lib.oc_nav_likelihood.argtypes = [vp, vp, vp, vp, ctypes.POINTER(OcSubtask), i32, i32, ctypes.c_double,
+                                      ctypes.c_double, vp, vp, i64, vp]
     lib.oc_step_n.restype = ctypes.c_int
     lib.oc_step_n.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]
     lib.oc_gen_actions.restype = ctypes.c_int

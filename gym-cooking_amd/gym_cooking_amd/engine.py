@@ -154,6 +154,22 @@ class OvercookedBatch:
                                        len(subtasks), _ptr(flags), _ptr(lower_bound), self.B, self._stream()))
         return flags, lower_bound
 
+    def nav_likelihood(self, state: torch.Tensor, taken: torch.Tensor, subtasks, self_agent: int,
+                       beta: float = 1.3, none_action_prob: float = 0.5, alloc: Optional[torch.Tensor] = None):
+        """Bayesian-delegation likelihoods (oc_nav_likelihood): prob_nav_actions of every row's
+        allocation given the executed actions `taken` (u8 [A][pitch]); returns
+        (likelihood f64 [pitch], flags u8 [pitch])."""
+        self._check(state, self.layout.state_bytes)
+        self._check(taken, self.A * self.pitch)
+        if alloc is not None:
+            self._check(alloc, self.pitch)
+        out = torch.empty(self.pitch, dtype=torch.float64, device=self.device)
+        flags = torch.empty(self.pitch, dtype=torch.uint8, device=self.device)
+        capi.check(self.lib.oc_nav_likelihood(self._h, _ptr(state), _ptr(taken), _ptr(alloc),
+                                              capi.subtask_array(subtasks), len(subtasks), self_agent, beta,
+                                              none_action_prob, _ptr(out), _ptr(flags), self.B, self._stream()))
+        return out, flags
+
     def gen_actions(self, actions: torch.Tensor, step: int, seed: int = 0, env_offset: int = 0) -> torch.Tensor:
         self._check(actions, self.A * self.pitch)
         capi.check(self.lib.oc_gen_actions(self._h, _ptr(actions), self.B, env_offset, step, seed, self._stream()))

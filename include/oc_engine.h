@@ -214,6 +214,9 @@ typedef struct {
 #define OC_ROLL_GOAL 0x02   /* is_goal_state(T(state, action)); 0 on OC_ROLL_ASSERT rows */
 #define OC_ROLL_ASSERT 0x04 /* joint: the two agents end co-located (the reference's
                                AssertionError at e2e_brtdp.py:143; state_out still written) */
+#define OC_ROLL_RAISES 0x08 /* the reference raises configuring the planner: two agents outside the
+                               subtask stand on one square (World.remove of the same Floor twice,
+                               gym_cooking/utils/world.py:307-315); row copied unchanged, bound 0 */
 #define OC_ROLL_BADALLOC 0x80 /* alloc id >= num_subtasks: row copied unchanged, bound 0 */
 
 /* One rollout transition per row e < B:
@@ -229,6 +232,37 @@ typedef struct {
 int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
                const uint8_t* alloc, const oc_subtask* subtasks, int32_t num_subtasks,
                uint8_t* out_flags, float* lower_bound, int64_t B, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Bayesian-delegation action likelihood: per row,
+ *   BayesianDelegator.prob_nav_actions(obs_tm1, actions_tm1, subtask, subtask_agent_names,
+ *                                      beta, no_level_1=True)
+ *     gym_cooking/delegation_planner/bayesian_delegator.py:461-689
+ * for a planner whose values are all value_init's (a fresh E2E_BRTDP, e2e_brtdp.py:678-729):
+ *   Q(s, a) = cost(a) + v_l(T(s, a)),  cost = 1.0 + 0.1 per moving subtask agent (:816-826),
+ *   v_l = 0 on goal states, else 1.1 * lower_bound - 1.09;
+ *   p = softmax(beta * (Q(s, taken) - Q(s, a')))[taken] over get_actions(s) (joint actions of a
+ *   pair that contains self_agent keep the other agent's taken action, :676-680);
+ *   subtask None (one agent): softmax(beta * [p0, (1 - p0) / n, ...])[taken != (0,0)], n = the
+ *   self agent's movable actions in the full (not Level-0) state.
+ * The reference's own bayes_update runs Level 1 (other agents' planners predict their moves)
+ * and BRTDP updates its values between calls; neither is restated here.
+ * ------------------------------------------------------------------------------------- */
+#define OC_LIK_OK 0x01       /* likelihood computed */
+#define OC_LIK_RAISES 0x04   /* the reference raises: taken action not in get_actions, a joint T
+                                co-location assert, two removed agents on one square (Level-0
+                                configuration), or None for two agents */
+#define OC_LIK_ZERODIV 0x08  /* None subtask and the self agent has no movable action */
+#define OC_LIK_BADALLOC 0x80 /* alloc id >= num_subtasks */
+
+/*   state        : obs_tm1 states (oc_layout), B rows
+ *   taken        : u8 [A][pitch] executed actions actions_tm1 (env.agent_actions, :770)
+ *   alloc/subtasks/num_subtasks : as oc_rollout (goal_count = the planner's cur_obj_count)
+ *   self_agent   : the delegating agent's index (BayesianDelegator.agent_name)
+ *   likelihood   : f64 [pitch]; out_flags : u8 [pitch] OC_LIK_* */
+int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* taken, const uint8_t* alloc,
+                      const oc_subtask* subtasks, int32_t num_subtasks, int32_t self_agent, double beta,
+                      double none_action_prob, double* likelihood, uint8_t* out_flags, int64_t B, void* stream);
 
 #ifdef __cplusplus
 }

@@ -538,7 +538,8 @@ static int cell_of(const Env* e, Loc l) { return l.y * e->L->width + l.x; }
 /* E2E_BRTDP._configure_planner_level, LEVEL0 branch (e2e_brtdp.py:389-406): every agent
  * not in the subtask leaves sim_agents, the object it holds leaves the world, and its Floor
  * is replaced by an AgentCounter. */
-static void level0_view(Env* e, const oc_subtask* s) {
+static int level0_view(Env* e, const oc_subtask* s) {
+    int raised = 0;
     for (int a = 0; a < e->A; ++a) {
         int in = 0;
         for (int i = 0; i < s->num_agents; ++i) in |= s->agent[i] == a;
@@ -549,8 +550,13 @@ static void level0_view(Env* e, const oc_subtask* s) {
             e->objs[ag->holding].alive = 0; /* env.world.remove(agent.holding) */
             ag->holding = -1;
         }
-        e->agent_counter |= 1ull << cell_of(e, ag->location); /* Floor -> AgentCounter */
+        /* env.world.remove(Floor(location)) asserts when a second removed agent stands on an
+         * already replaced Floor (world.py:307-315) */
+        const uint64_t bit = 1ull << cell_of(e, ag->location);
+        if (e->agent_counter & bit) raised = 1;
+        e->agent_counter |= bit; /* Floor -> AgentCounter */
     }
+    return raised;
 }
 
 /* gs.holding of a non-Floor square: the un-held object on it (Counter / Cutboard /
@@ -812,7 +818,13 @@ static void* run_roll(void* p) {
         Env env;
         int fl;
         unpack(&j->c, j->sin, e, &env, &fl);
-        level0_view(&env, s);
+        if (level0_view(&env, s)) { /* the reference raises configuring the planner: row copied */
+            unpack(&j->c, j->sin, e, &env, &fl);
+            pack(&j->c, &env, fl, j->sout, e);
+            j->flags[e] = OC_ROLL_RAISES;
+            j->lb[e] = 0.0f;
+            continue;
+        }
         int codes[2] = {OC_ACT_NOOP, OC_ACT_NOOP};
         for (int i = 0; i < s->num_agents; ++i) {
             const int c = j->act[s->agent[i] * P + e];
@@ -853,6 +865,133 @@ int oco_rollout(const oc_level_desc* L, int A, int K, const uint8_t* sin, uint8_
         j->b0 = B * t / nthreads;
         j->b1 = B * (t + 1) / nthreads;
         pthread_create(&th[t], NULL, run_roll, j);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    free(R);
+    return 0;
+}
+
+/* =========================================================================================
+ * Bayesian-delegation likelihood (prob_nav_actions, no_level_1, fresh planner values),
+ * delegation_planner/bayesian_delegator.py:461-689 over the rollout functions above.
+ * ========================================================================================= */
+
+/* E2E_BRTDP.Q(state, action, v_l) (e2e_brtdp.py:736-760) with value_init's v_l; returns 1
+ * when T raises (joint co-location) */
+static int q_value(const Env* env, const Reach* R, const oc_subtask* s, const int* codes, double* q) {
+    Env e2 = *env;
+    if (rollout_T(&e2, s, codes)) return 1;
+    double cost = 1.0; /* time_cost, + action_cost per non-(0,0) agent action (:816-826) */
+    for (int i = 0; i < s->num_agents; ++i)
+        if (codes[i] != OC_ACT_NOOP) cost += 0.1;
+    double v = 0.0;
+    if (!is_goal_state(&e2, s)) {
+        const double lower = lower_bound(&e2, R, s) * (1.0 + 0.1);
+        v = lower - 1.09;
+    }
+    *q = cost + 1.0 * v;
+    return 0;
+}
+
+static int likelihood_row(const Env* env_in, const Reach* R, const oc_subtask* s, const uint8_t* taken_all,
+                          int self_agent, double beta, double nap, double* out) {
+    Env env = *env_in;
+    if (s->kind == OC_SUB_NONE) { /* :629-641 on the full obs_tm1 */
+        if (s->num_agents != 1) return OC_LIK_RAISES;
+        int n = 0;
+        for (int c = 0; c < 4; ++c) n += single_action_legal(&env, self_agent, c);
+        if (n == 0) return OC_LIK_ZERODIV;
+        const double ap = (1.0 - nap) / n;
+        const double x0 = beta * nap, x1 = beta * ap, m = x0 > x1 ? x0 : x1;
+        double S = exp(x0 - m);
+        for (int k = 0; k < n; ++k) S += exp(x1 - m);
+        const int moved = taken_all[s->agent[0]] != OC_ACT_NOOP;
+        *out = (moved ? exp(x1 - m) : exp(x0 - m)) / S;
+        return OC_LIK_OK;
+    }
+    if (level0_view(&env, s)) return OC_LIK_RAISES;
+    int taken[2] = {OC_ACT_NOOP, OC_ACT_NOOP};
+    for (int i = 0; i < s->num_agents; ++i) taken[i] = taken_all[s->agent[i]] > OC_ACT_NOOP ? OC_ACT_NOOP : taken_all[s->agent[i]];
+    double old_q;
+    if (q_value(&env, R, s, taken, &old_q)) return OC_LIK_RAISES;
+    if (!action_legal(&env, s, taken)) return OC_LIK_RAISES; /* assert action in valid_nav_actions */
+    int other = -1; /* joint, self in the pair: keep the other agent's action (:676-680) */
+    if (s->num_agents == 2) {
+        if (s->agent[0] == self_agent) other = 1;
+        else if (s->agent[1] == self_agent) other = 0;
+    }
+    double x[25];
+    int nx = 0, ti = -1;
+    const int n0 = 5, n1 = s->num_agents == 2 ? 5 : 1;
+    for (int a0 = 0; a0 < n0; ++a0)
+        for (int a1 = 0; a1 < n1; ++a1) {
+            int c[2] = {a0, s->num_agents == 2 ? a1 : OC_ACT_NOOP};
+            if (!action_legal(&env, s, c)) continue;
+            if (other >= 0 && c[other] != taken[other]) continue;
+            double q;
+            if (q_value(&env, R, s, c, &q)) return OC_LIK_RAISES;
+            if (c[0] == taken[0] && (s->num_agents < 2 || c[1] == taken[1])) ti = nx;
+            x[nx++] = beta * (old_q - q);
+        }
+    if (ti < 0) return OC_LIK_RAISES;
+    double m = x[0];
+    for (int i = 1; i < nx; ++i) m = x[i] > m ? x[i] : m;
+    double S = 0.0;
+    for (int i = 0; i < nx; ++i) S += exp(x[i] - m);
+    *out = exp(x[ti] - m) / S;
+    return OC_LIK_OK;
+}
+
+typedef struct {
+    Cfg c;
+    const Reach* R;
+    const uint8_t *sin, *taken, *alloc;
+    const oc_subtask* subs;
+    int nsub, self_agent;
+    double beta, nap;
+    double* out;
+    uint8_t* flags;
+    int64_t b0, b1;
+} LikJob;
+
+static void* run_lik(void* p) {
+    LikJob* j = (LikJob*)p;
+    const int64_t P = j->c.pitch;
+    for (int64_t e = j->b0; e < j->b1; ++e) {
+        const int ai = j->alloc ? j->alloc[e] : 0;
+        j->out[e] = 0.0;
+        if (ai >= j->nsub) { j->flags[e] = OC_LIK_BADALLOC; continue; }
+        Env env;
+        int fl;
+        unpack(&j->c, j->sin, e, &env, &fl);
+        uint8_t taken[OC_MAX_AGENTS];
+        for (int a = 0; a < j->c.A; ++a) taken[a] = j->taken[a * P + e];
+        double v = 0.0;
+        const int f = likelihood_row(&env, j->R, &j->subs[ai], taken, j->self_agent, j->beta, j->nap, &v);
+        j->flags[e] = (uint8_t)f;
+        j->out[e] = f == OC_LIK_OK ? v : 0.0;
+    }
+    return NULL;
+}
+
+int oco_nav_likelihood(const oc_level_desc* L, int A, int K, const uint8_t* sin, const uint8_t* taken,
+                       const uint8_t* alloc, const oc_subtask* subs, int nsub, int self_agent, double beta, double nap,
+                       double* out, uint8_t* flags, int64_t B, int64_t pitch, int nthreads) {
+    if (nsub < 1 || self_agent < 0 || self_agent >= A) return -1;
+    Reach* R = (Reach*)malloc(sizeof(Reach));
+    build_reach(L, R);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    pthread_t th[64];
+    LikJob jobs[64];
+    for (int t = 0; t < nthreads; ++t) {
+        LikJob* j = &jobs[t];
+        j->c.L = L; j->c.A = A; j->c.K = K; j->c.max_T = 0; j->c.pitch = pitch;
+        j->R = R; j->sin = sin; j->taken = taken; j->alloc = alloc; j->subs = subs; j->nsub = nsub;
+        j->self_agent = self_agent; j->beta = beta; j->nap = nap; j->out = out; j->flags = flags;
+        j->b0 = B * t / nthreads;
+        j->b1 = B * (t + 1) / nthreads;
+        pthread_create(&th[t], NULL, run_lik, j);
     }
     for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
     free(R);

@@ -43,6 +43,10 @@ def lib() -> ctypes.CDLL:
         L.oco_rollout.restype = ctypes.c_int
         L.oco_rollout.argtypes = [ctypes.POINTER(capi.OcLevelDesc), i32, i32, vp, vp, vp, vp,
                                   ctypes.POINTER(capi.OcSubtask), i32, vp, vp, i64, i64, i32]
+        L.oco_nav_likelihood.restype = ctypes.c_int
+        L.oco_nav_likelihood.argtypes = [ctypes.POINTER(capi.OcLevelDesc), i32, i32, vp, vp, vp,
+                                         ctypes.POINTER(capi.OcSubtask), i32, i32, ctypes.c_double, ctypes.c_double,
+                                         vp, vp, i64, i64, i32]
         L.oco_action_code.restype = ctypes.c_uint8
         L.oco_action_code.argtypes = [u64, u64, u64, u64]
         _lib = L
@@ -90,6 +94,16 @@ class OracleBatch:
                                _p(alloc), subs, len(subtasks), _p(flags), _p(lb), self.B, self.pitch, nthreads)
         assert rc == 0, rc
         return flags[:self.B], lb[:self.B]
+
+    def nav_likelihood(self, state, taken, subtasks, alloc, self_agent, beta, none_action_prob, nthreads=8):
+        """prob_nav_actions rows (oco_nav_likelihood): returns (f64 [B], flags u8 [B])."""
+        out = np.zeros(self.pitch, np.float64)
+        flags = np.zeros(self.pitch, np.uint8)
+        rc = lib().oco_nav_likelihood(ctypes.byref(self.desc), self.A, self.K, _p(state), _p(taken), _p(alloc),
+                                      capi.subtask_array(subtasks), len(subtasks), self_agent, beta,
+                                      none_action_prob, _p(out), _p(flags), self.B, self.pitch, nthreads)
+        assert rc == 0, rc
+        return out[:self.B], flags[:self.B]
 
     def gen_actions(self, actions, env_offset, step, seed) -> None:
         rc = lib().oco_gen_actions(self.A, _p(actions), self.B, self.pitch, env_offset, step, seed)

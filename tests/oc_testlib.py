@@ -303,3 +303,58 @@ class RolloutRows:
             if len(errs) > 20:
                 break
         return errs
+
+
+class LikelihoodRows:
+    """Rows of tests/golden/likelihood.npz for one (config, self agent), with subtask tables
+    split into chunks of <= 64 configurations."""
+
+    def __init__(self, fx, cfg: int, self_agent: int):
+        st_cfg = fx["st_cfg"][fx["state"]]
+        sel = np.nonzero((st_cfg == cfg) & (fx["self_agent"] == self_agent))[0]
+        self.idx = sel
+        self.self_agent = self_agent
+        self.level = levels.load_level(str(fx["cfg_level"][cfg]))
+        self.A = int(fx["cfg_A"][cfg])
+        self.K = capi.item_slots(self.level)
+        st = fx["state"][sel]
+        self.agents, self.items, self.t = fx["st_agents"][st], fx["st_items"][st], fx["st_t"][st]
+        self.taken = fx["st_taken"][st]
+        self.beta, self.nap = float(fx["beta"]), float(fx["none_action_prob"])
+        self.B = len(sel)
+        keys, self.alloc, self.subtasks = {}, np.zeros(self.B, np.int64), []
+        for r, i in enumerate(sel):
+            n = int((fx["agents"][i] != PAD).sum())
+            key = (int(fx["kind"][i]), tuple(int(a) for a in fx["agents"][i][:n]),
+                   tuple(int(m) for m in fx["start"][i]), int(fx["goal_mask"][i]), int(fx["goal_count"][i]))
+            if key not in keys:
+                keys[key] = len(self.subtasks)
+                self.subtasks.append(capi.subtask(*key))
+            self.alloc[r] = keys[key]
+        self.exp_value, self.exp_raised = fx["value"][sel], fx["raised"][sel]
+
+    def chunks(self, max_sub: int = 64):
+        for c0 in range(0, len(self.subtasks), max_sub):
+            sel = np.nonzero((self.alloc >= c0) & (self.alloc < c0 + max_sub))[0]
+            yield sel, (self.alloc[sel] - c0).astype(np.uint8), self.subtasks[c0:c0 + max_sub]
+
+    def inputs(self, sel, pitch):
+        s = state_from_canonical(self.level, self.A, self.K, pitch, self.agents[sel], self.items[sel], self.t[sel])
+        taken = np.full((self.A, pitch), 4, np.uint8)
+        taken[:, :len(sel)] = self.taken[sel][:, :self.A].T
+        return s, taken.reshape(-1)
+
+    def compare(self, sel, value, flags, rtol=1e-12):
+        errs = []
+        for k, r in enumerate(sel):
+            raised = self.exp_raised[r]
+            if raised:
+                if not (flags[k] & (capi.LIK_RAISES | capi.LIK_ZERODIV)):
+                    errs.append("row %d: reference raised (%d), got flags %d value %r" % (self.idx[r], raised, flags[k],
+                                                                                      value[k]))
+                continue
+            if flags[k] != capi.LIK_OK or abs(value[k] - self.exp_value[r]) > rtol * abs(self.exp_value[r]):
+                errs.append("row %d: %r (flags %d) vs %r" % (self.idx[r], value[k], flags[k], self.exp_value[r]))
+            if len(errs) > 20:
+                break
+        return errs

@@ -2,6 +2,7 @@
 // so its logic can be checked against the CPU oracle and the reference rows without a GPU.
 // The loop mirrors oc_rollout_kernel's plane loads and stores; the product library never
 // contains this file.
+#include <math.h>
 #include <stdint.h>
 
 #define __device__
@@ -54,6 +55,52 @@ static void run(const oc_level_desc* lv, const uint8_t* sin, uint8_t* sout, cons
         flags[e] = (uint8_t)f;
         lb[e] = bound;
     }
+}
+
+template <int A, int K>
+static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* taken_p, const uint8_t* alloc,
+                const oc_subtask* subs, int nsub, int self_agent, double beta, double nap, double* out, uint8_t* flags,
+                int64_t B, int64_t P) {
+    static uint8_t dist[ocro::kMaxNodes * ocro::kMaxNodes];
+    ocro::RollLevel L;
+    ocro::build_roll_level(L, dist, lv->width, lv->height, lv->tiles);
+    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
+    for (int64_t e = 0; e < B; ++e) {
+        const int ai = alloc ? alloc[e] : 0;
+        double v = 0.0;
+        int f = OC_LIK_BADALLOC;
+        if (ai < nsub) {
+            ocro::Row r;
+            for (int a = 0; a < A; ++a) {
+                r.x |= (uint32_t)sin[a * P + e] << (8 * a);
+                r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
+                r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
+            }
+            for (int j = 0; j < K; ++j) {
+                r.loc |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
+                r.mask |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
+            }
+            uint32_t taken = 0;
+            for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
+            const oc_subtask& o = subs[ai];
+            ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
+                        {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, {0, 0}};
+            ocro::RowOps<A, K> ops(L, dist);
+            f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
+        }
+        out[e] = f == OC_LIK_OK ? v : 0.0;
+        flags[e] = (uint8_t)f;
+    }
+}
+
+extern "C" int lik_host(const oc_level_desc* lv, int A, int K, const uint8_t* sin, const uint8_t* taken,
+                        const uint8_t* alloc, const oc_subtask* subs, int nsub, int self_agent, double beta, double nap,
+                        double* out, uint8_t* flags, int64_t B, int64_t P) {
+#define L_(a, k) \
+    if (A == a && K == k) { lik<a, k>(lv, sin, taken, alloc, subs, nsub, self_agent, beta, nap, out, flags, B, P); return 0; }
+    L_(1, 4) L_(2, 4) L_(3, 4) L_(4, 4) L_(1, 8) L_(2, 8) L_(3, 8) L_(4, 8)
+#undef L_
+    return -1;
 }
 
 extern "C" int roll_host(const oc_level_desc* lv, int A, int K, const uint8_t* sin, uint8_t* sout, const uint8_t* act,

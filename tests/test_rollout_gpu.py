@@ -73,3 +73,19 @@ def test_rollout_single_config_and_bad_alloc():
     assert np.all(g_fl[bad] == capi.ROLL_BADALLOC) and np.all(g_lb[bad] == 0)
     v_in, v_out = tl.env_view(s, 2, ob.K, ob.pitch, ob.B), tl.env_view(g_out, 2, ob.K, ob.pitch, ob.B)
     assert np.array_equal(v_in[:, bad], v_out[:, bad])
+
+
+def test_rollout_flags_level0_double_removal():
+    import test_rollout_host as th  # noqa: F401
+    from gym_cooking_amd import levels
+    lv = levels.load_level("open-divider_salad")
+    ob = oracle.OracleBatch(lv, 3, 100, 4)
+    s = ob.new_state()
+    ob.reset(s)
+    v = tl.planes_view(s, 3, ob.K, ob.pitch)
+    v["ax"][2, :4], v["ay"][2, :4] = v["ax"][0, :4], v["ay"][0, :4]
+    subs = [capi.subtask(capi.SUB_CHOP, (1,), (0x01, 0), 0x11)]
+    acts = np.full(3 * ob.pitch, 3, np.uint8)
+    g_out, g_fl, g_lb = _gpu_rollout(lv, 3, 4, s, acts, subs, None)
+    assert np.all(g_fl == capi.ROLL_RAISES) and np.all(g_lb == 0)
+    assert np.array_equal(tl.env_view(g_out, 3, ob.K, ob.pitch, 4), tl.env_view(s, 3, ob.K, ob.pitch, 4))

@@ -111,3 +111,65 @@ def test_host_rollout_bad_alloc_rows_are_flagged():
     assert np.all(h_fl[bad] == capi.ROLL_BADALLOC) and np.all(h_lb[bad] == 0)
     v_in, v_out = tl.env_view(s, 2, ob.K, ob.pitch, ob.B), tl.env_view(h_out, 2, ob.K, ob.pitch, ob.B)
     assert np.array_equal(v_in[:, bad], v_out[:, bad])
+
+
+def host_likelihood(ob, s, taken, subs, alloc, self_agent, beta, nap):
+    L = _load()
+    if not hasattr(L, "_lik"):
+        vp = ctypes.c_void_p
+        L.lik_host.restype = ctypes.c_int
+        L.lik_host.argtypes = [ctypes.POINTER(capi.OcLevelDesc), ctypes.c_int, ctypes.c_int, vp, vp, vp,
+                               ctypes.POINTER(capi.OcSubtask), ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                               ctypes.c_double, vp, vp, ctypes.c_int64, ctypes.c_int64]
+        L._lik = True
+    out = np.zeros(ob.pitch, np.float64)
+    flags = np.zeros(ob.pitch, np.uint8)
+    rc = L.lik_host(ctypes.byref(ob.desc), ob.A, ob.K, _p(s), _p(taken), _p(alloc), capi.subtask_array(subs),
+                    len(subs), self_agent, beta, nap, _p(out), _p(flags), ob.B, ob.pitch)
+    assert rc == 0
+    return out[:ob.B], flags[:ob.B]
+
+
+@pytest.mark.parametrize("cfg", range(4))
+@pytest.mark.parametrize("self_agent", [0, 1])
+def test_host_likelihood_matches_reference(cfg, self_agent):
+    fx = tl.load_fixture("likelihood.npz")
+    rows = tl.LikelihoodRows(fx, cfg, self_agent)
+    for sel, alloc, subs in rows.chunks(capi.MAX_SUBTASKS):
+        ob = oracle.OracleBatch(rows.level, rows.A, 100, len(sel))
+        s, taken = rows.inputs(sel, ob.pitch)
+        a = np.zeros(ob.pitch, np.uint8)
+        a[:len(sel)] = alloc
+        v, f = host_likelihood(ob, s, taken, subs, a, self_agent, rows.beta, rows.nap)
+        errs = rows.compare(sel, v, f, 1e-12)
+        assert not errs, "\n".join(errs[:20])
+
+
+@pytest.mark.parametrize("level,A", [("open-divider_salad", 2), ("full-divider_salad", 4), ("partial-divider_tl", 3)])
+def test_host_likelihood_matches_oracle_random(level, A):
+    ob, s, acts, subs, alloc = random_rollout_case(level, A, 2000, seed=7 * A)
+    for self_agent in range(min(A, 2)):
+        o_v, o_f = ob.nav_likelihood(s, acts, subs, alloc, self_agent, 1.3, 0.5)
+        h_v, h_f = host_likelihood(ob, s, acts, subs, alloc, self_agent, 1.3, 0.5)
+        assert np.array_equal(o_f, h_f), np.argwhere(o_f != h_f)[:5]
+        ok = o_f == capi.LIK_OK
+        assert ok.sum() > 100
+        np.testing.assert_allclose(h_v[ok], o_v[ok], rtol=1e-13)
+
+
+def test_host_rollout_flags_level0_double_removal():
+    """Two agents outside the subtask on one square: the reference raises in set_settings."""
+    _load()
+    lv = levels.load_level("open-divider_salad")
+    ob = oracle.OracleBatch(lv, 3, 100, 4)
+    s = ob.new_state()
+    ob.reset(s)
+    v = tl.planes_view(s, 3, ob.K, ob.pitch)
+    v["ax"][2, :4], v["ay"][2, :4] = v["ax"][0, :4], v["ay"][0, :4]  # agents 1 and 3 co-located
+    subs = [capi.subtask(capi.SUB_CHOP, (1,), (0x01, 0), 0x11)]
+    acts = np.full(3 * ob.pitch, 3, np.uint8)
+    o_out = ob.new_state()
+    o_fl, o_lb = ob.rollout(s, o_out, acts, subs, None)
+    h_out, h_fl, h_lb = host_rollout(ob, s, acts, subs, None)
+    assert np.all(o_fl == capi.ROLL_RAISES) and np.all(h_fl == capi.ROLL_RAISES)
+    assert np.array_equal(tl.env_view(h_out, 3, ob.K, ob.pitch, 4), tl.env_view(s, 3, ob.K, ob.pitch, 4))
