@@ -117,12 +117,33 @@ def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 20) -> dict:
     ms = ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
     nbytes = 55 * rows
     legal = int((flags[:rows] & capi.ROLL_LEGAL).ne(0).sum())
-    return {"value": world * rows / (ms * 1e-3), "unit": "rollout rows/s", "rows_per_gpu": rows,
+    lik = measure_likelihood(eb, s, a, table, alloc, dev, world)
+    return {"value": world * rows / (ms * 1e-3), "unit": "rollout rows/s", "rows_per_gpu": rows, "likelihood": lik,
             "ms_per_launch": ms, "kernel": "oc_rollout_kernel<4,4>",
             "workload": "C5: full-divider_salad 4 agents, %d Salad (subtask, agents) configs, random joint actions"
                         % len(table),
             "algorithmic_bytes_per_row": 55, "achieved_GBs": nbytes / (ms * 1e-3) / 1e9,
             "frac_hbm": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "legal_rows": legal}
+
+
+def measure_likelihood(eb, states, taken, table, alloc, dev, world, reps: int = 5) -> dict:
+    """C5's consumer: Bayesian-delegation likelihoods (oc_nav_likelihood, prob_nav_actions with
+    value_init values) of the same rows -- every legal candidate action of a row is a rollout."""
+    from gym_cooking_amd import capi
+    for _ in range(2):
+        v, f = eb.nav_likelihood(states, taken, table, 0, 1.3, 0.5, alloc)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        v, f = eb.nav_likelihood(states, taken, table, 0, 1.3, 0.5, alloc)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
+    ok = int((f[:eb.B] == capi.LIK_OK).sum())
+    return {"value": world * eb.B / (ms * 1e-3), "unit": "likelihood rows/s", "ms_per_launch": ms,
+            "kernel": "oc_likelihood_kernel<4,4>", "rows_computed": ok, "bound": "compute (fp64 softmax over "
+            "up to 25 candidate rollouts per row)"}
 
 
 def load_traffic(path: str, kernel: str = "oc_step_n_kernel"):
