@@ -1,0 +1,274 @@
+"""Recipe subtasks of a level: the reference's STRIPS recipe decomposition (host side).
+
+``OvercookedEnvironment.all_subtasks`` (gym_cooking/envs/overcooked_environment.py:396-473)
+is the union, per recipe, of the actions on every shortest STRIPS plan from the level's
+initial predicates to ``Delivered(dish)``.  This module restates that computation:
+
+* subtasks ``Get / Chop / Merge / Deliver`` with their default and recipe-given pre- and
+  post-conditions (recipe_planner/utils.py:62-171);
+* each recipe's action set (recipe_planner/recipe.py:6-197: ``Get('Plate')``, per
+  ingredient ``Get / Chop / Merge(item, 'Plate', [Chopped(item), Fresh('Plate')])``,
+  ``Deliver(full_plate_name)``, and ``add_merge_actions`` over every ingredient combination);
+* the initial state ``NoPredicate + Fresh(name)`` per item content
+  (recipe_planner/stripsworld.py:13-31);
+* breadth-first search over predicate multisets to the first depth holding the goal, then
+  the union of actions over all shortest paths (stripsworld.py:38-123, ``is_valid_in`` /
+  ``get_next_from`` utils.py:84-99).
+
+The reference's result depends on Python's string hashing in two ways: the list order (it
+flattens sets), and which of two actions with the same transition survives -- its plan
+graph is a networkx DiGraph with one edge per (state, next state) pair, and the edge
+attribute is overwritten by whichever action the set iteration meets last
+(stripsworld.py:50-70), e.g. ``Merge(Tomato, Lettuce)`` vs ``Merge(Lettuce, Tomato)`` for
+Salad.  Here both are fixed: of parallel actions the one with the greatest ``str`` is kept
+(the choice the reference makes under PYTHONHASHSEED=0 for every builtin level), and the
+list is ordered by (plan depth, name).  tests/golden/gen_subtasks.py records the reference's
+variants under five hash seeds.
+
+``subtask_masks`` gives the start / goal content masks the navigation planner derives with
+``nav_utils.get_subtask_obj`` (navigation_planner/utils.py:181-246): the oc_subtask rows of
+``oc_rollout`` / ``oc_nav_likelihood``.
+"""
+from __future__ import annotations
+
+from itertools import combinations
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from . import levels as _levels
+
+_FOODS = ("Tomato", "Lettuce", "Onion")  # every food of recipe.py is FRESH_CHOPPED (core.py:311-350)
+_RECIPE_FOODS: Dict[str, Tuple[str, ...]] = {  # recipe.py:199-228, ingredient order
+    "SimpleTomato": ("Tomato",), "SimpleLettuce": ("Lettuce",),
+    "Salad": ("Tomato", "Lettuce"), "OnionSalad": ("Tomato", "Lettuce", "Onion"),
+}
+_NONE = "None"  # NoPredicate (utils.py:20-26) prints as 'None'
+
+
+def _join(names: Sequence[str]) -> str:
+    return "-".join(sorted(names))
+
+
+class Subtask:
+    """A STRIPS action used as a subtask (recipe_planner/utils.py:35-99): equal and hashed
+    by (name, args), printed ``Name(arg, ...)``."""
+
+    name = ""
+
+    def __init__(self, *args: str, pre: Optional[List[str]] = None, post: Optional[List[str]] = None):
+        self.args = tuple(args)
+        self.pre = list(pre) if pre is not None else self._pre_default()
+        self.post_add = list(post) if post is not None else self._post_default()
+        self.is_joint = False
+
+    def _pre_default(self) -> List[str]:
+        raise NotImplementedError
+
+    def _post_default(self) -> List[str]:
+        raise NotImplementedError
+
+    def __str__(self):
+        return "{}({})".format(self.name, ", ".join(self.args))
+
+    __repr__ = __str__
+
+    def __eq__(self, other):
+        return other is not None and getattr(other, "name", None) == self.name and \
+            tuple(getattr(other, "args", ())) == self.args
+
+    def __hash__(self):
+        return hash((self.name, self.args))
+
+    # STRIPS semantics over a predicate multiset (a sorted tuple of predicate strings)
+    def is_valid_in(self, state: Tuple[str, ...]) -> bool:  # utils.py:84-91
+        rest = list(state)
+        for p in self.pre:
+            if p not in rest:
+                return False
+            rest.remove(p)
+        return True
+
+    def get_next_from(self, state: Tuple[str, ...]) -> Tuple[str, ...]:  # utils.py:93-99
+        nxt = list(state)
+        for p in self.pre:
+            nxt.remove(p)
+        nxt += self.post_add
+        return tuple(sorted(nxt))
+
+
+class Get(Subtask):  # utils.py:107-118: None -> Fresh(X), None
+    name = "Get"
+
+    def _pre_default(self):
+        return [_NONE]
+
+    def _post_default(self):
+        return ["Fresh(%s)" % self.args[0], _NONE]
+
+
+class Chop(Subtask):  # utils.py:126-135: Fresh(X) -> Chopped(X)
+    name = "Chop"
+
+    def _pre_default(self):
+        return ["Fresh(%s)" % self.args[0]]
+
+    def _post_default(self):
+        return ["Chopped(%s)" % self.args[0]]
+
+
+class Merge(Subtask):  # utils.py:142-151: Chopped(X), Merged(Y) -> Merged(X-Y)
+    name = "Merge"
+
+    def _pre_default(self):
+        return ["Chopped(%s)" % self.args[0], "Merged(%s)" % self.args[1]]
+
+    def _post_default(self):
+        return ["Merged(%s)" % _join(self.args[0].split("-") + self.args[1].split("-"))]
+
+
+class Deliver(Subtask):  # utils.py:157-166: Merged(X) -> Delivered(X)
+    name = "Deliver"
+
+    def _pre_default(self):
+        return ["Merged(%s)" % self.args[0]]
+
+    def _post_default(self):
+        return ["Delivered(%s)" % self.args[0]]
+
+
+def recipe_actions(recipe: str) -> Tuple[List[Subtask], str]:
+    """(action set, goal predicate) of a recipe class (recipe.py:6-197).  The recipe adds
+    actions to a Python set, so of two equal actions (same name and args) the first added
+    one, with its pre-conditions, is kept."""
+    if recipe not in _RECIPE_FOODS:
+        raise ValueError("unknown recipe %r" % recipe)
+    uniq: Dict[Tuple[str, Tuple[str, ...]], Subtask] = {}
+    for act in _ordered_adds(recipe):
+        uniq.setdefault((act.name, act.args), act)
+    return list(uniq.values()), "Delivered(%s)" % _join(list(_RECIPE_FOODS[recipe]) + ["Plate"])
+
+
+def _ordered_adds(recipe: str) -> List[Subtask]:
+    """The recipe's ``actions.add`` calls in program order (a set keeps the first of equals)."""
+    out: List[Subtask] = [Get("Plate")]
+    foods = _RECIPE_FOODS[recipe]
+    for f in foods:
+        out += [Get(f), Chop(f), Merge(f, "Plate", pre=["Chopped(%s)" % f, "Fresh(Plate)"])]
+    names = sorted(foods)
+    out.append(Deliver(_join(list(names) + ["Plate"])))
+    for i in range(2, len(names) + 1):
+        for combo in combinations(names, i):
+            out.append(Merge(_join(combo), "Plate", pre=["Merged(%s)" % _join(combo), "Fresh(Plate)"]))
+            for item in combo:
+                rem = list(combo)
+                rem.remove(item)
+                rem_str, plate_str, rem_plate = _join(rem), _join([item, "Plate"]), _join(rem + ["Plate"])
+                if len(rem) == 1:
+                    out += [Merge(item, rem_str, pre=["Chopped(%s)" % item, "Chopped(%s)" % rem_str]),
+                            Merge(rem_str, plate_str), Merge(item, rem_plate)]
+                else:
+                    out += [Merge(item, rem_str),
+                            Merge(plate_str, rem_str, pre=["Merged(%s)" % plate_str, "Merged(%s)" % rem_str]),
+                            Merge(item, rem_plate)]
+    return out
+
+
+def initial_state(level: "_levels.Level") -> Tuple[str, ...]:
+    """STRIPSWorld initial predicates (stripsworld.py:13-31): None + Fresh(name) per content."""
+    preds = [_NONE]
+    for _cell, mask in level.items:
+        for name, bit in (("Plate", _levels.M_PLATE),) + tuple(zip(_FOODS, (_levels.M_TOMATO, _levels.M_LETTUCE,
+                                                                             _levels.M_ONION))):
+            if mask & bit:
+                preds.append("Fresh(%s)" % name)
+    return tuple(sorted(preds))
+
+
+def plan_subtasks(level: "_levels.Level", recipe: str, max_path_length: int = 14) -> List[Subtask]:
+    """Union of the actions on all shortest plans of one recipe (stripsworld.py:38-123),
+    ordered by (plan depth, str)."""
+    actions, goal = recipe_actions(recipe)
+    init = initial_state(level)
+    seen = {init}
+    layers = [[init]]
+    goal_states: List[Tuple[str, ...]] = []
+    for _ in range(max_path_length):  # generate_graph: breadth-first, stop at the first goal layer
+        nxt: List[Tuple[str, ...]] = []
+        for s in layers[-1]:
+            for a in actions:
+                if a.is_valid_in(s):
+                    n = a.get_next_from(s)
+                    if n not in seen:
+                        seen.add(n)
+                        nxt.append(n)
+                        if goal in n:
+                            goal_states.append(n)
+        layers.append(nxt)
+        if goal_states:
+            break
+    if not goal_states:  # the reference prints and sys.exit(0)s (stripsworld.py:58-60)
+        raise RuntimeError("goal state could not be found, try increasing --max-num-subtasks")
+    if len(goal_states) != 1:
+        raise RuntimeError("recipe %s reaches %d distinct goal states at the same depth; the reference "
+                           "keeps whichever its set iteration meets first" % (recipe, len(goal_states)))
+    # one edge per (state, next state) pair, as in the DiGraph: parallel actions collapse
+    # to the one with the greatest str
+    def edges(s):
+        out: Dict[Tuple[str, ...], Subtask] = {}
+        for a in actions:
+            if a.is_valid_in(s):
+                n = a.get_next_from(s)
+                if n not in out or str(a) > str(out[n]):
+                    out[n] = a
+        return out
+
+    # nx.all_shortest_paths(initial -> goal): sweep back over the layers, keeping the states
+    # with an edge into the previous sweep's set and the actions on those edges
+    on_path = {goal_states[0]}
+    depth_of: Dict[Subtask, int] = {}
+    for d in range(len(layers) - 2, -1, -1):
+        keep = set()
+        for s in layers[d]:
+            for n, a in edges(s).items():
+                if n in on_path:
+                    keep.add(s)
+                    depth_of[a] = min(depth_of.get(a, d), d)
+        on_path = keep
+    return sorted(depth_of, key=lambda a: (depth_of[a], str(a)))
+
+
+def all_subtasks(level: "_levels.Level", max_path_length: int = 14) -> List[Subtask]:
+    """``OvercookedEnvironment.all_subtasks`` (run_recipes, overcooked_environment.py:396-473):
+    the per-recipe unions, concatenated in recipe order (duplicates across recipes kept)."""
+    out: List[Subtask] = []
+    for r in level.recipes:
+        out += plan_subtasks(level, r, max_path_length)
+    return out
+
+
+def _name_mask(names: str, chopped: bool) -> int:
+    m = 0
+    for n in names.split("-"):
+        if n == "Plate":
+            m |= _levels.M_PLATE
+            continue
+        bit = {"Tomato": _levels.M_TOMATO, "Lettuce": _levels.M_LETTUCE, "Onion": _levels.M_ONION}[n]
+        m |= bit | (_levels.chopped(bit) if chopped else 0)
+    return m
+
+
+def subtask_masks(subtask: Optional[Subtask]) -> Tuple[int, Tuple[int, int], int]:
+    """(OC_SUB_* kind, (start mask a, start mask b), goal mask) as nav_utils.get_subtask_obj
+    builds them (navigation_planner/utils.py:181-246): Chop: fresh -> chopped food;
+    Merge: both arguments with every food in its last (chopped) state, a bare Plate as is,
+    goal = their union; Deliver: the plated dish, start == goal."""
+    if subtask is None:
+        return 0, (0, 0), 0
+    if subtask.name == "Chop":
+        return 1, (_name_mask(subtask.args[0], False), 0), _name_mask(subtask.args[0], True)
+    if subtask.name == "Merge":
+        a, b = _name_mask(subtask.args[0], True), _name_mask(subtask.args[1], True)
+        return 2, (a, b), a | b
+    if subtask.name == "Deliver":
+        m = _name_mask(subtask.args[0], True)
+        return 3, (m, 0), m
+    raise NotImplementedError("{} was not recognized".format(subtask))  # utils.py:244-245

@@ -12,7 +12,7 @@ from gym_cooking_amd import envs, levels
 from oracle import oracle
 
 
-@pytest.mark.parametrize("fixture", ["kat.npz", "streams.npz"])
+@pytest.mark.parametrize("fixture", ["kat.npz", "streams.npz", "greedy.npz"])
 def test_is_collision_reproduces_reference_exec_and_pairs(fixture):
     """check_collisions (overcooked_environment.py:724-762) rebuilt from envs.is_collision on
     the fixture's pre-step agent locations and original actions == the reference's executed

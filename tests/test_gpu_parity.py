@@ -39,7 +39,7 @@ def _gpu_step_fn(eb):
     return fn
 
 
-@pytest.mark.parametrize("fixture", ["kat.npz", "streams.npz"])
+@pytest.mark.parametrize("fixture", ["kat.npz", "streams.npz", "greedy.npz"])
 def test_engine_matches_reference_fixtures(dev, fixture):
     fx = tl.load_fixture(fixture)
     for g in tl.episode_groups(fx):

@@ -57,7 +57,7 @@ def _step_fn(sb):
     return fn
 
 
-@pytest.mark.parametrize("fixture", ["kat.npz", "streams.npz"])
+@pytest.mark.parametrize("fixture", ["kat.npz", "streams.npz", "greedy.npz"])
 def test_swar_step_matches_reference_fixtures(fixture):
     _load()
     fx = tl.load_fixture(fixture)
