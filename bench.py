@@ -146,6 +146,42 @@ def measure_likelihood(eb, states, taken, table, alloc, dev, world, reps: int = 
             "up to 25 candidate rollouts per row)"}
 
 
+def measure_render(dev, world, level: str, A: int, B: int = 1024, reps: int = 10) -> dict:
+    """Secondary line, SURVEY 8(f) #4: image observations (oc_render, GameImage.get_image_obs)
+    of B mid-episode random-play states.  Algorithmic bytes per image: the u8 [H*80, W*80, 3]
+    output plus the env's state bytes (the static level image and sprites are L2-resident
+    and read by every env)."""
+    from gym_cooking_amd.engine import OvercookedBatch
+    from gym_cooking_amd.render import Renderer
+    eb = OvercookedBatch(level, A, B, max_T=100, device=dev)
+    s, s2 = eb.new_state(), eb.new_state()
+    eb.reset(s)
+    a = eb.new_actions()
+    for t in range(37):
+        eb.gen_actions(a, t, 13)
+        eb.step(s, s2, a)
+        s, s2 = s2, s
+    rd = Renderer(eb)
+    out = rd.new_images()
+    for _ in range(2):
+        rd.render(s, out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        rd.render(s, out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
+    img_bytes = out[0].numel()
+    nbytes = B * (img_bytes + eb.layout.num_planes)
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"value": world * B / (ms * 1e-3), "unit": "images/s", "envs_per_gpu": B, "ms_per_launch": ms,
+            "kernel": "oc_render_kernel<%d,%d>" % (A, eb.K), "image_shape": list(out.shape[1:]),
+            "algorithmic_bytes_per_image": img_bytes + eb.layout.num_planes, "achieved_GBs": gbs,
+            "frac_hbm": gbs / HBM_PEAK_GBS, "bound": "hbm (writes)"}
+
+
 def load_traffic(path: str, kernel: str = "oc_step_n_kernel"):
     """Calibrated HBM bytes per launch of `kernel` from tools/pmc_report.py's output."""
     try:
@@ -215,6 +251,7 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-step", action="store_true", help="skip the secondary one-launch-per-step line")
     ap.add_argument("--no-rollout", action="store_true", help="skip the secondary oc_rollout (C5) measurement")
+    ap.add_argument("--no-render", action="store_true", help="skip the secondary oc_render measurement")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -333,6 +370,8 @@ def main() -> int:
         line["per_step_launch"]["traffic"] = load_traffic(args.traffic_json, "oc_step_kernel")[0]
     if not args.no_rollout:
         line["rollout"] = measure_rollout(dev, world)
+    if not args.no_render:
+        line["render"] = measure_render(dev, world, args.level, args.agents)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget, threads)

@@ -15,6 +15,7 @@
 //   oc_step_n_kernel  n steps per launch with the state in registers; every step's state,
 //                     executed actions and collision mask are still written.
 //   oc_rollout_kernel navigation-planner rollout rows (oc_rollout.h).
+//   oc_render_kernel  image observations.
 //   reset / gen_actions / checksum / stats_reduce helpers.
 // All of them accumulate nothing on the host; statistics are per-block rows of no-return
 // 64-bit atomics reduced by oc_stats_reduce for the all-gather of episode summaries.
@@ -461,6 +462,130 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
     }
 }
 
+// Image observation (oc_render, GameImage.get_image_obs: gym_cooking/misc/game/gameimage.py:31-51,
+// Game.on_render / draw_*: game.py:56-186).  One block per (env, cell row): the first W lanes
+// build each cell's ordered draw list in LDS (items not held in slot order, then every agent
+// in order followed by its held item), then the block writes the row's tile*W*tile*3 output
+// bytes, 4 pixels (12 bytes, three dwords) per lane and iteration, consecutive lanes on
+// consecutive pixels.  A pixel starts from the static level image and blends every sprite of
+// its cell's list that covers it.  Everything is tile-local: every sprite lies inside its cell.
+struct RenderArgs {
+    int32_t W, H, tile;
+    int32_t size[OC_RENDER_SIZES], offset[OC_RENDER_SIZES], food_base[OC_RENDER_SIZES];
+    int32_t plate_off[2], agent_off[OC_MAX_AGENTS];
+    uint32_t chan_map;
+    int64_t pitch;
+    uint8_t food_sprite[128];
+};
+constexpr int kRenderMaxW = 32, kRenderMaxDraw = 2 * OC_MAX_ITEMS + 3 * OC_MAX_AGENTS;
+
+// SDL 1.2 per-pixel alpha blit of an RGBA source pixel onto an RGB destination pixel
+// (BlitNtoNPixelAlpha / ALPHA_BLEND: d = (((s - d) * a + 255) >> 8) + d per channel, a = 0 skipped).
+__device__ __forceinline__ uint32_t sdl_blend(uint32_t d, uint32_t s) {
+    const int a = (int)(s >> 24);
+    if (a == 0) return d;
+    uint32_t out = 0u;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int sc = (int)((s >> (8 * c)) & 0xFFu), dc = (int)((d >> (8 * c)) & 0xFFu);
+        out |= (uint32_t)((((sc - dc) * a + 255) >> 8) + dc) << (8 * c);
+    }
+    return out;
+}
+
+__device__ __forceinline__ uint32_t chan_byte(uint32_t px, uint32_t sel) {
+    return sel >= 3u ? 0u : (px >> (8u * sel)) & 0xFFu;
+}
+
+template <int A, int K>
+__global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const uint8_t* __restrict__ state,
+                                                           const uint32_t* __restrict__ atlas,
+                                                           const uint32_t* __restrict__ bg,
+                                                           uint8_t* __restrict__ out) {
+    __shared__ uint32_t dl_off[kRenderMaxW][kRenderMaxDraw];
+    __shared__ uint32_t dl_geo[kRenderMaxW][kRenderMaxDraw];  // size | offset << 16
+    __shared__ int32_t dl_n[kRenderMaxW];
+    const int64_t e = blockIdx.x / (uint32_t)R.H;
+    const int ty = (int)(blockIdx.x % (uint32_t)R.H);
+    const int W = R.W, tile = R.tile;
+    constexpr int kPX = 0, kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
+    if ((int)threadIdx.x < W) {
+        const int tx = threadIdx.x, cell = ty * W + tx;
+        const uint8_t* s = state + e;
+        const int64_t P = R.pitch;
+        uint32_t held = 0u;
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            const uint32_t h = s[(kPH + a) * P];
+            if (h < (uint32_t)K) held |= 1u << h;
+        }
+        int n = 0;
+        auto push = [&](int32_t off, int cls) {
+            dl_off[tx][n] = (uint32_t)off;
+            dl_geo[tx][n] = (uint32_t)R.size[cls] | ((uint32_t)R.offset[cls] << 16);
+            ++n;
+        };
+        // an item: a plate first, its contents at the container class; else the food itself
+        auto push_item = [&](uint32_t m, int cls_plain, int cls_in_plate, int plate) {
+            const uint32_t f = m & ~OC_M_PLATE;
+            if (m & OC_M_PLATE) push(R.plate_off[plate], cls_plain);
+            const int cls = (m & OC_M_PLATE) ? cls_in_plate : cls_plain;
+            if (f != 0u && R.food_sprite[f] != 0xFFu)
+                push(R.food_base[cls] + (int32_t)R.food_sprite[f] * R.size[cls] * R.size[cls], cls);
+        };
+        // Game.on_render: objects not held (draw_object, game.py:138-160) ...
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (s[(kPL + j) * P] == (uint8_t)cell && !((held >> j) & 1u)) push_item(s[(kPM + j) * P], 0, 1, 0);
+        // ... then the agents in order, each with its held object (draw_agent / draw_agent_object, :98-136)
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            if ((int)s[(kPY + a) * P] * W + (int)s[(kPX + a) * P] != cell) continue;
+            push(R.agent_off[a], 0);
+            const uint32_t h = s[(kPH + a) * P];
+            if (h < (uint32_t)K) push_item(s[(kPM + h) * P], 2, 3, 1);
+        }
+        dl_n[tx] = n;
+    }
+    __syncthreads();
+    const int row_px = W * tile, G = row_px / 4;  // 4-pixel groups per image row
+    const int items = tile * G;
+    const int64_t img_bytes = (int64_t)R.H * tile * row_px * 3;
+    uint8_t* img = out + e * img_bytes;
+    for (int i = threadIdx.x; i < items; i += kBlock) {
+        const int r = i / G, g = i - r * G;
+        const int py = ty * tile + r, px0 = 4 * g;
+        const uint4 b4 = *(const uint4*)(bg + (int64_t)py * row_px + px0);
+        uint32_t p[4] = {b4.x, b4.y, b4.z, b4.w};
+        const int tx = px0 / tile, lx0 = px0 - tx * tile;
+        const int n = dl_n[tx];
+        for (int d = 0; d < n; ++d) {
+            const uint32_t geo = dl_geo[tx][d];
+            const int sz = (int)(geo & 0xFFFFu), o = (int)(geo >> 16);
+            const int dy = r - o;
+            if ((unsigned)dy >= (unsigned)sz) continue;
+            const uint32_t* spr = atlas + dl_off[tx][d] + dy * sz;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int dx = lx0 + k - o;
+                if ((unsigned)dx < (unsigned)sz) p[k] = sdl_blend(p[k], spr[dx]);
+            }
+        }
+        const uint32_t c0 = R.chan_map & 0xFFu, c1 = (R.chan_map >> 8) & 0xFFu, c2 = (R.chan_map >> 16) & 0xFFu;
+        uint32_t bytes[12];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bytes[3 * k] = chan_byte(p[k], c0);
+            bytes[3 * k + 1] = chan_byte(p[k], c1);
+            bytes[3 * k + 2] = chan_byte(p[k], c2);
+        }
+        uint32_t* dst = (uint32_t*)(img + ((int64_t)py * row_px + px0) * 3);
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+            dst[w] = bytes[4 * w] | (bytes[4 * w + 1] << 8) | (bytes[4 * w + 2] << 16) | (bytes[4 * w + 3] << 24);
+    }
+}
+
 // reset(): broadcast the level template (overcooked_environment.py:201-250).
 template <int A, int K>
 __global__ __launch_bounds__(kBlock) void oc_reset_kernel(LevelArgs L, uint8_t* __restrict__ s) {
@@ -887,6 +1012,47 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
                        alloc, h->roll_dist, self_agent, beta, none_action_prob, likelihood, out_flags)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_LIK)
     return hip_check("oc_nav_likelihood launch");
+}
+
+int oc_render(const oc_handle* h, const void* state, const uint32_t* atlas, const uint32_t* background,
+              const oc_render_desc* desc, uint8_t* out, int64_t B, void* stream) {
+    if (h == nullptr || state == nullptr || atlas == nullptr || background == nullptr || desc == nullptr ||
+        out == nullptr || B < 0)
+        return fail(OC_EINVAL, "bad argument");
+    const int W = h->level.width, H = h->level.height;
+    if (W > kRenderMaxW) return fail(OC_ELEVEL, "render: width %d > %d", W, kRenderMaxW);
+    if (desc->tile < 4 || desc->tile % 4 != 0 || desc->tile > 1024) return fail(OC_EINVAL, "render: tile %d", desc->tile);
+    for (int c = 0; c < OC_RENDER_SIZES; ++c)
+        if (desc->size[c] < 0 || desc->offset[c] < 0 || desc->size[c] + desc->offset[c] > desc->tile)
+            return fail(OC_EINVAL, "render: size class %d (%d at %d) leaves the %d-px cell", c, desc->size[c],
+                        desc->offset[c], desc->tile);
+    for (int q = 0; q < 3; ++q)
+        if (((desc->chan_map >> (8 * q)) & 0xFFu) > 3u) return fail(OC_EINVAL, "render: chan_map 0x%x", desc->chan_map);
+    if (((uintptr_t)atlas | (uintptr_t)background | (uintptr_t)out) & 15u) return fail(OC_EINVAL, "misaligned buffer");
+    if (B == 0) return OC_OK;
+    if (B * H > 0x7FFFFFFFll) return fail(OC_EINVAL, "render: batch too large");
+    RenderArgs R;
+    R.W = W;
+    R.H = H;
+    R.tile = desc->tile;
+    for (int c = 0; c < OC_RENDER_SIZES; ++c) {
+        R.size[c] = desc->size[c];
+        R.offset[c] = desc->offset[c];
+        R.food_base[c] = desc->food_base[c];
+    }
+    R.plate_off[0] = desc->plate_off[0];
+    R.plate_off[1] = desc->plate_off[1];
+    for (int a = 0; a < OC_MAX_AGENTS; ++a) R.agent_off[a] = desc->agent_off[a];
+    R.chan_map = desc->chan_map;
+    R.pitch = pitch_for(B);
+    for (int m = 0; m < 128; ++m) R.food_sprite[m] = desc->food_sprite[m];
+    const dim3 grid((unsigned)(B * H));
+    hipStream_t st = (hipStream_t)stream;
+#define OC_LAUNCH_RENDER(A, K)                                                                               \
+    hipLaunchKernelGGL((oc_render_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state, atlas, \
+                       background, out)
+    OC_DISPATCH(h->A, h->K, OC_LAUNCH_RENDER)
+    return hip_check("oc_render launch");
 }
 
 int oc_gen_actions(const oc_handle* h, uint8_t* actions, int64_t B, int64_t env_offset, int64_t step,

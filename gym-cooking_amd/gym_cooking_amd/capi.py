@@ -30,7 +30,8 @@ OC_STAT_NAMES = ("episodes", "successes", "steps", "collisions", "errors")
 # Every symbol include/oc_engine.h declares (tests check the library exports them all).
 EXPORTED_SYMBOLS = (
     "oc_abi_version", "oc_last_error", "oc_create", "oc_destroy", "oc_get_layout", "oc_reset",
-    "oc_step", "oc_step_n", "oc_rollout", "oc_nav_likelihood", "oc_gen_actions", "oc_state_checksum", "oc_stats_size", "oc_stats_reduce",
+    "oc_step", "oc_step_n", "oc_rollout", "oc_nav_likelihood", "oc_render", "oc_gen_actions", "oc_state_checksum",
+    "oc_stats_size", "oc_stats_reduce",
 )
 
 
@@ -68,6 +69,19 @@ class OcSubtask(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("num_agents", ctypes.c_int32), ("agent", ctypes.c_uint8 * 2),
                 ("start_mask", ctypes.c_uint8 * 2), ("goal_mask", ctypes.c_uint8),
                 ("goal_count", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 2)]
+
+
+OC_RENDER_SIZES = 4
+OC_CHAN_RGB = 0x00020100
+OC_CHAN_REFERENCE = 0x00030100
+
+
+class OcRenderDesc(ctypes.Structure):
+    """oc_render_desc (include/oc_engine.h): sprite atlas layout and output channel map."""
+    _fields_ = [("tile", ctypes.c_int32), ("size", ctypes.c_int32 * OC_RENDER_SIZES),
+                ("offset", ctypes.c_int32 * OC_RENDER_SIZES), ("food_base", ctypes.c_int32 * OC_RENDER_SIZES),
+                ("plate_off", ctypes.c_int32 * 2), ("agent_off", ctypes.c_int32 * OC_MAX_AGENTS),
+                ("food_sprite", ctypes.c_uint8 * 128), ("chan_map", ctypes.c_uint32)]
 
 
 def subtask(kind: int, agents, start_masks, goal_mask: int, goal_count: int = 0) -> OcSubtask:
@@ -159,6 +173,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.oc_nav_likelihood.restype = ctypes.c_int
     lib.oc_nav_likelihood.argtypes = [vp, vp, vp, vp, ctypes.POINTER(OcSubtask), i32, i32, ctypes.c_double,
                                       ctypes.c_double, vp, vp, i64, vp]
+    lib.oc_render.restype = ctypes.c_int
+    lib.oc_render.argtypes = [vp, vp, vp, vp, ctypes.POINTER(OcRenderDesc), vp, i64, vp]
     lib.oc_step_n.restype = ctypes.c_int
     lib.oc_step_n.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]
     lib.oc_gen_actions.restype = ctypes.c_int

@@ -264,6 +264,41 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
                       const oc_subtask* subtasks, int32_t num_subtasks, int32_t self_agent, double beta,
                       double none_action_prob, double* likelihood, uint8_t* out_flags, int64_t B, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Image observation: what GameImage.get_image_obs returns after on_render
+ *   gym_cooking/misc/game/gameimage.py:31-51, game.py:56-186
+ * per env: the static level image (floor fill, counters with a 1-px border, delivery and
+ * cutboard sprites; built once on the host by gym_cooking_amd/render.py), then every item
+ * that is not held (tile-size sprite; a plate first, its contents at the container size /
+ * offset), then each agent in order with its held item (holding size / offset), each sprite
+ * blended per pixel with SDL 1.2's ALPHA_BLEND (d += ((s - d) * a + 255) >> 8, a = 0 skipped).
+ * Output u8 [B][H*tile][W*tile][3]; byte c of a pixel = source channel (chan_map >> 8c) & 0xFF
+ * (0 R, 1 G, 2 B, 3 constant 0).  The reference reads its 0x00RRGGBB pixels through
+ * pygame.Color(int) (0xRRGGBBAA) and stores (g, b, r) = (R, G, 0): OC_CHAN_REFERENCE.
+ * ------------------------------------------------------------------------------------- */
+#define OC_RENDER_SIZES 4          /* tile, container, holding, holding container */
+#define OC_CHAN_RGB 0x00020100u
+#define OC_CHAN_REFERENCE 0x00030100u
+
+typedef struct {
+    int32_t tile;                         /* pixels per cell (Game.scale, 80) */
+    int32_t size[OC_RENDER_SIZES];        /* sprite edge per size class: 80, 56, 40, 28 */
+    int32_t offset[OC_RENDER_SIZES];      /* sprite origin inside its cell: 0, 12, 40, 46 */
+    int32_t food_base[OC_RENDER_SIZES];   /* atlas pixel offset of food sprite 0 of each size class;
+                                             food sprite i of class c at food_base[c] + i*size[c]^2 */
+    int32_t plate_off[2];                 /* plate sprite at tile size, at holding size */
+    int32_t agent_off[OC_MAX_AGENTS];     /* agent-<colour> sprite (utils/agent.py:25 colour order) */
+    uint8_t food_sprite[128];             /* plate-less content mask -> food sprite index, 0xFF none */
+    uint32_t chan_map;                    /* OC_CHAN_* */
+} oc_render_desc;
+
+/*   state      : B states (oc_layout)
+ *   atlas      : device u32 RGBA sprites (R | G<<8 | B<<16 | A<<24), laid out as desc says
+ *   background : device u32 RGBX [H*tile][W*tile], the static level image
+ *   out        : device u8 [B][H*tile][W*tile][3] */
+int oc_render(const oc_handle* h, const void* state, const uint32_t* atlas, const uint32_t* background,
+              const oc_render_desc* desc, uint8_t* out, int64_t B, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

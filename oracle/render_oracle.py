@@ -1,0 +1,113 @@
+"""CPU restatement of the image observation (test infrastructure only).
+
+Checks oc_render.  Only tests/ may import this; the product path never does.
+
+It restates GameImage.get_image_obs (gym_cooking/misc/game/gameimage.py:31-51) over
+Game.on_render (gym_cooking/misc/game/game.py:56-186) literally, one env at a time in numpy:
+  screen.fill(Color.FLOOR)                                    game.py:63
+  draw_gridsquare per square: Counter / Delivery / Cutboard   game.py:80-96
+  draw_object per object not held                             game.py:68-74, 138-160
+  draw_agent per agent + draw_agent_object                    game.py:76-77, 98-136
+  blit = SDL 1.2 per-pixel alpha ALPHA_BLEND                  d += ((s - d) * a + 255) >> 8, a > 0
+  PixelArray -> pygame.Color(int) -> (g, b, r)                gameimage.py:44-51
+It decodes objects from the engine's state planes itself.  The only thing it shares with the
+product is the sprite data (gym_cooking_amd/assets/sprites.npz, tools/gen_sprites.py).
+
+Parity unpinned: pygame/SDL are not available, so the reference's own images cannot be
+generated.  This restatement is checked on its geometry and on hand-computed pixels
+(tests/test_render.py).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SPRITES = os.path.join(ROOT, "gym-cooking_amd", "gym_cooking_amd", "assets", "sprites.npz")
+
+SCALE = 80                                   # game.py:26
+FLOOR = (245, 230, 210)                      # misc/game/utils.py Color
+COUNTER = (220, 170, 110)
+COUNTER_BORDER = (114, 93, 51)
+DELIVERY = (96, 96, 96)
+COLORS = ["blue", "magenta", "yellow", "green"]   # utils/agent.py:25
+NAMES = [(0x02, "Lettuce"), (0x04, "Onion"), (0x01, "Tomato")]   # sorted by name (core.py:161-171)
+
+
+def _sprites():
+    with np.load(SPRITES) as z:
+        return {k: z[k] for k in z.files}
+
+
+def _blit(screen, img, x0, y0):
+    h, w = img.shape[:2]
+    d = screen[y0:y0 + h, x0:x0 + w].astype(np.int64)
+    s = img[..., :3].astype(np.int64)
+    a = img[..., 3:4].astype(np.int64)
+    screen[y0:y0 + h, x0:x0 + w] = np.where(a == 0, d, (((s - d) * a + 255) >> 8) + d).astype(np.uint8)
+
+
+def _full_name(mask):
+    """Object.full_name without the plate: state + name, sorted by name."""
+    parts = ["%s%s" % ("Chopped" if mask & (bit << 4) else "Fresh", n) for bit, n in NAMES if mask & bit]
+    return "-".join(parts)
+
+
+def _draw_obj(screen, spr, mask, x, y, held):
+    holding, container = int(0.5 * SCALE), int(0.7 * SCALE)
+    hc = int(0.7 * holding)
+    if held:
+        off_plain = int(SCALE * (1 - 0.5))
+        off_in = int(SCALE * ((1 - 0.5) + (1 - 0.7) / 2 * 0.5))
+        size_plain, size_in = holding, hc
+    else:
+        off_plain, off_in = 0, int(SCALE * (1 - 0.7) / 2)
+        size_plain, size_in = SCALE, container
+    if mask & 0x08:  # any Plate in contents
+        _blit(screen, spr["Plate@%d" % size_plain], x * SCALE + off_plain, y * SCALE + off_plain)
+        if mask & 0x07:  # len(obj.contents) > 1
+            _blit(screen, spr["%s@%d" % (_full_name(mask), size_in)], x * SCALE + off_in, y * SCALE + off_in)
+    else:
+        _blit(screen, spr["%s@%d" % (_full_name(mask), size_plain)], x * SCALE + off_plain, y * SCALE + off_plain)
+
+
+def render_env(level, env_bytes, A, K, spr=None, channels="reference"):
+    """One env's image from its state bytes (ax[A] ay[A] ah[A] loc[K] mask[K] t_lo t_hi flags)."""
+    spr = _sprites() if spr is None else spr
+    W, H = level.width, level.height
+    b = [int(v) for v in env_bytes]
+    ax, ay, ah = b[0:A], b[A:2 * A], b[2 * A:3 * A]
+    loc, mask = b[3 * A:3 * A + K], b[3 * A + K:3 * A + 2 * K]
+    screen = np.empty((H * SCALE, W * SCALE, 3), np.uint8)
+    screen[...] = FLOOR
+    for c, kind in enumerate(level.tiles):
+        x, y = c % W, c // W
+        if kind == 0:
+            continue
+        r = screen[y * SCALE:(y + 1) * SCALE, x * SCALE:(x + 1) * SCALE]
+        if kind in (1, 2):
+            r[...] = COUNTER
+            r[0, :] = COUNTER_BORDER
+            r[-1, :] = COUNTER_BORDER
+            r[:, 0] = COUNTER_BORDER
+            r[:, -1] = COUNTER_BORDER
+        if kind == 3:
+            r[...] = DELIVERY
+            _blit(screen, spr["delivery@80"], x * SCALE, y * SCALE)
+        if kind == 2:
+            _blit(screen, spr["cutboard@80"], x * SCALE, y * SCALE)
+    held = {h for h in ah if h < K}
+    for j in range(K):
+        if loc[j] != 0xFF and j not in held:
+            _draw_obj(screen, spr, mask[j], loc[j] % W, loc[j] // W, False)
+    for a in range(A):
+        _blit(screen, spr["agent-%s@80" % COLORS[a]], ax[a] * SCALE, ay[a] * SCALE)
+        if ah[a] < K:
+            _draw_obj(screen, spr, mask[ah[a]], ax[a], ay[a], True)
+    if channels == "rgb":
+        return screen
+    out = np.zeros_like(screen)  # Color(0x00RRGGBB) -> r=0, g=R, b=G; stored (g, b, r)
+    out[..., 0] = screen[..., 0]
+    out[..., 1] = screen[..., 1]
+    return out

@@ -1,0 +1,161 @@
+"""Image observations (GameImage.get_image_obs, gym_cooking/misc/game/).
+
+Parity unpinned: pygame/SDL are absent, so no reference image exists.  The kernel
+(oc_render) is checked bit-exact against the independent numpy restatement
+oracle/render_oracle.py on fixture states recorded from the reference (streams.npz,
+greedy.npz: plates, merged and delivered dishes, held items, 2-4 agents).  The restatement's
+constants are checked against the values the reference's expressions evaluate to."""
+import numpy as np
+import pytest
+
+import oc_testlib as tl
+from gym_cooking_amd import capi, levels, render
+
+from oracle import render_oracle
+
+
+def test_geometry_is_the_references():
+    """game.py:26-33 sizes and :166-186 offsets, as numpy's astype(int) evaluates them."""
+    t = np.asarray((80, 80))
+    hold = tuple((0.5 * t).astype(int))
+    assert render.SIZES == (80, int((0.7 * t).astype(int)[0]), hold[0], int((0.7 * np.asarray(hold)).astype(int)[0]))
+    assert render.SIZES == (80, 56, 40, 28)
+    sl = np.asarray((3 * 80, 2 * 80))
+    assert tuple((sl + 80 * (1 - 0.5)).astype(int) - sl) == (40, 40)
+    assert tuple((sl + 80 * (1 - 0.7) / 2).astype(int) - sl) == (12, 12)
+    assert tuple((sl + 80 * ((1 - 0.5) + (1 - 0.7) / 2 * 0.5)).astype(int) - sl) == (46, 46)
+    assert render.OFFSETS == (0, 12, 40, 46)
+
+
+def test_sdl_blend_values():
+    d = np.array([[10, 200, 255]], np.uint8)
+    assert render.sdl_blend(d, np.array([[255, 0, 0, 0]], np.uint8)).tolist() == [[10, 200, 255]]  # a = 0: skipped
+    # opaque, darker source: ((0 - 200) * 255 + 255) >> 8 = -199, so 200 -> 1, not 0
+    assert render.sdl_blend(d, np.array([[255, 0, 0, 255]], np.uint8)).tolist() == [[255, 1, 1]]
+    # (s - d) * a + 255 >> 8: 10 + ((100 - 10) * 128 + 255 >> 8) = 10 + 45; 200 + ((-200 * 128 + 255) >> 8) = 100
+    assert render.sdl_blend(d, np.array([[100, 0, 255, 128]], np.uint8)).tolist() == [[55, 100, 255]]
+    # a = 255 and s = d - 1 leaves d (ALPHA_BLEND's +255 rounding)
+    assert render.sdl_blend(np.array([[7, 7, 7]], np.uint8), np.array([[6, 6, 6, 255]], np.uint8)).tolist() == [[7, 7, 7]]
+
+
+def test_every_reachable_item_has_a_sprite():
+    """Every item mask in the reference fixtures maps to a sprite the reference has (a plate
+    alone needs none)."""
+    for name in ("streams.npz", "kat.npz", "greedy.npz"):
+        fx = tl.load_fixture(name)
+        masks = {int(m) for m in np.unique(fx["items"][..., 0]) if m != tl.PAD} | \
+                {int(m) for m in np.unique(fx["agents"][..., 2]) if m not in (0, tl.PAD)}
+        for m in masks:
+            if m & ~levels.M_PLATE:
+                assert render.food_sprite_name(m) is not None, hex(m)
+
+
+@pytest.mark.parametrize("level", sorted(levels.BUILTIN_LEVELS))
+def test_static_background_matches_oracle(level):
+    """Host background == the oracle's image wherever no object or agent is drawn."""
+    lv = levels.load_level(level)
+    tabs = render.RenderTables(lv)
+    A, K = 1, capi.item_slots(lv)
+    env = np.zeros(3 * A + 2 * K + 3, np.uint8)
+    env[0], env[1], env[2] = lv.spawns[0][0], lv.spawns[0][1], 0xFF
+    env[3 * A:3 * A + K] = 0xFF  # no items
+    img = render_oracle.render_env(lv, env, A, K, channels="rgb")
+    x, y = lv.spawns[0]
+    mask = np.ones(img.shape[:2], bool)
+    mask[y * 80:(y + 1) * 80, x * 80:(x + 1) * 80] = False
+    assert np.array_equal(img[mask], tabs.background_rgb[mask])
+    assert tabs.background.dtype == np.uint32 and tabs.background.shape == (lv.height * 80, lv.width * 80)
+
+
+def _fixture_states(name, max_per_group=48):
+    """(level, A, K, pitch, state, B) batches built from fixture canonical states, spread over
+    each (level, A) group's steps."""
+    fx = tl.load_fixture(name)
+    for g in tl.episode_groups(fx):
+        offs = []
+        for e in g.idx:
+            o, T = int(fx["ep_state_off"][e]), int(fx["ep_T"][e])
+            offs += list(range(o, o + T + 1))
+        offs = np.array(offs)
+        offs = offs[(fx["flags"][offs] & 0x04) == 0]  # ERR states have no defined objects
+        if len(offs) > max_per_group:
+            offs = offs[np.linspace(0, len(offs) - 1, max_per_group).astype(int)]
+        K = capi.item_slots(g.level)
+        B = len(offs)
+        pitch = capi.pitch_for(B)
+        s = tl.state_from_canonical(g.level, g.A, K, pitch, fx["agents"][offs], fx["items"][offs], fx["t"][offs])
+        yield g.level, g.A, K, pitch, s, B
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fixture", ["greedy.npz", "streams.npz"])
+def test_render_kernel_matches_oracle(fixture):
+    import torch
+    from gym_cooking_amd.engine import OvercookedBatch
+    spr = render.load_sprites()
+    n = 0
+    for lv, A, K, pitch, s, B in _fixture_states(fixture, 24 if fixture == "streams.npz" else 64):
+        eb = OvercookedBatch(lv, A, B, max_T=100)
+        rd = render.Renderer(eb, spr)
+        st = torch.from_numpy(s).to(eb.device)
+        ev = tl.env_view(s, A, K, pitch, B)
+        for channels in ("reference", "rgb"):
+            img = rd.render(st, channels=channels).cpu().numpy()
+            for b in range(B):
+                exp = render_oracle.render_env(lv, ev[:, b], A, K, channels=channels)
+                assert np.array_equal(img[b], exp), (lv.name, A, b, channels, int(np.sum(img[b] != exp)))
+        n += B
+    assert n > 100
+
+
+@pytest.mark.gpu
+def test_render_random_batch_and_errors():
+    """A random-action batch (agents overlapping items at deliveries, 4 agents), and the
+    C-ABI's argument checks."""
+    import torch
+    from gym_cooking_amd.engine import OvercookedBatch
+    eb = OvercookedBatch("open-divider_tl", 4, 300, max_T=100)
+    s, s2 = eb.new_state(), eb.new_state()
+    eb.reset(s)
+    a = eb.new_actions()
+    for t in range(37):
+        eb.gen_actions(a, t, 11)
+        eb.step(s, s2, a)
+        s, s2 = s2, s
+    rd = render.Renderer(eb)
+    img = rd.render(s).cpu().numpy()
+    host = s.cpu().numpy()
+    ev = tl.env_view(host, 4, eb.K, eb.pitch, eb.B)
+    for b in range(0, eb.B, 7):
+        assert np.array_equal(img[b], render_oracle.render_env(eb.level, ev[:, b], 4, eb.K)), b
+    assert not img[..., 2].any()  # the reference's channel mapping leaves channel 2 zero
+    bad = rd.tables.desc_with("rgb")
+    bad.chan_map = 0x00040100
+    with pytest.raises(RuntimeError):
+        capi.check(eb.lib.oc_render(eb._h, render.ctypes.c_void_p(s.data_ptr()),
+                                    render.ctypes.c_void_p(rd.atlas.data_ptr()),
+                                    render.ctypes.c_void_p(rd.background.data_ptr()), render.ctypes.byref(bad),
+                                    render.ctypes.c_void_p(rd.new_images().data_ptr()), eb.B, eb._stream()))
+
+
+@pytest.mark.gpu
+def test_shim_image_obs():
+    """OvercookedEnvironment(with_image_obs=True): info['image_obs'] and game.get_image_obs()
+    are the current state's image (step :290-300)."""
+    import types
+    from gym_cooking_amd.envs import OvercookedEnvironment
+    fx, A = tl.load_fixture("greedy.npz"), 2
+    arg = types.SimpleNamespace(level="open-divider_tl", num_agents=A, max_num_timesteps=100, seed=1, model1=None,
+                                model2=None, model3=None, model4=None, record=False, with_image_obs=True)
+    env = OvercookedEnvironment(arg)
+    env.reset()
+    e = 3  # the greedy open-divider_tl episode: plates, merges and two deliveries
+    lv = env.level
+    for step in range(int(fx["ep_T"][e])):
+        codes = fx["act"][fx["ep_act_off"][e] + step][:A]
+        _, _, _, info = env.step({"agent-%d" % (a + 1): levels.ACTIONS[int(codes[a])] for a in range(A)})
+        if step % 5 == 4 or step == int(fx["ep_T"][e]) - 1:
+            exp = render_oracle.render_env(lv, env.state_bytes(), A, capi.item_slots(lv))
+            assert info["image_obs"].shape == (lv.height * 80, lv.width * 80, 3)
+            assert np.array_equal(info["image_obs"], exp), step
+            assert np.array_equal(env.game.get_image_obs(), exp)
