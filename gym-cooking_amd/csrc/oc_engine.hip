@@ -466,8 +466,8 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
 // Game.on_render / draw_*: game.py:56-186).  One block per (env, cell row): the first W lanes
 // build each cell's ordered draw list in LDS (items not held in slot order, then every agent
 // in order followed by its held item), then the block writes the row's tile*W*tile*3 output
-// bytes, 4 pixels (12 bytes, three dwords) per lane and iteration, consecutive lanes on
-// consecutive pixels.  A pixel starts from the static level image and blends every sprite of
+// bytes, 16 pixels (48 bytes, three 16-byte non-temporal stores) per lane and iteration,
+// consecutive lanes on consecutive pixels.  A pixel starts from the static level image and blends every sprite of
 // its cell's list that covers it.  Everything is tile-local: every sprite lies inside its cell.
 struct RenderArgs {
     int32_t W, H, tile;
@@ -478,6 +478,7 @@ struct RenderArgs {
     uint8_t food_sprite[128];
 };
 constexpr int kRenderMaxW = 32, kRenderMaxDraw = 2 * OC_MAX_ITEMS + 3 * OC_MAX_AGENTS;
+constexpr int kRenderPx = 16;  // pixels per lane and iteration: 48 output bytes, three 16-byte stores
 
 // SDL 1.2 per-pixel alpha blit of an RGBA source pixel onto an RGB destination pixel
 // (BlitNtoNPixelAlpha / ALPHA_BLEND: d = (((s - d) * a + 255) >> 8) + d per channel, a = 0 skipped).
@@ -491,10 +492,6 @@ __device__ __forceinline__ uint32_t sdl_blend(uint32_t d, uint32_t s) {
         out |= (uint32_t)((((sc - dc) * a + 255) >> 8) + dc) << (8 * c);
     }
     return out;
-}
-
-__device__ __forceinline__ uint32_t chan_byte(uint32_t px, uint32_t sel) {
-    return sel >= 3u ? 0u : (px >> (8u * sel)) & 0xFFu;
 }
 
 template <int A, int K>
@@ -548,41 +545,61 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
         dl_n[tx] = n;
     }
     __syncthreads();
-    const int row_px = W * tile, G = row_px / 4;  // 4-pixel groups per image row
+    const int row_px = W * tile, G = row_px / kRenderPx;  // 16-pixel groups per image row
     const int items = tile * G;
     const int64_t img_bytes = (int64_t)R.H * tile * row_px * 3;
     uint8_t* img = out + e * img_bytes;
+    // chan_map -> v_perm selector: output byte c <- pixel byte (chan_map >> 8c), 0x0C = zero
+    uint32_t psel = 0x0C000000u;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const uint32_t ch = (R.chan_map >> (8 * c)) & 0xFFu;
+        psel |= (ch >= 3u ? 0x0Cu : ch) << (8 * c);
+    }
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     for (int i = threadIdx.x; i < items; i += kBlock) {
         const int r = i / G, g = i - r * G;
-        const int py = ty * tile + r, px0 = 4 * g;
-        const uint4 b4 = *(const uint4*)(bg + (int64_t)py * row_px + px0);
-        uint32_t p[4] = {b4.x, b4.y, b4.z, b4.w};
-        const int tx = px0 / tile, lx0 = px0 - tx * tile;
+        const int py = ty * tile + r, px0 = kRenderPx * g;
+        const u32x4* bsrc = (const u32x4*)(bg + (int64_t)py * row_px + px0);
+        uint32_t p[kRenderPx];
+#pragma unroll
+        for (int q = 0; q < kRenderPx / 4; ++q) {
+            const u32x4 v = bsrc[q];
+            p[4 * q] = v.x;
+            p[4 * q + 1] = v.y;
+            p[4 * q + 2] = v.z;
+            p[4 * q + 3] = v.w;
+        }
+        const int tx = px0 / tile, lx0 = px0 - tx * tile;  // a group never straddles two cells
         const int n = dl_n[tx];
         for (int d = 0; d < n; ++d) {
             const uint32_t geo = dl_geo[tx][d];
             const int sz = (int)(geo & 0xFFFFu), o = (int)(geo >> 16);
             const int dy = r - o;
-            if ((unsigned)dy >= (unsigned)sz) continue;
+            if ((unsigned)dy >= (unsigned)sz || lx0 + kRenderPx <= o || lx0 >= o + sz) continue;
             const uint32_t* spr = atlas + dl_off[tx][d] + dy * sz;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < kRenderPx; ++k) {
                 const int dx = lx0 + k - o;
                 if ((unsigned)dx < (unsigned)sz) p[k] = sdl_blend(p[k], spr[dx]);
             }
         }
-        const uint32_t c0 = R.chan_map & 0xFFu, c1 = (R.chan_map >> 8) & 0xFFu, c2 = (R.chan_map >> 16) & 0xFFu;
-        uint32_t bytes[12];
+        // 16 pixels -> 48 bytes: per 4 pixels three dwords of packed 3-byte pixels
+        u32x4* dst = (u32x4*)(img + ((int64_t)py * row_px + px0) * 3);
+        uint32_t w[12];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            bytes[3 * k] = chan_byte(p[k], c0);
-            bytes[3 * k + 1] = chan_byte(p[k], c1);
-            bytes[3 * k + 2] = chan_byte(p[k], c2);
+        for (int q = 0; q < kRenderPx / 4; ++q) {
+            const uint32_t a0 = __builtin_amdgcn_perm(0u, p[4 * q], psel), a1 = __builtin_amdgcn_perm(0u, p[4 * q + 1], psel),
+                           a2 = __builtin_amdgcn_perm(0u, p[4 * q + 2], psel), a3 = __builtin_amdgcn_perm(0u, p[4 * q + 3], psel);
+            w[3 * q] = a0 | (a1 << 24);
+            w[3 * q + 1] = (a1 >> 8) | (a2 << 16);
+            w[3 * q + 2] = (a2 >> 16) | (a3 << 8);
         }
-        uint32_t* dst = (uint32_t*)(img + ((int64_t)py * row_px + px0) * 3);
 #pragma unroll
-        for (int w = 0; w < 3; ++w)
-            dst[w] = bytes[4 * w] | (bytes[4 * w + 1] << 8) | (bytes[4 * w + 2] << 16) | (bytes[4 * w + 3] << 24);
+        for (int q = 0; q < 3; ++q) {
+            const u32x4 v = {w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+            __builtin_nontemporal_store(v, dst + q);  // streamed once: keep L2 for the level image and sprites
+        }
     }
 }
 
@@ -1021,7 +1038,8 @@ int oc_render(const oc_handle* h, const void* state, const uint32_t* atlas, cons
         return fail(OC_EINVAL, "bad argument");
     const int W = h->level.width, H = h->level.height;
     if (W > kRenderMaxW) return fail(OC_ELEVEL, "render: width %d > %d", W, kRenderMaxW);
-    if (desc->tile < 4 || desc->tile % 4 != 0 || desc->tile > 1024) return fail(OC_EINVAL, "render: tile %d", desc->tile);
+    if (desc->tile < kRenderPx || desc->tile % kRenderPx != 0 || desc->tile > 1024)
+        return fail(OC_EINVAL, "render: tile %d (a multiple of %d)", desc->tile, kRenderPx);
     for (int c = 0; c < OC_RENDER_SIZES; ++c)
         if (desc->size[c] < 0 || desc->offset[c] < 0 || desc->size[c] + desc->offset[c] > desc->tile)
             return fail(OC_EINVAL, "render: size class %d (%d at %d) leaves the %d-px cell", c, desc->size[c],

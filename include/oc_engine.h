@@ -281,7 +281,7 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
 #define OC_CHAN_REFERENCE 0x00030100u
 
 typedef struct {
-    int32_t tile;                         /* pixels per cell (Game.scale, 80) */
+    int32_t tile;                         /* pixels per cell (Game.scale, 80; a multiple of 16) */
     int32_t size[OC_RENDER_SIZES];        /* sprite edge per size class: 80, 56, 40, 28 */
     int32_t offset[OC_RENDER_SIZES];      /* sprite origin inside its cell: 0, 12, 40, 46 */
     int32_t food_base[OC_RENDER_SIZES];   /* atlas pixel offset of food sprite 0 of each size class;
