@@ -118,7 +118,9 @@ def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 20) -> dict:
     nbytes = 55 * rows
     legal = int((flags[:rows] & capi.ROLL_LEGAL).ne(0).sum())
     lik = measure_likelihood(eb, s, a, table, alloc, dev, world)
+    bnd = measure_bounds(eb, s, table, dev, world)
     return {"value": world * rows / (ms * 1e-3), "unit": "rollout rows/s", "rows_per_gpu": rows, "likelihood": lik,
+            "subtask_bounds": bnd,
             "ms_per_launch": ms, "kernel": "oc_rollout_kernel<4,4>",
             "workload": "C5: full-divider_salad 4 agents, %d Salad (subtask, agents) configs, random joint actions"
                         % len(table),
@@ -144,6 +146,29 @@ def measure_likelihood(eb, states, taken, table, alloc, dev, world, reps: int = 
     return {"value": world * eb.B / (ms * 1e-3), "unit": "likelihood rows/s", "ms_per_launch": ms,
             "kernel": "oc_likelihood_kernel<4,4>", "rows_computed": ok, "bound": "compute (fp64 softmax over "
             "up to 25 candidate rollouts per row)"}
+
+
+def measure_bounds(eb, states, table, dev, world, reps: int = 10) -> dict:
+    """C5's prior setup: full-state subtask bounds + allocation feasibility (oc_subtask_bounds,
+    get_lower_bound_for_subtask_given_objs / subtask_alloc_is_doable) of every env x every
+    configuration of the table.  Algorithmic bytes per env: S(4) = 23 state bytes read + 5 B
+    (f32 bound, u8 doable) written per configuration."""
+    for _ in range(2):
+        lb, ok = eb.subtask_bounds(states, table)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        eb.subtask_bounds(states, table, lb, ok)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
+    cells = eb.B * len(table)
+    nbytes = eb.B * (23 + 5 * len(table))
+    return {"value": world * cells / (ms * 1e-3), "unit": "(env, configuration) bounds/s", "ms_per_launch": ms,
+            "kernel": "oc_bounds_kernel<4,4>", "envs": eb.B, "configurations": len(table),
+            "doable": int(ok[:, :eb.B].sum()), "achieved_GBs": nbytes / (ms * 1e-3) / 1e9,
+            "bound": "compute (LDS distance-table walk per configuration)"}
 
 
 def measure_render(dev, world, level: str, A: int, B: int = 1024, reps: int = 10) -> dict:

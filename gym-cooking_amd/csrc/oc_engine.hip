@@ -15,6 +15,7 @@
 //   oc_step_n_kernel  n steps per launch with the state in registers; every step's state,
 //                     executed actions and collision mask are still written.
 //   oc_rollout_kernel navigation-planner rollout rows (oc_rollout.h).
+//   oc_bounds_kernel  full-state subtask lower bounds + allocation feasibility (oc_subtask_bounds).
 //   oc_render_kernel  image observations.
 //   reset / gen_actions / checksum / stats_reduce helpers.
 // All of them accumulate nothing on the host; statistics are per-block rows of no-return
@@ -462,6 +463,31 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
     }
 }
 
+// Full-state subtask bounds (oc_subtask_bounds): one env per lane, every subtask configuration
+// of the call in turn (configurations and tables in LDS).  Output [subtask][pitch], so each
+// store instruction of a wave covers 64 consecutive envs of one configuration.
+template <int A, int K>
+__global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uint8_t* __restrict__ sin,
+                                                           const uint8_t* __restrict__ dist_g,
+                                                           float* __restrict__ lb, uint8_t* __restrict__ doable) {
+    __shared__ uint32_t dist_w[ocro::kMaxNodes * ocro::kMaxNodes / 4];
+    __shared__ ocro::RollLevel Ls;
+    __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
+    stage_roll_tables(R, dist_g, dist_w, Ls, subs);
+    const uint8_t* dist = (const uint8_t*)dist_w;
+    const int64_t P = R.pitch;
+    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
+        const ocro::Row r = load_row<A, K>(sin, P, e);
+        ocro::RowOps<A, K> ops(Ls, dist);
+        for (int i = 0; i < R.nsub; ++i) {
+            float v;
+            const bool ok = ops.full_bound(r, subs[i], v);
+            lb[i * P + e] = v;
+            doable[i * P + e] = ok ? 1 : 0;
+        }
+    }
+}
+
 // Image observation (oc_render, GameImage.get_image_obs: gym_cooking/misc/game/gameimage.py:31-51,
 // Game.on_render / draw_*: game.py:56-186).  One block per (env, cell row): the first W lanes
 // build each cell's ordered draw list in LDS (items not held in slot order, then every agent
@@ -740,6 +766,7 @@ struct oc_handle {
     LevelArgs args;
     ocro::RollLevel roll;       // planner rollout tables (nnodes < 0: graph too large)
     uint8_t* roll_dist = nullptr;  // device: reachability distances [kMaxNodes][kMaxNodes]
+    uint8_t roll_dist_host[ocro::kMaxNodes * ocro::kMaxNodes];  // the same table on the host
 };
 
 // Statistics rows: one per block of the larger of the oc_step / oc_step_n grids.
@@ -830,20 +857,38 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     h->args = L;
     // planner rollout: the static reachability graph's BFS table (world.py:67-108)
     {
-        static uint8_t dist[ocro::kMaxNodes * ocro::kMaxNodes];
+        uint8_t* dist = h->roll_dist_host;
         const int n = ocro::build_roll_level(h->roll, dist, W, H, lv->tiles);
         if (n < 0) {
             h->roll.nnodes = -1;
         } else {
             if (hipSetDevice(device) != hipSuccess ||
-                hipMalloc(&h->roll_dist, sizeof(dist)) != hipSuccess ||
-                hipMemcpy(h->roll_dist, dist, sizeof(dist), hipMemcpyHostToDevice) != hipSuccess) {
+                hipMalloc(&h->roll_dist, sizeof(h->roll_dist_host)) != hipSuccess ||
+                hipMemcpy(h->roll_dist, dist, sizeof(h->roll_dist_host), hipMemcpyHostToDevice) != hipSuccess) {
                 h->roll_dist = nullptr;  // no device (e.g. a CPU-only build check): rollout unavailable
                 (void)hipGetLastError();
             }
         }
     }
     *out = h;
+    return OC_OK;
+}
+
+int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint8_t* node_of, int64_t node_of_len, uint8_t* dist,
+                    int64_t dist_len) {
+    if (h == nullptr || num_nodes == nullptr) return fail(OC_EINVAL, "bad argument");
+    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes", ocro::kMaxNodes);
+    const int n = h->roll.nnodes, cells = h->level.width * h->level.height;
+    *num_nodes = n;
+    if (node_of != nullptr) {
+        if (node_of_len < (int64_t)cells * 5) return fail(OC_EINVAL, "node_of needs %d bytes", cells * 5);
+        for (int i = 0; i < cells * 5; ++i) node_of[i] = h->roll.node[i];
+    }
+    if (dist != nullptr) {
+        if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %d bytes", n * n);
+        for (int u = 0; u < n; ++u)
+            for (int v = 0; v < n; ++v) dist[u * n + v] = h->roll_dist_host[u * ocro::kMaxNodes + v];
+    }
     return OC_OK;
 }
 
@@ -1029,6 +1074,25 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
                        alloc, h->roll_dist, self_agent, beta, none_action_prob, likelihood, out_flags)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_LIK)
     return hip_check("oc_nav_likelihood launch");
+}
+
+int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* subtasks, int32_t num_subtasks,
+                      float* lower_bound, uint8_t* doable, int64_t B, void* stream) {
+    if (h == nullptr || state == nullptr || subtasks == nullptr || lower_bound == nullptr || doable == nullptr ||
+        B < 0)
+        return fail(OC_EINVAL, "bad argument");
+    if (((uintptr_t)lower_bound & 3u) || ((uintptr_t)state & 1u)) return fail(OC_EINVAL, "misaligned buffer");
+    RollArgs R;
+    if (const int rc = roll_args(h, subtasks, num_subtasks, B, R)) return rc;
+    if (B == 0) return OC_OK;
+    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)kCUs * 8;
+    const dim3 grid((unsigned)(need < cap ? need : cap));
+    hipStream_t st = (hipStream_t)stream;
+#define OC_LAUNCH_BOUNDS(A, K)                                                                             \
+    hipLaunchKernelGGL((oc_bounds_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state,     \
+                       h->roll_dist, lower_bound, doable)
+    OC_DISPATCH(h->A, h->K, OC_LAUNCH_BOUNDS)
+    return hip_check("oc_subtask_bounds launch");
 }
 
 int oc_render(const oc_handle* h, const void* state, const uint32_t* atlas, const uint32_t* background,

@@ -353,7 +353,15 @@ struct RowOps {
 
     // get_lower_bound_for_subtask_given_objs (overcooked_environment.py:594-664)
     OC_RH float lower_bound(const Row& r, const Sub& s) const {
-        float pen = 0.0f;
+        float pen;
+        const float d = lower_bound_parts(r, s, pen);
+        return d + pen;
+    }
+
+    // The same, split: returns World.get_lower_bound_between's distance (world.py:115-146) and
+    // sets `pen` to the holding penalty (overcooked_environment.py:611-640).
+    OC_RH float lower_bound_parts(const Row& r, const Sub& s, float& pen) const {
+        pen = 0.0f;
         int ag0 = 0, ag1 = 0, na = 0;
 #pragma unroll
         for (int a = 0; a < A; ++a) {
@@ -380,7 +388,20 @@ struct RowOps {
                 });
             });
         }
-        return lower + pen;
+        return lower;
+    }
+
+    // oc_subtask_bounds on a full state (no Level-0 view): lb = get_lower_bound_for_subtask_
+    // given_objs; returns BayesianDelegator.subtask_alloc_is_doable (bayesian_delegator.py:98-156):
+    // None -> true, else the distance < world.perimeter.
+    OC_RH bool full_bound(const Row& r, const Sub& s, float& lb) {
+        ac = 0;
+        active = 1u << s.agent[0];
+        if (s.n == 2) active |= 1u << s.agent[1];
+        float pen;
+        const float d = lower_bound_parts(r, s, pen);
+        lb = d + pen;
+        return s.kind == 0 || d < (float)L.perimeter;
     }
 
     // The whole row: returns OC_ROLL_* flags; r becomes the Level-0 next state (unchanged when

@@ -11,6 +11,7 @@ from __future__ import annotations
 import ctypes
 from typing import Dict, Optional
 
+import numpy as np
 import torch
 
 from . import capi
@@ -169,6 +170,36 @@ class OvercookedBatch:
                                               capi.subtask_array(subtasks), len(subtasks), self_agent, beta,
                                               none_action_prob, _ptr(out), _ptr(flags), self.B, self._stream()))
         return out, flags
+
+    def subtask_bounds(self, state: torch.Tensor, subtasks, lower_bound: Optional[torch.Tensor] = None,
+                       doable: Optional[torch.Tensor] = None):
+        """Full-state subtask bounds (oc_subtask_bounds): for every env and configuration,
+        get_lower_bound_for_subtask_given_objs and subtask_alloc_is_doable; returns
+        (lower bound f32 [S][pitch], doable u8 [S][pitch])."""
+        S = len(subtasks)
+        self._check(state, self.layout.state_bytes)
+        if lower_bound is None:
+            lower_bound = torch.empty((S, self.pitch), dtype=torch.float32, device=self.device)
+        if doable is None:
+            doable = torch.empty((S, self.pitch), dtype=torch.uint8, device=self.device)
+        self._check(lower_bound, 4 * S * self.pitch)
+        self._check(doable, S * self.pitch)
+        capi.check(self.lib.oc_subtask_bounds(self._h, _ptr(state), capi.subtask_array(subtasks), S,
+                                              _ptr(lower_bound), _ptr(doable), self.B, self._stream()))
+        return lower_bound, doable
+
+    def reachability(self):
+        """The level's static reachability graph (oc_reachability): (node_of u8 [W*H*5] with
+        0xFF = not a node, dist u8 [n][n] with 0xFF = no path)."""
+        import ctypes
+        n = ctypes.c_int32()
+        capi.check(self.lib.oc_reachability(self._h, ctypes.byref(n), None, 0, None, 0))
+        cells = self.level.width * self.level.height
+        node_of = np.zeros(cells * 5, np.uint8)
+        dist = np.zeros((n.value, n.value), np.uint8)
+        capi.check(self.lib.oc_reachability(self._h, ctypes.byref(n), node_of.ctypes.data, node_of.size,
+                                            dist.ctypes.data, dist.size))
+        return node_of, dist
 
     def gen_actions(self, actions: torch.Tensor, step: int, seed: int = 0, env_offset: int = 0) -> torch.Tensor:
         self._check(actions, self.A * self.pitch)

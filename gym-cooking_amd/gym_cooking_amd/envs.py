@@ -147,12 +147,97 @@ class SimAgentView:
         return "None" if self.holding is None else self.holding.full_name
 
 
+class NoPath(Exception):
+    """No path between two reachability-graph nodes (networkx raises NetworkXNoPath)."""
+
+
+class ReachabilityGraph:
+    """``World.reachability_graph`` (utils/world.py:67-108) as oc_create builds it: nodes are
+    ``(location, approach)``, approach ``(0, 0)`` for a Floor square or the NAV_ACTION from
+    which a collidable square is reached; ``shortest_path_length`` reads the all-pairs BFS
+    table the kernels use (oc_reachability).  ``to_networkx()`` gives the reference's
+    ``nx.Graph`` when networkx is importable."""
+
+    _APPROACH = NAV_ACTIONS + [(0, 0)]
+
+    def __init__(self, width: int, node_of: np.ndarray, dist: np.ndarray):
+        self.width = width
+        self._id: Dict[tuple, int] = {}
+        for key, n in enumerate(node_of.tolist()):
+            if n != 0xFF:
+                c, d = divmod(key, 5)
+                self._id[((c % width, c // width), self._APPROACH[d])] = n
+        self._dist = dist
+
+    def nodes(self) -> list:
+        return sorted(self._id, key=self._id.get)
+
+    def edges(self) -> list:
+        nodes = self.nodes()
+        return [(u, v) for i, u in enumerate(nodes) for v in nodes[i + 1:] if self._dist[i, nodes.index(v)] == 1]
+
+    def __contains__(self, node) -> bool:
+        return self._key(node) in self._id
+
+    def __len__(self) -> int:
+        return len(self._id)
+
+    @staticmethod
+    def _key(node):
+        (x, y), a = node
+        return (int(x), int(y)), (int(a[0]), int(a[1]))
+
+    def shortest_path_length(self, source, target) -> int:
+        """nx.shortest_path_length(reachability_graph, source, target); raises NoPath."""
+        u, v = self._id.get(self._key(source)), self._id.get(self._key(target))
+        if u is None or v is None or self._dist[u, v] == 0xFF:
+            raise NoPath("no path between %r and %r" % (source, target))
+        return int(self._dist[u, v])
+
+    def to_networkx(self):
+        import networkx as nx
+        g = nx.Graph()
+        g.add_nodes_from(self.nodes())
+        g.add_edges_from(self.edges())
+        return g
+
+
+def get_subtask_obj(subtask):
+    """nav_utils.get_subtask_obj (navigation_planner/utils.py:181-246): (start, goal) objects of
+    a subtask (a list of two for Merge; (None, None) for None), compared by contents like the
+    reference's Objects."""
+    kind, (sa, sb), goal = _recipes.subtask_masks(subtask)
+    if kind == 0:
+        return None, None
+    obj = lambda m: ItemView(-1, m, None, False)  # noqa: E731
+    start = [obj(sa), obj(sb)] if kind == 2 else obj(sa)
+    return start, obj(goal)
+
+
+def get_subtask_action_obj(subtask):
+    """nav_utils.get_subtask_action_obj (navigation_planner/utils.py:154-177): the static
+    square a subtask acts on (Cutboard for Chop, Delivery for Deliver, else None)."""
+    if subtask is None:
+        return None
+    if subtask.name not in ("Chop", "Merge", "Deliver"):
+        raise ValueError("Did not recognize subtask {} so could not find the appropriate subtask location"
+                         .format(subtask))
+    name = {"Chop": "Cutboard", "Deliver": "Delivery"}.get(subtask.name)
+    return GridSquareView(name, None, None) if name else None
+
+
+def _is_merge(subtask) -> bool:
+    return subtask is not None and subtask.name == "Merge"
+
+
 class WorldView:
     """The reference ``World`` queries (utils/world.py:285-436) over one env's state."""
 
     NAV_ACTIONS = NAV_ACTIONS
 
-    def __init__(self, level: _levels.Level, items: Sequence[ItemView], group_names: Sequence[str] = ()):
+    def __init__(self, level: _levels.Level, items: Sequence[ItemView], group_names: Sequence[str] = (),
+                 reachability_graph: Optional[ReachabilityGraph] = None):
+        self.reachability_graph = reachability_graph
         self.level = level
         self.width, self.height = level.width, level.height
         self.perimeter = 2 * (self.width + self.height)  # overcooked_environment.py:198
@@ -227,6 +312,56 @@ class WorldView:
         x, y = location
         return min(max(x, 0), self.width - 1), min(max(y, 0), self.height - 1)
 
+    def get_lower_bound_between(self, subtask, agent_locs, A_locs, B_locs):  # world.py:115-146
+        lower_bound = self.perimeter + 1
+        for A_loc in A_locs:
+            for B_loc in B_locs:
+                bound = self.get_lower_bound_between_helper(subtask, tuple(agent_locs), tuple(A_loc), tuple(B_loc))
+                if bound < lower_bound:
+                    lower_bound = bound
+        return lower_bound
+
+    def get_lower_bound_between_helper(self, subtask, agent_locs, A_loc, B_loc):  # world.py:148-264
+        g = self.reachability_graph
+        if g is None:
+            raise RuntimeError("this world view has no reachability graph")
+        spl = g.shortest_path_length
+        lower_bound = self.perimeter + 1
+        A_na = [(0, 0)] if not self.get_gridsquare_at(A_loc).collidable else NAV_ACTIONS
+        B_na = [(0, 0)] if not self.get_gridsquare_at(B_loc).collidable else NAV_ACTIONS
+
+        def dist(u, v, default):
+            try:
+                return spl(u, v)
+            except NoPath:
+                return default
+
+        for a_na in A_na:
+            for b_na in B_na:
+                if len(agent_locs) == 1:
+                    try:
+                        b1 = spl((agent_locs[0], (0, 0)), (A_loc, a_na))
+                        b2 = spl((A_loc, a_na), (B_loc, b_na))
+                    except NoPath:
+                        continue
+                    bound = b1 + b2 - 1
+                else:
+                    b1A = dist((agent_locs[0], (0, 0)), (A_loc, a_na), self.perimeter)
+                    b2A = dist((agent_locs[1], (0, 0)), (A_loc, a_na), self.perimeter)
+                    b1B = dist((agent_locs[0], (0, 0)), (B_loc, b_na), self.perimeter)
+                    b2B = dist((agent_locs[1], (0, 0)), (B_loc, b_na), self.perimeter)
+                    mA, mB = min(b1A, b2A), min(b1B, b2B)
+                    man = float(abs(A_loc[0] - B_loc[0]) + abs(A_loc[1] - B_loc[1]))  # manhattan_dist
+                    if _is_merge(subtask):
+                        if (b1A == mA and b1B == mB) or (b2A == mA and b2B == mB):  # check_bound :266-283
+                            mA, mB = 2 * mA, 2 * mB
+                        bound = max(mA, mB) + (man - 1) / 2
+                    else:
+                        bound = mA + man - 1
+                if bound < lower_bound:
+                    lower_bound = bound
+        return max(1, lower_bound)
+
 
 def is_collision(world, agent1_loc, agent2_loc, agent1_action, agent2_action):
     """OvercookedEnvironment.is_collision (overcooked_environment.py:671-722): [execute1,
@@ -251,7 +386,8 @@ def is_collision(world, agent1_loc, agent2_loc, agent1_action, agent2_action):
     return execute
 
 
-def build_views(level: _levels.Level, A: int, K: int, env_bytes: np.ndarray, actions=None, group_names=()):
+def build_views(level: _levels.Level, A: int, K: int, env_bytes: np.ndarray, actions=None, group_names=(),
+                reachability_graph: Optional[ReachabilityGraph] = None):
     """(sim_agents, world, t, flags) of one env from its canonical state bytes
     (oc_testlib.env_view order: ax[A] ay[A] ah[A] loc[K] mask[K] t_lo t_hi flags);
     `group_names`: object names whose (possibly empty) groups the world keeps."""
@@ -270,7 +406,7 @@ def build_views(level: _levels.Level, A: int, K: int, env_bytes: np.ndarray, act
     for a in range(A):
         act = None if actions is None else actions[a]
         agents.append(SimAgentView("agent-%d" % (a + 1), COLORS[a], (ax[a], ay[a]), items.get(ah[a]), act))
-    return agents, WorldView(level, list(items.values()), group_names), t, flags
+    return agents, WorldView(level, list(items.values()), group_names, reachability_graph), t, flags
 
 
 # ---------------------------------------------------------------------------------------
@@ -319,7 +455,7 @@ class OvercookedEnvironment:
     def _refresh(self, actions=None):
         eng = self._engine
         self.sim_agents, self.world, self.t, self._flags = build_views(self.level, eng.A, eng.K, self._host, actions,
-                                                                       sorted(self._group_names))
+                                                                       sorted(self._group_names), eng.reach)
         self._group_names = self._group_names | {it.name for it in self.world.items}
 
     # -- gym API ----------------------------------------------------------------------------
@@ -438,6 +574,53 @@ class OvercookedEnvironment:
     def is_collision(self, agent1_loc, agent2_loc, agent1_action, agent2_action):  # :671-722
         return is_collision(self.world, agent1_loc, agent2_loc, agent1_action, agent2_action)
 
+    def get_AB_locs_given_objs(self, subtask, subtask_agent_names, start_obj, goal_obj, subtask_action_obj):
+        """overcooked_environment.py:480-589: (A_locs, B_locs) of a subtask -- un-held start
+        objects plus the subtask agents holding one; Cutboard / Delivery squares for Chop /
+        Deliver (Deliver drops A locations already on a Delivery)."""
+        w = self.world
+
+        def held_by_subtask_agents(obj):
+            return [a.location for a in self.sim_agents if a.name in subtask_agent_names and a.holding == obj]
+
+        name = None if subtask is None else subtask.name
+        if name == "Chop":
+            return (w.get_object_locs(start_obj, is_held=False) + held_by_subtask_agents(start_obj),
+                    w.get_all_object_locs(subtask_action_obj))
+        if name == "Deliver":
+            B_locs = w.get_all_object_locs(subtask_action_obj)
+            A_locs = w.get_object_locs(start_obj, is_held=False) + held_by_subtask_agents(start_obj)
+            return [a for a in A_locs if a not in B_locs], B_locs
+        if name == "Merge":
+            return (w.get_object_locs(start_obj[0], is_held=False) + held_by_subtask_agents(start_obj[0]),
+                    w.get_object_locs(start_obj[1], is_held=False) + held_by_subtask_agents(start_obj[1]))
+        return [], []
+
+    def get_lower_bound_for_subtask_given_objs(self, subtask, subtask_agent_names, start_obj=None, goal_obj=None,
+                                               subtask_action_obj=None):
+        """overcooked_environment.py:594-664, evaluated by the oc_subtask_bounds kernel on this
+        env's state.  The objects are the ones get_subtask_obj / get_subtask_action_obj give for
+        `subtask` (the only ones the reference passes); they are implied by it."""
+        assert len(subtask_agent_names) <= 2, 'passed in {} agents but can only do 1 or 2'.format(
+            len(subtask_agent_names))
+        lb, _ = self._subtask_bound(subtask, subtask_agent_names)
+        return lb
+
+    def subtask_alloc_is_doable(self, subtask, subtask_agent_names) -> bool:
+        """BayesianDelegator.subtask_alloc_is_doable(env, ...) (bayesian_delegator.py:98-156),
+        evaluated by the oc_subtask_bounds kernel on this env's state."""
+        if subtask is None:
+            return True
+        _, ok = self._subtask_bound(subtask, subtask_agent_names)
+        return ok
+
+    def _subtask_bound(self, subtask, subtask_agent_names):
+        names = self.get_agent_names()
+        agents = sorted(names.index(n) for n in subtask_agent_names)
+        kind, starts, goal = _recipes.subtask_masks(subtask)
+        lb, ok = self._engine.bounds(self._host, [capi.subtask(kind, agents, list(starts), goal, 0)])
+        return float(lb[0]), bool(ok[0])
+
     def state_bytes(self) -> np.ndarray:
         """The env's state bytes (ax[A] ay[A] ah[A] loc[K] mask[K] t_lo t_hi flags)."""
         return self._host.copy()
@@ -481,6 +664,8 @@ class _Single:
         self.s_in, self.s_out = batch.new_state(), batch.new_state()
         self.act, self.ex, self.coll = batch.new_actions(), batch.new_exec(), batch.new_coll()
         self._t = batch.layout.plane_t
+        node_of, dist = batch.reachability()
+        self.reach = ReachabilityGraph(batch.level.width, node_of, dist)
 
     def _download(self, buf) -> np.ndarray:
         host = buf.view(self.NP, self.P)[:, :2].cpu().numpy()  # env 0 of every plane (+ t's high byte)
@@ -498,6 +683,12 @@ class _Single:
     def reset(self) -> np.ndarray:
         self.b.reset(self.s_in)
         return self._download(self.s_in)
+
+    def bounds(self, env_bytes: np.ndarray, subtasks):
+        """oc_subtask_bounds of this env: (lb f32 [S], doable u8 [S])."""
+        self._upload(env_bytes, self.s_in)
+        lb, ok = self.b.subtask_bounds(self.s_in, subtasks)
+        return lb[:, 0].cpu().numpy(), ok[:, 0].cpu().numpy()
 
     def step(self, env_bytes: np.ndarray, codes: Sequence[int]):
         cur = env_bytes.copy()

@@ -264,6 +264,38 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
                       const oc_subtask* subtasks, int32_t num_subtasks, int32_t self_agent, double beta,
                       double none_action_prob, double* likelihood, uint8_t* out_flags, int64_t B, void* stream);
 
+/* The level's static reachability graph, World.make_reachability_graph (utils/world.py:67-108),
+ * as built by oc_create: nodes are (cell, approach) with approach 0..3 = World.NAV_ACTIONS (the
+ * side a collidable square is reached from) and 4 = (0, 0) (a Floor square).  Host data; works
+ * without a device.
+ *   num_nodes : out, n
+ *   node_of   : nullable u8 [W*H*5]: node id of (cell, approach), 0xFF = not a node
+ *   dist      : nullable u8 [n][n]: nx.shortest_path_length between nodes, 0xFF = no path
+ * World.get_lower_bound_between(_helper) (world.py:115-283) evaluates over exactly this table. */
+int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint8_t* node_of, int64_t node_of_len, uint8_t* dist,
+                    int64_t dist_len);
+
+/* ---------------------------------------------------------------------------------------
+ * Subtask bounds on full environment states (no planner Level-0 view): for every env e and
+ * every configuration i of the call,
+ *   lower_bound[i][e] = env.get_lower_bound_for_subtask_given_objs(subtask, agents, start_obj,
+ *                        goal_obj, subtask_action_obj)
+ *                       gym_cooking/envs/overcooked_environment.py:594-664, with
+ *                       get_AB_locs_given_objs :480-589 and World.get_lower_bound_between(_helper)
+ *                       utils/world.py:115-283 (None: perimeter + 1 + holding penalty)
+ *   doable[i][e]      = BayesianDelegator.subtask_alloc_is_doable(env, subtask, agents)
+ *                       delegation_planner/bayesian_delegator.py:98-156 (None: 1; else the
+ *                       get_lower_bound_between distance < world.perimeter), the feasibility
+ *                       test of prune_subtask_allocs (:200-260)
+ * Replaces the per-(state, allocation) Python calls of the delegation planner's prior setup
+ * (set_priors -> prune_subtask_allocs) and of a drop-in env's planner queries.
+ *   state       : B states (oc_layout)
+ *   subtasks    : host array of num_subtasks (<= OC_MAX_SUBTASKS); goal_count is ignored
+ *   lower_bound : f32 [num_subtasks][pitch];  doable : u8 [num_subtasks][pitch]
+ * ------------------------------------------------------------------------------------- */
+int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* subtasks, int32_t num_subtasks,
+                      float* lower_bound, uint8_t* doable, int64_t B, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Image observation: what GameImage.get_image_obs returns after on_render
  *   gym_cooking/misc/game/gameimage.py:31-51, game.py:56-186

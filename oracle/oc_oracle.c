@@ -739,8 +739,9 @@ static double lb_helper(const Env* e, const Reach* R, const oc_subtask* s, const
 }
 
 /* get_lower_bound_for_subtask_given_objs (overcooked_environment.py:594-664) with
- * get_AB_locs_given_objs (:480-589) and World.get_lower_bound_between (world.py:115-146) */
-static double lower_bound(const Env* e, const Reach* R, const oc_subtask* s) {
+ * get_AB_locs_given_objs (:480-589) and World.get_lower_bound_between (world.py:115-146):
+ * returns the get_lower_bound_between distance; *pen_out gets the holding penalty */
+static double lower_bound_parts(const Env* e, const Reach* R, const oc_subtask* s, double* pen_out) {
     double penalty = 0.0;
     Loc agent_locs[2];
     int na = 0;
@@ -797,7 +798,14 @@ static double lower_bound(const Env* e, const Reach* R, const oc_subtask* s) {
             const double b = lb_helper(e, R, s, agent_locs, Al[i], Bl[j]);
             if (b < lower) lower = b;
         }
-    return lower + penalty;
+    *pen_out = penalty;
+    return lower;
+}
+
+static double lower_bound(const Env* e, const Reach* R, const oc_subtask* s) {
+    double pen;
+    const double d = lower_bound_parts(e, R, s, &pen);
+    return d + pen;
 }
 
 typedef struct {
@@ -992,6 +1000,70 @@ int oco_nav_likelihood(const oc_level_desc* L, int A, int K, const uint8_t* sin,
         j->b0 = B * t / nthreads;
         j->b1 = B * (t + 1) / nthreads;
         pthread_create(&th[t], NULL, run_lik, j);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    free(R);
+    return 0;
+}
+
+/* =========================================================================================
+ * Subtask bounds on full states (no Level-0 view): for env e and subtask configuration i,
+ *   lb[i*pitch + e]     = get_lower_bound_for_subtask_given_objs (overcooked_environment.py:594-664)
+ *   doable[i*pitch + e] = BayesianDelegator.subtask_alloc_is_doable (bayesian_delegator.py:98-156):
+ *                         None -> 1, else get_lower_bound_between < world.perimeter
+ * ========================================================================================= */
+typedef struct {
+    Cfg c;
+    const Reach* R;
+    const uint8_t* sin;
+    const oc_subtask* subs;
+    int nsub;
+    float* lb;
+    uint8_t* doable;
+    int64_t b0, b1;
+} BoundJob;
+
+static void* run_bounds(void* p) {
+    BoundJob* j = (BoundJob*)p;
+    const int64_t P = j->c.pitch;
+    const double perimeter = 2.0 * (j->c.L->width + j->c.L->height);
+    for (int64_t e = j->b0; e < j->b1; ++e) {
+        Env env;
+        int fl;
+        unpack(&j->c, j->sin, e, &env, &fl);
+        for (int i = 0; i < j->nsub; ++i) {
+            const oc_subtask* s = &j->subs[i];
+            double pen;
+            const double d = lower_bound_parts(&env, j->R, s, &pen);
+            j->lb[i * P + e] = (float)(d + pen);
+            j->doable[i * P + e] = (uint8_t)(s->kind == OC_SUB_NONE || d < perimeter);
+        }
+    }
+    return NULL;
+}
+
+int oco_subtask_bounds(const oc_level_desc* L, int A, int K, const uint8_t* sin, const oc_subtask* subs, int nsub,
+                       float* lb, uint8_t* doable, int64_t B, int64_t pitch, int nthreads) {
+    if (nsub < 1) return -1;
+    for (int i = 0; i < nsub; ++i) {
+        if (subs[i].num_agents < 1 || subs[i].num_agents > 2) return -1;
+        for (int q = 0; q < subs[i].num_agents; ++q)
+            if (subs[i].agent[q] >= A) return -1;
+        if (subs[i].num_agents == 2 && subs[i].agent[0] >= subs[i].agent[1]) return -1;
+    }
+    Reach* R = (Reach*)malloc(sizeof(Reach));
+    build_reach(L, R);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    pthread_t th[64];
+    BoundJob jobs[64];
+    for (int t = 0; t < nthreads; ++t) {
+        BoundJob* j = &jobs[t];
+        j->c.L = L; j->c.A = A; j->c.K = K; j->c.max_T = 0; j->c.pitch = pitch;
+        j->R = R; j->sin = sin; j->subs = subs; j->nsub = nsub; j->lb = lb; j->doable = doable;
+        j->b0 = B * t / nthreads;
+        j->b1 = B * (t + 1) / nthreads;
+        pthread_create(&th[t], NULL, run_bounds, j);
     }
     for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
     free(R);

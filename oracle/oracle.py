@@ -47,6 +47,9 @@ def lib() -> ctypes.CDLL:
         L.oco_nav_likelihood.argtypes = [ctypes.POINTER(capi.OcLevelDesc), i32, i32, vp, vp, vp,
                                          ctypes.POINTER(capi.OcSubtask), i32, i32, ctypes.c_double, ctypes.c_double,
                                          vp, vp, i64, i64, i32]
+        L.oco_subtask_bounds.restype = ctypes.c_int
+        L.oco_subtask_bounds.argtypes = [ctypes.POINTER(capi.OcLevelDesc), i32, i32, vp,
+                                         ctypes.POINTER(capi.OcSubtask), i32, vp, vp, i64, i64, i32]
         L.oco_action_code.restype = ctypes.c_uint8
         L.oco_action_code.argtypes = [u64, u64, u64, u64]
         _lib = L
@@ -104,6 +107,16 @@ class OracleBatch:
                                       none_action_prob, _p(out), _p(flags), self.B, self.pitch, nthreads)
         assert rc == 0, rc
         return out[:self.B], flags[:self.B]
+
+    def subtask_bounds(self, state, subtasks, nthreads=8):
+        """Full-state subtask bounds (oco_subtask_bounds): returns (lb f32 [S][B], doable u8 [S][B])."""
+        S = len(subtasks)
+        lb = np.zeros(S * self.pitch, np.float32)
+        doable = np.zeros(S * self.pitch, np.uint8)
+        rc = lib().oco_subtask_bounds(ctypes.byref(self.desc), self.A, self.K, _p(state), capi.subtask_array(subtasks),
+                                      S, _p(lb), _p(doable), self.B, self.pitch, nthreads)
+        assert rc == 0, rc
+        return lb.reshape(S, self.pitch)[:, :self.B], doable.reshape(S, self.pitch)[:, :self.B]
 
     def gen_actions(self, actions, env_offset, step, seed) -> None:
         rc = lib().oco_gen_actions(self.A, _p(actions), self.B, self.pitch, env_offset, step, seed)

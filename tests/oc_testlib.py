@@ -358,3 +358,51 @@ class LikelihoodRows:
             if len(errs) > 20:
                 break
         return errs
+
+
+class BoundRows:
+    """Rows of tests/golden/bounds.npz for one (level, A) config: the config's states (one env
+    each) and its subtask table; every row is one (state, subtask) cell of the
+    oc_subtask_bounds output."""
+
+    def __init__(self, fx, cfg: int):
+        st_sel = np.nonzero(fx["st_cfg"] == cfg)[0]
+        self.level = levels.load_level(str(fx["cfg_level"][cfg]))
+        self.A = int(fx["cfg_A"][cfg])
+        self.K = capi.item_slots(self.level)
+        self.agents, self.items, self.t = fx["st_agents"][st_sel], fx["st_items"][st_sel], fx["st_t"][st_sel]
+        self.B = len(st_sel)
+        env_of = {int(s): b for b, s in enumerate(st_sel)}
+        sel = np.nonzero(np.isin(fx["state"], st_sel))[0]
+        keys, self.subtasks = {}, []
+        self.row_env = np.zeros(len(sel), np.int64)
+        self.row_sub = np.zeros(len(sel), np.int64)
+        for r, i in enumerate(sel):
+            n = int((fx["agents"][i] != PAD).sum())
+            key = (int(fx["kind"][i]), tuple(int(a) for a in fx["agents"][i][:n]),
+                   tuple(int(m) for m in fx["start"][i]), int(fx["goal_mask"][i]))
+            if key not in keys:
+                keys[key] = len(self.subtasks)
+                self.subtasks.append(capi.subtask(key[0], key[1], key[2], key[3], 0))
+            self.row_env[r] = env_of[int(fx["state"][i])]
+            self.row_sub[r] = keys[key]
+        self.idx = sel
+        self.exp_lb = fx["lb"][sel]
+        self.exp_doable = fx["doable"][sel].astype(np.uint8)
+
+    def state(self, pitch: int) -> np.ndarray:
+        return state_from_canonical(self.level, self.A, self.K, pitch, self.agents, self.items, self.t)
+
+    def compare(self, lb: np.ndarray, doable: np.ndarray, sub0: int = 0):
+        """Mismatches of [S][B] outputs covering subtasks [sub0, sub0 + S) against the rows."""
+        errs = []
+        S = lb.shape[0]
+        for r in np.nonzero((self.row_sub >= sub0) & (self.row_sub < sub0 + S))[0]:
+            s, b = self.row_sub[r] - sub0, self.row_env[r]
+            if float(lb[s, b]) != float(self.exp_lb[r]) or int(doable[s, b]) != int(self.exp_doable[r]):
+                errs.append("row %d (env %d, subtask %d): lb %r doable %d vs %r %d" % (
+                    self.idx[r], b, self.row_sub[r], float(lb[s, b]), int(doable[s, b]), float(self.exp_lb[r]),
+                    int(self.exp_doable[r])))
+            if len(errs) > 20:
+                break
+        return errs

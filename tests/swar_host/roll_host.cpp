@@ -112,3 +112,43 @@ extern "C" int roll_host(const oc_level_desc* lv, int A, int K, const uint8_t* s
 #undef R_
     return -1;
 }
+
+// oc_bounds_kernel's loop: every env x every configuration, [subtask][pitch] outputs
+template <int A, int K>
+static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask* subs, int nsub, float* lb,
+                   uint8_t* doable, int64_t B, int64_t P) {
+    static uint8_t dist[ocro::kMaxNodes * ocro::kMaxNodes];
+    ocro::RollLevel L;
+    ocro::build_roll_level(L, dist, lv->width, lv->height, lv->tiles);
+    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
+    for (int64_t e = 0; e < B; ++e) {
+        ocro::Row r;
+        for (int a = 0; a < A; ++a) {
+            r.x |= (uint32_t)sin[a * P + e] << (8 * a);
+            r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
+            r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
+        }
+        for (int j = 0; j < K; ++j) {
+            r.loc |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
+            r.mask |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
+        }
+        ocro::RowOps<A, K> ops(L, dist);
+        for (int i = 0; i < nsub; ++i) {
+            const oc_subtask& o = subs[i];
+            ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
+                        {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, {0, 0}};
+            float v;
+            doable[i * P + e] = ops.full_bound(r, s, v) ? 1 : 0;
+            lb[i * P + e] = v;
+        }
+    }
+}
+
+extern "C" int bounds_host(const oc_level_desc* lv, int A, int K, const uint8_t* sin, const oc_subtask* subs, int nsub,
+                           float* lb, uint8_t* doable, int64_t B, int64_t P) {
+#define B_(a, k) \
+    if (A == a && K == k) { bounds<a, k>(lv, sin, subs, nsub, lb, doable, B, P); return 0; }
+    B_(1, 4) B_(2, 4) B_(3, 4) B_(4, 4) B_(1, 8) B_(2, 8) B_(3, 8) B_(4, 8)
+#undef B_
+    return -1;
+}

@@ -1,0 +1,97 @@
+"""The gym shim's planner queries on the host (CPU): the reachability graph the engine exports
+(oc_reachability) against the reference's own ``world.reachability_graph`` of every builtin
+level (tests/golden/reach.json), and ``get_AB_locs_given_objs`` +
+``world.get_lower_bound_between`` + the holding penalty over the shim's object views against
+the reference's ``get_lower_bound_for_subtask_given_objs`` / ``subtask_alloc_is_doable`` rows
+(tests/golden/bounds.npz).  The kernel path of the same queries is tests/test_bounds_gpu.py."""
+import ctypes
+import json
+import os
+import types
+
+import numpy as np
+import pytest
+
+import oc_testlib as tl
+from gym_cooking_amd import capi, envs, levels, recipes
+
+
+def _reach(level_name):
+    if not os.path.isfile(capi.LIB_PATH):
+        pytest.skip("liboc_engine.so not built")
+    lib = capi.load_library()
+    lv = levels.load_level(level_name)
+    d = capi.level_desc(lv, 2)
+    h = ctypes.c_void_p()
+    capi.check(lib.oc_create(ctypes.byref(d), 2, 100, 0, ctypes.byref(h)))
+    try:
+        n = ctypes.c_int32()
+        capi.check(lib.oc_reachability(h, ctypes.byref(n), None, 0, None, 0))
+        node_of = np.zeros(lv.width * lv.height * 5, np.uint8)
+        dist = np.zeros((n.value, n.value), np.uint8)
+        capi.check(lib.oc_reachability(h, ctypes.byref(n), node_of.ctypes.data, node_of.size, dist.ctypes.data,
+                                       dist.size))
+        assert lib.oc_reachability(h, ctypes.byref(n), node_of.ctypes.data, 3, None, 0) == -1  # too small
+    finally:
+        lib.oc_destroy(h)
+    return lv, envs.ReachabilityGraph(lv.width, node_of, dist)
+
+
+def _key(n):
+    return (tuple(n[0]), tuple(n[1]))
+
+
+@pytest.mark.parametrize("level", sorted(json.load(open(os.path.join(tl.GOLDEN, "reach.json")))))
+def test_reachability_graph_matches_reference(level):
+    ref = json.load(open(os.path.join(tl.GOLDEN, "reach.json")))[level]
+    _, g = _reach(level)
+    assert sorted(g.nodes()) == sorted(_key(n) for n in ref["nodes"])
+    assert sorted(tuple(sorted(e)) for e in g.edges()) == sorted(tuple(sorted(_key(n) for n in e))
+                                                                  for e in ref["edges"])
+    # BFS distances are path lengths over exactly those edges
+    nodes = g.nodes()
+    assert g.shortest_path_length(nodes[0], nodes[0]) == 0
+    for u, v in g.edges()[:10]:
+        assert g.shortest_path_length(u, v) == 1
+
+
+def _subtask(kind, start, goal):
+    name = lambda m: envs.ItemView(-1, int(m), None, False).name  # noqa: E731
+    if kind == 0:
+        return None
+    if kind == 1:
+        return recipes.Chop(name(start[0]))
+    if kind == 2:
+        return recipes.Merge(name(start[0]), name(start[1]))
+    return recipes.Deliver(name(goal))
+
+
+@pytest.mark.parametrize("cfg", range(5))
+def test_host_planner_queries_match_reference_rows(cfg):
+    fx = tl.load_fixture("bounds.npz")
+    rows = tl.BoundRows(fx, cfg)
+    lv, g = _reach(str(fx["cfg_level"][cfg]))
+    P = capi.pitch_for(rows.B)
+    s = rows.state(P)
+    views = tl.env_view(s, rows.A, rows.K, P, rows.B).T
+    errs = []
+    for r, i in enumerate(rows.idx):
+        agents_, world, _, _ = envs.build_views(lv, rows.A, rows.K, views[rows.row_env[r]], reachability_graph=g)
+        env = types.SimpleNamespace(sim_agents=agents_, world=world)
+        st = _subtask(int(fx["kind"][i]), fx["start"][i], int(fx["goal_mask"][i]))
+        names = [agents_[a].name for a in fx["agents"][i] if a != tl.PAD]
+        start_obj, goal_obj = envs.get_subtask_obj(st)
+        A_locs, B_locs = envs.OvercookedEnvironment.get_AB_locs_given_objs(
+            env, st, names, start_obj, goal_obj, envs.get_subtask_action_obj(st))
+        dist = world.get_lower_bound_between(st, tuple(a.location for a in agents_ if a.name in names),
+                                             tuple(A_locs), tuple(B_locs))
+        pen = 0.0
+        for a in agents_:  # overcooked_environment.py:611-640
+            if a.name in names and a.holding is not None and not envs._is_merge(st):
+                if a.holding != start_obj and a.holding != goal_obj:
+                    pen += 1.0
+        lb = dist + min(pen, 1)
+        doable = st is None or dist < world.perimeter
+        if float(lb) != float(rows.exp_lb[r]) or int(doable) != int(rows.exp_doable[r]):
+            errs.append("row %d: lb %r doable %d vs %r %d" % (i, lb, doable, rows.exp_lb[r], rows.exp_doable[r]))
+    assert not errs, "\n".join(errs[:20])
