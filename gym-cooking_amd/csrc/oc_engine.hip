@@ -35,6 +35,7 @@
 namespace {
 
 constexpr int kBlock = 256;  // 4 waves
+constexpr int kStepBlock = 128;  // oc_step_kernel: 2 waves
 constexpr int kEPL = 4;      // envs per lane: one dword per byte plane
 constexpr int kEnvsPerBlock = kBlock * kEPL;
 
@@ -169,20 +170,22 @@ __device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tb
     if (has_coll) bst32(b.coll, cm, vo, 0u);
 }
 
-// Persistent, software-pipelined step: a grid of a few blocks per CU walks the batch in
-// chunks of kEnvsPerBlock envs; each lane issues the loads of its next chunk before stepping
-// the current one, so HBM reads, VALU work and stores of different chunks overlap instead of
-// running as three chip-wide phases.  Every lane leaves the loop after ceil(lanes/stride)
-// iterations (no inter-block communication, no spin).
+// One step over the batch: one chunk (kEPL envs) per lane, 128-thread blocks, a grid that
+// covers the whole batch at once (P / 512 blocks, ~4 waves per SIMD resident at 2^20 envs).
+// Each lane issues its chunk's loads first, then the block builds its tile-class table while
+// they are in flight.  Measured on MI355X (tools/stepexp.hip, 2^20 envs, hipGraph of 100
+// ping-pong steps): 9.1 us/step, against 11.1 for a persistent 2-blocks-per-CU grid with a
+// software-pipelined chunk loop (2 chunks per lane at this size: mostly ramp and drain),
+// 10.2 with 256-thread blocks, 9.1 with 2 chunks per lane, and 6.5 for the same loads and
+// stores with no compute.  Staggering block start times did not help (9.2-9.3).
 template <int A, int K>
-__global__ __launch_bounds__(kBlock) void oc_step_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
-                                                         uint8_t* __restrict__ sout,
-                                                         const uint8_t* __restrict__ actions,
-                                                         uint8_t* __restrict__ exec_out,
-                                                         uint8_t* __restrict__ coll_out,
-                                                         uint64_t* __restrict__ stats) {
-    const uint32_t P = (uint32_t)L.pitch;                 // state <= 4 GiB (checked on the host)
-    const uint32_t nlanes = P / kEPL;                     // multiple of kBlock
+__global__ __launch_bounds__(kStepBlock) void oc_step_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
+                                                             uint8_t* __restrict__ sout,
+                                                             const uint8_t* __restrict__ actions,
+                                                             uint8_t* __restrict__ exec_out,
+                                                             uint8_t* __restrict__ coll_out,
+                                                             uint64_t* __restrict__ stats, uint32_t stat_rows) {
+    const uint32_t P = (uint32_t)L.pitch;  // state <= 2 GiB (checked on the host)
     constexpr int NP = 3 * A + 2 * K + 3;
     Bufs b;
     b.sin = make_rsrc(sin, (int64_t)NP * P);
@@ -191,41 +194,28 @@ __global__ __launch_bounds__(kBlock) void oc_step_kernel(LevelArgs L, const uint
     const bool has_ex = exec_out != nullptr, has_coll = coll_out != nullptr;
     b.ex = make_rsrc(has_ex ? (const void*)exec_out : (const void*)sout, (int64_t)A * P);
     b.coll = make_rsrc(has_coll ? (const void*)coll_out : (const void*)sout, (int64_t)P);
-    const uint32_t stride = gridDim.x * (uint32_t)kBlock;
-    uint32_t g = blockIdx.x * (uint32_t)kBlock + threadIdx.x;
-    StepStats st;
-    // Two register sets used in turn (loop unrolled by 2: no register copies of in-flight
-    // loads).  The prefetch is unconditional so the compiler's counted vmcnt waits stay exact;
-    // past the last chunk it re-reads the current one (an L2 hit, no HBM traffic).
-    Chunk<A, K> ca, cb;
-    const bool active = g < nlanes;  // block-uniform
-    if (active) load_chunk<A, K>(ca, b, P, g);  // in flight while the block builds its table
+    const uint32_t g = blockIdx.x * (uint32_t)kStepBlock + threadIdx.x;  // grid * kStepBlock == P / kEPL
+    Chunk<A, K> c;
+    load_chunk<A, K>(c, b, P, g);  // in flight while the block builds its table
     // tile class per cell (bit7 Floor, bit6 Delivery, bit5 Cutboard); cells >= 64 read 0
     __shared__ uint8_t tbl[256];
-    tbl[threadIdx.x] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, threadIdx.x);  // kBlock == 256
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the LDS write, not the chunk loads
-    __builtin_amdgcn_s_barrier();
-    if (active) {
-        for (;;) {
-            load_chunk<A, K>(cb, b, P, g + stride < nlanes ? g + stride : g);
-            step_chunk<A, K>(L, tbl, ca, b, has_ex, has_coll, P, g, st);
-            g += stride;
-            if (g >= nlanes) break;
-            load_chunk<A, K>(ca, b, P, g + stride < nlanes ? g + stride : g);
-            step_chunk<A, K>(L, tbl, cb, b, has_ex, has_coll, P, g, st);
-            g += stride;
-            if (g >= nlanes) break;
-        }
+#pragma unroll
+    for (int i = 0; i < 256 / kStepBlock; ++i) {
+        const uint32_t cell = threadIdx.x + i * kStepBlock;
+        tbl[cell] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, cell);
     }
-
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the LDS writes, not the chunk loads
+    __builtin_amdgcn_s_barrier();
+    StepStats st;
+    step_chunk<A, K>(L, tbl, c, b, has_ex, has_coll, P, g, st);
     if (stats != nullptr) {  // wave sums, then fire-and-forget 64-bit atomics into this block's row
         const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
                                        wave_sum(st.err)};
         if ((threadIdx.x & 63u) == 0u) {
-            unsigned long long* row = (unsigned long long*)stats + (int64_t)blockIdx.x * OC_NSTATS;
+            unsigned long long* row = (unsigned long long*)stats + (int64_t)(blockIdx.x % stat_rows) * OC_NSTATS;
 #pragma unroll
-            for (int c = 0; c < OC_NSTATS; ++c)
-                if (v[c]) atomicAdd(row + c, (unsigned long long)v[c]);
+            for (int q = 0; q < OC_NSTATS; ++q)
+                if (v[q]) atomicAdd(row + q, (unsigned long long)v[q]);
         }
     }
 }
@@ -743,14 +733,9 @@ int hip_check(const char* what) {
     return OC_OK;
 }
 
-// MI355X: 256 CUs.  The step grid is persistent: min(blocks needed, kCUs * blocks per CU).
+// MI355X: 256 CUs (persistent grids of the multi-step, rollout and likelihood kernels).
 constexpr int kCUs = 256;
 
-int64_t step_grid(int64_t pitch, int blocks_per_cu) {
-    const int64_t need = pitch / kEnvsPerBlock;
-    const int64_t cap = (int64_t)kCUs * blocks_per_cu;
-    return need < cap ? need : cap;
-}
 
 int64_t pitch_for(int64_t B) {
     int64_t p = (B + OC_PITCH_ALIGN - 1) / OC_PITCH_ALIGN * OC_PITCH_ALIGN;
@@ -762,18 +747,17 @@ int64_t pitch_for(int64_t B) {
 struct oc_handle {
     oc_level_desc level;
     int32_t A, K, max_T, device;
-    int32_t blocks_per_cu;  // persistent step grid: blocks per CU (OC_BLOCKS_PER_CU, default 2)
     LevelArgs args;
     ocro::RollLevel roll;       // planner rollout tables (nnodes < 0: graph too large)
     uint8_t* roll_dist = nullptr;  // device: reachability distances [kMaxNodes][kMaxNodes]
     uint8_t roll_dist_host[ocro::kMaxNodes * ocro::kMaxNodes];  // the same table on the host
 };
 
-// Statistics rows: one per block of the larger of the oc_step / oc_step_n grids.
-int64_t stats_rows(const oc_handle* h, int64_t B) {
-    const int64_t P = pitch_for(B), need = P / kEnvsPerBlock, cap = (int64_t)kCUs * 5;
-    const int64_t a = step_grid(P, h->blocks_per_cu), b = need < cap ? need : cap;
-    return a > b ? a : b;
+// Statistics rows: one per block of the oc_step_n grid; oc_step's blocks share them modulo
+// the row count (atomics).
+int64_t stats_rows(const oc_handle*, int64_t B) {
+    const int64_t need = pitch_for(B) / kEnvsPerBlock, cap = (int64_t)kCUs * 5;
+    return need < cap ? need : cap;
 }
 
 extern "C" {
@@ -849,11 +833,6 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     h->K = K;
     h->max_T = max_T;
     h->device = device;
-    h->blocks_per_cu = 2;
-    if (const char* e = getenv("OC_BLOCKS_PER_CU")) {  // tuning knob
-        const int v = atoi(e);
-        if (v >= 1 && v <= 16) h->blocks_per_cu = v;
-    }
     h->args = L;
     // planner rollout: the static reachability graph's BFS table (world.py:67-108)
     {
@@ -955,11 +934,12 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
     L.B = B;
     if ((int64_t)(3 * h->A + 2 * h->K + 3) * L.pitch >= (1ll << 31))
         return fail(OC_EINVAL, "batch too large for one launch (state must be < 2 GiB)");
-    const dim3 grid((unsigned)step_grid(L.pitch, h->blocks_per_cu));
+    const dim3 grid((unsigned)(L.pitch / kEPL / kStepBlock));  // pitch is a multiple of 4096
+    const uint32_t rows = (uint32_t)stats_rows(h, B);
     hipStream_t s = (hipStream_t)stream;
-#define OC_LAUNCH_STEP(A, K)                                                                          \
-    hipLaunchKernelGGL((oc_step_kernel<A, K>), grid, dim3(kBlock), 0, s, L, (const uint8_t*)state_in, \
-                       (uint8_t*)state_out, actions, exec_actions, coll_mask, stats)
+#define OC_LAUNCH_STEP(A, K)                                                                              \
+    hipLaunchKernelGGL((oc_step_kernel<A, K>), grid, dim3(kStepBlock), 0, s, L, (const uint8_t*)state_in, \
+                       (uint8_t*)state_out, actions, exec_actions, coll_mask, stats, rows)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_STEP)
     return hip_check("oc_step launch");
 }

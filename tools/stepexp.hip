@@ -1,0 +1,190 @@
+// tools/stepexp.hip -- per-step kernel launch-shape experiments (includes the engine TU).
+// Build: hipcc -O3 -std=c++20 --offload-arch=gfx950 -o tools/stepexp tools/stepexp.hip
+// Workload: partial-divider_salad, 2 agents, B = 2^20, ping-pong state, fresh actions per step,
+// stats on: the bench's per_step_launch line.  Every variant's final state is checked against
+// the product kernel's.
+#include "../gym-cooking_amd/csrc/oc_engine.hip"
+
+#include <vector>
+
+#define CK(x)                                                                                      \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } \
+    } while (0)
+
+namespace {
+
+// Non-persistent: lane g owns chunks g, g + nl/CH, ...: all CH chunks' loads issued first,
+// then each stepped and stored.  BS threads per block.
+template <int A, int K, int CH, int BS, int S = 1, int D = 0, bool MEMONLY = false>
+__global__ __launch_bounds__(BS) void step_flat(LevelArgs L, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
+                                                const uint8_t* __restrict__ actions, uint8_t* __restrict__ exec_out,
+                                                uint8_t* __restrict__ coll_out, uint64_t* __restrict__ stats) {
+    const uint32_t P = (uint32_t)L.pitch, nlanes = P / kEPL, span = nlanes / CH;
+    constexpr int NP = 3 * A + 2 * K + 3;
+    Bufs b;
+    b.sin = make_rsrc(sin, (int64_t)NP * P);
+    b.sout = make_rsrc(sout, (int64_t)NP * P);
+    b.act = make_rsrc(actions, (int64_t)A * P);
+    b.ex = make_rsrc(exec_out, (int64_t)A * P);
+    b.coll = make_rsrc(coll_out, (int64_t)P);
+    const uint32_t g0 = blockIdx.x * (uint32_t)BS + threadIdx.x;
+    if (S > 1) {  // cohort stagger: later blocks start loading later
+        const uint32_t cohort = blockIdx.x * S / gridDim.x;
+        for (uint32_t k = 0; k < cohort * D; ++k) __builtin_amdgcn_s_sleep(1);
+    }
+    Chunk<A, K> c[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) load_chunk<A, K>(c[i], b, P, g0 + i * span);
+    __shared__ uint8_t tbl[256];
+    for (int i = threadIdx.x; i < 256; i += BS) tbl[i] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, i);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    StepStats st;
+    if (MEMONLY) {
+        constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const uint32_t vo = (g0 + i * span) * 4u;
+            for (int a = 0; a < A; ++a) {
+                bst32(b.sout, c[i].wx[a] ^ tbl[a], vo, a * P);
+                bst32(b.sout, c[i].wy[a], vo, (kPY + a) * P);
+                bst32(b.sout, c[i].wh[a], vo, (kPH + a) * P);
+                bst32(b.ex, c[i].wa[a], vo, a * P);
+            }
+            for (int j = 0; j < K; ++j) {
+                bst32(b.sout, c[i].wl[j], vo, (kPL + j) * P);
+                bst32(b.sout, c[i].wm[j], vo, (kPM + j) * P);
+            }
+            typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+            const u32x2 tw = {c[i].wt.x, c[i].wt.y};
+            __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)((g0 + i * span) * 8u), (int)(kPT * P), 0);
+            bst32(b.sout, c[i].wf, vo, kPF * P);
+            bst32(b.coll, c[i].wf, vo, 0u);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) step_chunk<A, K>(L, tbl, c[i], b, true, true, P, g0 + i * span, st);
+    }
+    const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
+                                   wave_sum(st.err)};
+    if ((threadIdx.x & 63u) == 0u) {
+        unsigned long long* row = (unsigned long long*)stats + (int64_t)(blockIdx.x & 1023) * OC_NSTATS;
+#pragma unroll
+        for (int q = 0; q < OC_NSTATS; ++q)
+            if (v[q]) atomicAdd(row + q, (unsigned long long)v[q]);
+    }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const int64_t B = argc > 1 ? atoll(argv[1]) : (1ll << 20);
+    const int A = 2, K = 4;
+    oc_level_desc lv{};
+    const char* rows[7] = {"-----t-", "/  -  l", "/  -  -", "*  -  -", "-  -  -", "-     p", "-----p-"};
+    lv.width = 7;
+    lv.height = 7;
+    int ni = 0;
+    for (int y = 0; y < 7; ++y)
+        for (int x = 0; x < 7; ++x) {
+            const char ch = rows[y][x];
+            const int c = y * 7 + x;
+            lv.tiles[c] = ch == ' ' ? 0 : ch == '/' ? 2 : ch == '*' ? 3 : 1;
+            if (ch == 't' || ch == 'l' || ch == 'p') {
+                lv.item_cell[ni] = (uint8_t)c;
+                lv.item_mask[ni++] = ch == 't' ? 1 : ch == 'l' ? 2 : 8;
+            }
+        }
+    lv.num_items = ni;
+    lv.num_spawns = 4;
+    const uint8_t sx[4] = {2, 4, 4, 2}, sy[4] = {1, 1, 4, 4};
+    for (int a = 0; a < 4; ++a) { lv.spawn_x[a] = sx[a]; lv.spawn_y[a] = sy[a]; }
+    lv.num_goals = 1;
+    lv.goal_mask[0] = 0x3B;
+    oc_handle* h;
+    if (oc_create(&lv, A, 100, 0, &h) != 0) { printf("create: %s\n", oc_last_error()); return 1; }
+    oc_layout lay;
+    oc_get_layout(h, B, &lay);
+    const int64_t P = lay.pitch, NP = lay.num_planes;
+    const int R = 100;  // distinct action buffers, one per step of a run
+    uint8_t *sa, *sb, *act, *ex, *coll;
+    CK(hipMalloc(&sa, NP * P));
+    CK(hipMalloc(&sb, NP * P));
+    CK(hipMalloc(&act, (int64_t)R * A * P));
+    CK(hipMalloc(&ex, A * P));
+    CK(hipMalloc(&coll, P));
+    uint64_t* stats;
+    CK(hipMalloc(&stats, 1 << 20));
+    CK(hipMemset(stats, 0, 1 << 20));
+    for (int r = 0; r < R; ++r) oc_gen_actions(h, act + (int64_t)r * A * P, B, 0, r, 1, nullptr);
+    CK(hipDeviceSynchronize());
+    LevelArgs L = h->args;
+    L.pitch = P;
+    L.B = B;
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const double bytes = 39.0 * B;
+    printf("B=%lld  algorithmic %.1f MB/step, %d steps per graph\n", (long long)B, bytes / 1e6, R);
+    std::vector<uint8_t> ref(NP * P), got(NP * P);
+
+    // run(step): R ping-pong steps from the reset state, as a hipGraph; returns us/step and
+    // leaves the final state in sa (R even)
+    auto run = [&](const char* name, auto step_fn) {
+        hipGraph_t gr;
+        hipGraphExec_t ge;
+        CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+        for (int r = 0; r < R; ++r) step_fn(r & 1 ? sb : sa, r & 1 ? sa : sb, act + (int64_t)r * A * P);
+        CK(hipStreamEndCapture(s, &gr));
+        CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+        float best = 1e30f;
+        for (int rep = 0; rep < 6; ++rep) {
+            oc_reset(h, sa, B, s);
+            CK(hipEventRecord(e0, s));
+            CK(hipGraphLaunch(ge, s));
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (rep > 0 && ms < best) best = ms;
+        }
+        CK(hipMemcpy(got.data(), sa, NP * P, hipMemcpyDeviceToHost));
+        const double us = best * 1000.0 / R;
+        const bool same = ref.empty() || got == ref;
+        printf("%-40s %7.2f us/step  %6.2f TB/s alg  %s\n", name, us, bytes / us / 1e6, same ? "ok" : "MISMATCH");
+        CK(hipGraphExecDestroy(ge));
+        CK(hipGraphDestroy(gr));
+        return us;
+    };
+    ref.clear();
+    run("product oc_step", [&](uint8_t* i, uint8_t* o, uint8_t* a) { oc_step(h, i, o, a, ex, coll, stats, B, s); });
+    ref = got;
+    const uint32_t nl = (uint32_t)(P / kEPL);
+#define FLATX(NAME, CH, BS, ...)                                                                            \
+    run(NAME, [&](uint8_t* i, uint8_t* o, uint8_t* a) {                                                       \
+        hipLaunchKernelGGL((step_flat<2, 4, CH, BS, __VA_ARGS__>), dim3(nl / CH / BS), dim3(BS), 0, s, L, i, o, a, ex, coll, stats); \
+    })
+    FLATX("flat CH=1 block 128", 1, 128, 1, 0, false);
+    FLATX("flat CH=1 block 256", 1, 256, 1, 0, false);
+    FLATX("flat CH=2 block 128", 1, 128, 1, 0, false);
+    ref.clear();
+    FLATX("MEMONLY flat CH=1 block 128", 1, 128, 1, 0, true);
+    FLATX("MEMONLY flat CH=1 block 256", 1, 256, 1, 0, true);
+    FLATX("MEMONLY flat CH=2 block 128", 2, 128, 1, 0, true);
+    run("product oc_step", [&](uint8_t* i, uint8_t* o, uint8_t* a) { oc_step(h, i, o, a, ex, coll, stats, B, s); });
+    ref = got;
+    FLATX("stagger S2 D8   block 128", 1, 128, 2, 8, false);
+    FLATX("stagger S2 D16  block 128", 1, 128, 2, 16, false);
+    FLATX("stagger S2 D32  block 128", 1, 128, 2, 32, false);
+    FLATX("stagger S4 D4   block 128", 1, 128, 4, 4, false);
+    FLATX("stagger S4 D8   block 128", 1, 128, 4, 8, false);
+    FLATX("stagger S4 D16  block 128", 1, 128, 4, 16, false);
+    FLATX("stagger S8 D4   block 128", 1, 128, 8, 4, false);
+    FLATX("stagger S8 D8   block 128", 1, 128, 8, 8, false);
+    FLATX("stagger S4 D8   block 256", 1, 256, 4, 8, false);
+    return 0;
+}
