@@ -60,11 +60,18 @@ struct LevelArgs {
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, int j) { return (w >> (8 * j)) & 0xFFu; }
 __device__ __forceinline__ uint32_t byte_of2(const uint32_t (&w)[2], int j) { return byte_of(w[j >> 2], j & 3); }
 
-// Statistics partial sums, one row of OC_NSTATS uint64 per block.
+// Statistics partial sums, one row of OC_NSTATS uint64 per block.  Wave sum over DPP (VALU
+// lane moves, no LDS round trips): an inclusive scan inside each 16-lane row (row_shr 1, 2,
+// 4, 8), then row 0's and row 1's totals broadcast into the rows above (row_bcast 15 / 31);
+// lane 63 ends with the wave total.
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 // One lane's slice of the batch: kEPL consecutive envs, one dword per byte plane.
@@ -88,8 +95,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64
 __device__ __forceinline__ uint32_t bld32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
 }
+// Store cache policy (gfx950 CPol bits of the buffer intrinsics): 0 plain, 2 nt, 16 sc1,
+// 17 sc0 sc1.  sc1 stores leave no dirty line in the XCD's L2, so the bytes go out to HBM
+// while the kernel still computes instead of in the write-back at the kernel boundary (which
+// costs about B / 6 TB/s for B dirty bytes, MI355X_MICROARCH.md "boundary").
+// oc_step_n, whose trajectory stream is far larger than L2, is faster with nt stores instead
+// (tools/stepexp.hip: 4.3 vs 5.2-5.3 us/step at 2^20 envs; sc1 5.3).
+constexpr int kCPsc1 = 16, kCPnt = 2;
+template <int CP = 0>
 __device__ __forceinline__ void bst32(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t voff, uint32_t soff) {
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, CP);
 }
 
 template <int A, int K>
@@ -120,7 +135,7 @@ struct StepStats {
 };
 
 // Step the kEPL envs of chunk c (SWAR, oc_swar.h) and store every output plane word of lane g.
-template <int A, int K>
+template <int A, int K, int CP = 0>
 __device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tbl, Chunk<A, K>& c, const Bufs& b,
                                            bool has_ex, bool has_coll, uint32_t P, uint32_t g, StepStats& st) {
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
@@ -150,24 +165,24 @@ __device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tb
     const uint32_t vo = g * 4u;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-        bst32(b.sout, c.wx[a], vo, a * P);
-        bst32(b.sout, c.wy[a], vo, (kPY + a) * P);
-        bst32(b.sout, c.wh[a], vo, (kPH + a) * P);
+        bst32<CP>(b.sout, c.wx[a], vo, a * P);
+        bst32<CP>(b.sout, c.wy[a], vo, (kPY + a) * P);
+        bst32<CP>(b.sout, c.wh[a], vo, (kPH + a) * P);
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        bst32(b.sout, c.wl[j], vo, (kPL + j) * P);
-        bst32(b.sout, c.wm[j], vo, (kPM + j) * P);
+        bst32<CP>(b.sout, c.wl[j], vo, (kPL + j) * P);
+        bst32<CP>(b.sout, c.wm[j], vo, (kPM + j) * P);
     }
     typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
     const u32x2 tw = {T0, T1};
-    __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)(g * 8u), (int)(kPT * P), 0);
-    bst32(b.sout, c.wf, vo, kPF * P);
+    __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)(g * 8u), (int)(kPT * P), CP);
+    bst32<CP>(b.sout, c.wf, vo, kPF * P);
     if (has_ex) {
 #pragma unroll
-        for (int a = 0; a < A; ++a) bst32(b.ex, ex[a], vo, a * P);
+        for (int a = 0; a < A; ++a) bst32<CP>(b.ex, ex[a], vo, a * P);
     }
-    if (has_coll) bst32(b.coll, cm, vo, 0u);
+    if (has_coll) bst32<CP>(b.coll, cm, vo, 0u);
 }
 
 // One step over the batch: one chunk (kEPL envs) per lane, 128-thread blocks, a grid that
@@ -207,7 +222,7 @@ __global__ __launch_bounds__(kStepBlock) void oc_step_kernel(LevelArgs L, const 
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the LDS writes, not the chunk loads
     __builtin_amdgcn_s_barrier();
     StepStats st;
-    step_chunk<A, K>(L, tbl, c, b, has_ex, has_coll, P, g, st);
+    step_chunk<A, K, kCPsc1>(L, tbl, c, b, has_ex, has_coll, P, g, st);
     if (stats != nullptr) {  // wave sums, then fire-and-forget 64-bit atomics into this block's row
         const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
                                        wave_sum(st.err)};
@@ -225,7 +240,7 @@ __global__ __launch_bounds__(kStepBlock) void oc_step_kernel(LevelArgs L, const 
 // and writes the step's outputs: the full state into traj[r] (when given), the executed
 // actions and the collision mask; the state after the last step goes to sout.  Outputs are
 // byte-identical to n oc_step launches with ping-pong buffers.
-template <int A, int K>
+template <int A, int K, int CP = 0>
 __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
                                                            uint8_t* __restrict__ sout,
                                                            const uint8_t* __restrict__ actions,
@@ -277,8 +292,8 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
             ocsw::step4<A, K>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, act, ex, cm, cls_of);
             const uint32_t ended = (c.wf & ~f_in & vmask) & ocsw::k01;
             st.eps += __popc(ended);
-    st.succ += __popc(c.wf & (ended << 1));
-    st.err += __popc(c.wf & (ended << 2));
+            st.succ += __popc(c.wf & (ended << 1));
+            st.err += __popc(c.wf & (ended << 2));
             st.coll += __popc(cm & vmask);
             const uint32_t efull = (0x80808080u - ended) ^ 0x80808080u;  // no multiply
             const uint32_t sa = T0 & __builtin_amdgcn_perm(0u, efull, 0x01010000u);
@@ -288,39 +303,39 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
                 const uint32_t base = (uint32_t)r * NP * P;
 #pragma unroll
                 for (int a = 0; a < A; ++a) {
-                    bst32(tr, c.wx[a], vo, base + a * P);
-                    bst32(tr, c.wy[a], vo, base + (kPY + a) * P);
-                    bst32(tr, c.wh[a], vo, base + (kPH + a) * P);
+                    bst32<CP>(tr, c.wx[a], vo, base + a * P);
+                    bst32<CP>(tr, c.wy[a], vo, base + (kPY + a) * P);
+                    bst32<CP>(tr, c.wh[a], vo, base + (kPH + a) * P);
                 }
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
-                    bst32(tr, c.wl[j], vo, base + (kPL + j) * P);
-                    bst32(tr, c.wm[j], vo, base + (kPM + j) * P);
+                    bst32<CP>(tr, c.wl[j], vo, base + (kPL + j) * P);
+                    bst32<CP>(tr, c.wm[j], vo, base + (kPM + j) * P);
                 }
                 const u32x2 tw = {T0, T1};
-                __builtin_amdgcn_raw_buffer_store_b64(tw, tr, (int)(g * 8u), (int)(base + kPT * P), 0);
-                bst32(tr, c.wf, vo, base + kPF * P);
+                __builtin_amdgcn_raw_buffer_store_b64(tw, tr, (int)(g * 8u), (int)(base + kPT * P), CP);
+                bst32<CP>(tr, c.wf, vo, base + kPF * P);
             }
             if (has_ex) {
 #pragma unroll
-                for (int a = 0; a < A; ++a) bst32(b.ex, ex[a], vo, (uint32_t)(r * A + a) * P);
+                for (int a = 0; a < A; ++a) bst32<CP>(b.ex, ex[a], vo, (uint32_t)(r * A + a) * P);
             }
-            if (has_coll) bst32(b.coll, cm, vo, (uint32_t)r * P);
+            if (has_coll) bst32<CP>(b.coll, cm, vo, (uint32_t)r * P);
         }
 #pragma unroll
         for (int a = 0; a < A; ++a) {
-            bst32(b.sout, c.wx[a], vo, a * P);
-            bst32(b.sout, c.wy[a], vo, (kPY + a) * P);
-            bst32(b.sout, c.wh[a], vo, (kPH + a) * P);
+            bst32<CP>(b.sout, c.wx[a], vo, a * P);
+            bst32<CP>(b.sout, c.wy[a], vo, (kPY + a) * P);
+            bst32<CP>(b.sout, c.wh[a], vo, (kPH + a) * P);
         }
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            bst32(b.sout, c.wl[j], vo, (kPL + j) * P);
-            bst32(b.sout, c.wm[j], vo, (kPM + j) * P);
+            bst32<CP>(b.sout, c.wl[j], vo, (kPL + j) * P);
+            bst32<CP>(b.sout, c.wm[j], vo, (kPM + j) * P);
         }
         const u32x2 tw = {T0, T1};
-        __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)(g * 8u), (int)(kPT * P), 0);
-        bst32(b.sout, c.wf, vo, kPF * P);
+        __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)(g * 8u), (int)(kPT * P), CP);
+        bst32<CP>(b.sout, c.wf, vo, kPF * P);
     }
     if (stats != nullptr) {
         const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
@@ -974,7 +989,7 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
         uint8_t* cm = coll_mask ? coll_mask + off * L.pitch : nullptr;
         const uint8_t* ac = actions + off * h->A * L.pitch;
 #define OC_LAUNCH_STEPN(A, K)                                                                                     \
-    hipLaunchKernelGGL((oc_step_n_kernel<A, K>), grid, dim3(kBlock), 0, s, L, src, (uint8_t*)state_out, ac, tr, ex, cm, \
+    hipLaunchKernelGGL((oc_step_n_kernel<A, K, kCPnt>), grid, dim3(kBlock), 0, s, L, src, (uint8_t*)state_out, ac, tr, ex, cm, \
                        stats, m)
         OC_DISPATCH(h->A, h->K, OC_LAUNCH_STEPN)
         src = (const uint8_t*)state_out;

@@ -5,6 +5,7 @@
 // the product kernel's.
 #include "../gym-cooking_amd/csrc/oc_engine.hip"
 
+#include <algorithm>
 #include <vector>
 
 #define CK(x)                                                                                      \
@@ -17,7 +18,7 @@ namespace {
 
 // Non-persistent: lane g owns chunks g, g + nl/CH, ...: all CH chunks' loads issued first,
 // then each stepped and stored.  BS threads per block.
-template <int A, int K, int CH, int BS, int S = 1, int D = 0, bool MEMONLY = false>
+template <int A, int K, int CH, int BS, int S = 1, int D = 0, bool MEMONLY = false, int CP = 0>
 __global__ __launch_bounds__(BS) void step_flat(LevelArgs L, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
                                                 const uint8_t* __restrict__ actions, uint8_t* __restrict__ exec_out,
                                                 uint8_t* __restrict__ coll_out, uint64_t* __restrict__ stats) {
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(BS) void step_flat(LevelArgs L, const uint8_t* __re
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < CH; ++i) step_chunk<A, K>(L, tbl, c[i], b, true, true, P, g0 + i * span, st);
+        for (int i = 0; i < CH; ++i) step_chunk<A, K, CP>(L, tbl, c[i], b, true, true, P, g0 + i * span, st);
     }
     const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
                                    wave_sum(st.err)};
@@ -77,7 +78,83 @@ __global__ __launch_bounds__(BS) void step_flat(LevelArgs L, const uint8_t* __re
     }
 }
 
+// Wave timeline of one flat step launch: lane 0 of every wave records s_memrealtime (100 MHz)
+// at start, when its loads have landed, when its stores are issued and when they are acked.
+template <int A, int K, int BS, bool MEMONLY>
+__global__ __launch_bounds__(BS) void step_timeline(LevelArgs L, const uint8_t* __restrict__ sin,
+                                                    uint8_t* __restrict__ sout, const uint8_t* __restrict__ actions,
+                                                    uint8_t* __restrict__ exec_out, uint8_t* __restrict__ coll_out,
+                                                    uint64_t* __restrict__ tl) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t P = (uint32_t)L.pitch;
+    constexpr int NP = 3 * A + 2 * K + 3;
+    Bufs b;
+    b.sin = make_rsrc(sin, (int64_t)NP * P);
+    b.sout = make_rsrc(sout, (int64_t)NP * P);
+    b.act = make_rsrc(actions, (int64_t)A * P);
+    b.ex = make_rsrc(exec_out, (int64_t)A * P);
+    b.coll = make_rsrc(coll_out, (int64_t)P);
+    const uint32_t g = blockIdx.x * (uint32_t)BS + threadIdx.x;
+    Chunk<A, K> c;
+    load_chunk<A, K>(c, b, P, g);
+    __shared__ uint8_t tbl[256];
+    for (int i = threadIdx.x; i < 256; i += BS) tbl[i] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, i);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every load landed
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    StepStats st;
+    if (MEMONLY) {
+        constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+        const uint32_t vo = g * 4u;
+        for (int a = 0; a < A; ++a) {
+            bst32(b.sout, c.wx[a] ^ tbl[a], vo, a * P);
+            bst32(b.sout, c.wy[a], vo, (kPY + a) * P);
+            bst32(b.sout, c.wh[a], vo, (kPH + a) * P);
+            bst32(b.ex, c.wa[a], vo, a * P);
+        }
+        for (int j = 0; j < K; ++j) {
+            bst32(b.sout, c.wl[j], vo, (kPL + j) * P);
+            bst32(b.sout, c.wm[j], vo, (kPM + j) * P);
+        }
+        typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+        const u32x2 tw = {c.wt.x, c.wt.y};
+        __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)(g * 8u), (int)(kPT * P), 0);
+        bst32(b.sout, c.wf, vo, kPF * P);
+        bst32(b.coll, c.wf, vo, 0u);
+    } else {
+        step_chunk<A, K>(L, tbl, c, b, true, true, P, g, st);
+    }
+    const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63u) == 0u) {
+        uint64_t* o = tl + (uint64_t)(g >> 6) * 5;
+        o[0] = t0; o[1] = t1; o[2] = t2; o[3] = t3;
+        o[4] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_ID
+    }
+}
+
 }  // namespace
+
+static void timeline_report(const char* name, const std::vector<uint64_t>& t, int nw) {
+    uint64_t base = ~0ull;
+    for (int w = 0; w < nw; ++w) base = t[w * 5] < base ? t[w * 5] : base;
+    std::vector<double> ev[4];
+    double dur[3] = {0, 0, 0};
+    for (int w = 0; w < nw; ++w) {
+        for (int k = 0; k < 4; ++k) ev[k].push_back((t[w * 5 + k] - base) * 0.01);  // us
+        for (int k = 0; k < 3; ++k) dur[k] += (t[w * 5 + k + 1] - t[w * 5 + k]) * 0.01;
+    }
+    printf("%s: %d waves; per-wave mean: load %.2f us, compute+issue %.2f us, store drain %.2f us\n", name, nw,
+           dur[0] / nw, dur[1] / nw, dur[2] / nw);
+    const char* nm[4] = {"start", "loaded", "issued", "acked"};
+    for (int k = 0; k < 4; ++k) {
+        std::sort(ev[k].begin(), ev[k].end());
+        printf("  %-7s p0 %5.2f p10 %5.2f p25 %5.2f p50 %5.2f p75 %5.2f p90 %5.2f p100 %5.2f\n", nm[k], ev[k][0],
+               ev[k][nw / 10], ev[k][nw / 4], ev[k][nw / 2], ev[k][3 * nw / 4], ev[k][9 * nw / 10], ev[k][nw - 1]);
+    }
+}
 
 int main(int argc, char** argv) {
     const int64_t B = argc > 1 ? atoll(argv[1]) : (1ll << 20);
@@ -177,14 +254,40 @@ int main(int argc, char** argv) {
     FLATX("MEMONLY flat CH=2 block 128", 2, 128, 1, 0, true);
     run("product oc_step", [&](uint8_t* i, uint8_t* o, uint8_t* a) { oc_step(h, i, o, a, ex, coll, stats, B, s); });
     ref = got;
-    FLATX("stagger S2 D8   block 128", 1, 128, 2, 8, false);
-    FLATX("stagger S2 D16  block 128", 1, 128, 2, 16, false);
-    FLATX("stagger S2 D32  block 128", 1, 128, 2, 32, false);
-    FLATX("stagger S4 D4   block 128", 1, 128, 4, 4, false);
-    FLATX("stagger S4 D8   block 128", 1, 128, 4, 8, false);
-    FLATX("stagger S4 D16  block 128", 1, 128, 4, 16, false);
-    FLATX("stagger S8 D4   block 128", 1, 128, 8, 4, false);
-    FLATX("stagger S8 D8   block 128", 1, 128, 8, 8, false);
-    FLATX("stagger S4 D8   block 256", 1, 256, 4, 8, false);
+    FLATX("store plain    block 128", 1, 128, 1, 0, false, 0);
+    FLATX("store sc1      block 128", 1, 128, 1, 0, false, 16);
+    FLATX("store sc1 CH2  block 128", 2, 128, 1, 0, false, 16);
+    FLATX("MEMONLY plain  block 128", 1, 128, 1, 0, true, 0);
+    // oc_step_n store policy: 2 launches x 100 steps, trajectory written (the bench headline)
+    {
+        uint8_t* traj;
+        uint8_t *exn, *colln;
+        CK(hipMalloc(&traj, (int64_t)R * NP * P));
+        CK(hipMalloc(&exn, (int64_t)R * A * P));
+        CK(hipMalloc(&colln, (int64_t)R * P));
+        const int64_t need = P / kEnvsPerBlock, cap = (int64_t)kCUs * 5;
+        const dim3 grid((unsigned)(need < cap ? need : cap));
+        auto stepn = [&](auto kern, const char* name) {
+            float best = 1e30f;
+            for (int rep = 0; rep < 6; ++rep) {
+                oc_reset(h, sa, B, s);
+                CK(hipEventRecord(e0, s));
+                hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, sa, sb, act, traj, exn, colln, stats, R);
+                hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, sb, sa, act, traj, exn, colln, stats, R);
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (rep > 0 && ms < best) best = ms;
+            }
+            const double us = best * 1000.0 / (2 * R);
+            printf("%-40s %7.2f us/step  %6.2f TB/s alg (22.17 B/env-step)\n", name, us, 22.17 * B / us / 1e6);
+        };
+        stepn(oc_step_n_kernel<2, 4, 0>, "step_n plain stores");
+        stepn(oc_step_n_kernel<2, 4, 16>, "step_n sc1 stores");
+        stepn(oc_step_n_kernel<2, 4, 2>, "step_n nt stores");
+        stepn(oc_step_n_kernel<2, 4, 0>, "step_n plain stores");
+        stepn(oc_step_n_kernel<2, 4, 16>, "step_n sc1 stores");
+    }
     return 0;
 }
