@@ -49,20 +49,20 @@ __global__ __launch_bounds__(BS) void step_flat(LevelArgs L, const uint8_t* __re
         for (int i = 0; i < CH; ++i) {
             const uint32_t vo = (g0 + i * span) * 4u;
             for (int a = 0; a < A; ++a) {
-                bst32(b.sout, c[i].wx[a] ^ tbl[a], vo, a * P);
-                bst32(b.sout, c[i].wy[a], vo, (kPY + a) * P);
-                bst32(b.sout, c[i].wh[a], vo, (kPH + a) * P);
-                bst32(b.ex, c[i].wa[a], vo, a * P);
+                bst32<CP>(b.sout, c[i].wx[a] ^ tbl[a], vo, a * P);
+                bst32<CP>(b.sout, c[i].wy[a], vo, (kPY + a) * P);
+                bst32<CP>(b.sout, c[i].wh[a], vo, (kPH + a) * P);
+                bst32<CP>(b.ex, c[i].wa[a], vo, a * P);
             }
             for (int j = 0; j < K; ++j) {
-                bst32(b.sout, c[i].wl[j], vo, (kPL + j) * P);
-                bst32(b.sout, c[i].wm[j], vo, (kPM + j) * P);
+                bst32<CP>(b.sout, c[i].wl[j], vo, (kPL + j) * P);
+                bst32<CP>(b.sout, c[i].wm[j], vo, (kPM + j) * P);
             }
             typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
             const u32x2 tw = {c[i].wt.x, c[i].wt.y};
-            __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)((g0 + i * span) * 8u), (int)(kPT * P), 0);
-            bst32(b.sout, c[i].wf, vo, kPF * P);
-            bst32(b.coll, c[i].wf, vo, 0u);
+            __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)((g0 + i * span) * 8u), (int)(kPT * P), CP);
+            bst32<CP>(b.sout, c[i].wf, vo, kPF * P);
+            bst32<CP>(b.coll, c[i].wf, vo, 0u);
         }
     } else {
 #pragma unroll
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(BS) void step_flat(LevelArgs L, const uint8_t* __re
 
 // Wave timeline of one flat step launch: lane 0 of every wave records s_memrealtime (100 MHz)
 // at start, when its loads have landed, when its stores are issued and when they are acked.
-template <int A, int K, int BS, bool MEMONLY>
+template <int A, int K, int BS, bool MEMONLY, int CP = 16>
 __global__ __launch_bounds__(BS) void step_timeline(LevelArgs L, const uint8_t* __restrict__ sin,
                                                     uint8_t* __restrict__ sout, const uint8_t* __restrict__ actions,
                                                     uint8_t* __restrict__ exec_out, uint8_t* __restrict__ coll_out,
@@ -108,22 +108,22 @@ __global__ __launch_bounds__(BS) void step_timeline(LevelArgs L, const uint8_t* 
         constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
         const uint32_t vo = g * 4u;
         for (int a = 0; a < A; ++a) {
-            bst32(b.sout, c.wx[a] ^ tbl[a], vo, a * P);
-            bst32(b.sout, c.wy[a], vo, (kPY + a) * P);
-            bst32(b.sout, c.wh[a], vo, (kPH + a) * P);
-            bst32(b.ex, c.wa[a], vo, a * P);
+            bst32<CP>(b.sout, c.wx[a] ^ tbl[a], vo, a * P);
+            bst32<CP>(b.sout, c.wy[a], vo, (kPY + a) * P);
+            bst32<CP>(b.sout, c.wh[a], vo, (kPH + a) * P);
+            bst32<CP>(b.ex, c.wa[a], vo, a * P);
         }
         for (int j = 0; j < K; ++j) {
-            bst32(b.sout, c.wl[j], vo, (kPL + j) * P);
-            bst32(b.sout, c.wm[j], vo, (kPM + j) * P);
+            bst32<CP>(b.sout, c.wl[j], vo, (kPL + j) * P);
+            bst32<CP>(b.sout, c.wm[j], vo, (kPM + j) * P);
         }
         typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
         const u32x2 tw = {c.wt.x, c.wt.y};
-        __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)(g * 8u), (int)(kPT * P), 0);
-        bst32(b.sout, c.wf, vo, kPF * P);
-        bst32(b.coll, c.wf, vo, 0u);
+        __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)(g * 8u), (int)(kPT * P), CP);
+        bst32<CP>(b.sout, c.wf, vo, kPF * P);
+        bst32<CP>(b.coll, c.wf, vo, 0u);
     } else {
-        step_chunk<A, K>(L, tbl, c, b, true, true, P, g, st);
+        step_chunk<A, K, CP>(L, tbl, c, b, true, true, P, g, st);
     }
     const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
     __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -245,49 +245,22 @@ int main(int argc, char** argv) {
     run(NAME, [&](uint8_t* i, uint8_t* o, uint8_t* a) {                                                       \
         hipLaunchKernelGGL((step_flat<2, 4, CH, BS, __VA_ARGS__>), dim3(nl / CH / BS), dim3(BS), 0, s, L, i, o, a, ex, coll, stats); \
     })
-    FLATX("flat CH=1 block 128", 1, 128, 1, 0, false);
-    FLATX("flat CH=1 block 256", 1, 256, 1, 0, false);
-    FLATX("flat CH=2 block 128", 1, 128, 1, 0, false);
     ref.clear();
-    FLATX("MEMONLY flat CH=1 block 128", 1, 128, 1, 0, true);
-    FLATX("MEMONLY flat CH=1 block 256", 1, 256, 1, 0, true);
-    FLATX("MEMONLY flat CH=2 block 128", 2, 128, 1, 0, true);
-    run("product oc_step", [&](uint8_t* i, uint8_t* o, uint8_t* a) { oc_step(h, i, o, a, ex, coll, stats, B, s); });
-    ref = got;
-    FLATX("store plain    block 128", 1, 128, 1, 0, false, 0);
-    FLATX("store sc1      block 128", 1, 128, 1, 0, false, 16);
-    FLATX("store sc1 CH2  block 128", 2, 128, 1, 0, false, 16);
-    FLATX("MEMONLY plain  block 128", 1, 128, 1, 0, true, 0);
-    // oc_step_n store policy: 2 launches x 100 steps, trajectory written (the bench headline)
+    FLATX("MEMONLY sc1    block 128", 1, 128, 1, 0, true, 16);
     {
-        uint8_t* traj;
-        uint8_t *exn, *colln;
-        CK(hipMalloc(&traj, (int64_t)R * NP * P));
-        CK(hipMalloc(&exn, (int64_t)R * A * P));
-        CK(hipMalloc(&colln, (int64_t)R * P));
-        const int64_t need = P / kEnvsPerBlock, cap = (int64_t)kCUs * 5;
-        const dim3 grid((unsigned)(need < cap ? need : cap));
-        auto stepn = [&](auto kern, const char* name) {
-            float best = 1e30f;
-            for (int rep = 0; rep < 6; ++rep) {
-                oc_reset(h, sa, B, s);
-                CK(hipEventRecord(e0, s));
-                hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, sa, sb, act, traj, exn, colln, stats, R);
-                hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, sb, sa, act, traj, exn, colln, stats, R);
-                CK(hipEventRecord(e1, s));
-                CK(hipEventSynchronize(e1));
-                float ms;
-                CK(hipEventElapsedTime(&ms, e0, e1));
-                if (rep > 0 && ms < best) best = ms;
-            }
-            const double us = best * 1000.0 / (2 * R);
-            printf("%-40s %7.2f us/step  %6.2f TB/s alg (22.17 B/env-step)\n", name, us, 22.17 * B / us / 1e6);
-        };
-        stepn(oc_step_n_kernel<2, 4, 0>, "step_n plain stores");
-        stepn(oc_step_n_kernel<2, 4, 16>, "step_n sc1 stores");
-        stepn(oc_step_n_kernel<2, 4, 2>, "step_n nt stores");
-        stepn(oc_step_n_kernel<2, 4, 0>, "step_n plain stores");
-        stepn(oc_step_n_kernel<2, 4, 16>, "step_n sc1 stores");
+        const int nw = (int)(nl / 64);
+        uint64_t* tl;
+        CK(hipMalloc(&tl, (size_t)nw * 5 * 8));
+        std::vector<uint64_t> host((size_t)nw * 5);
+#define TL(NAME, BS, MO)                                                                                         \
+        for (int rep = 0; rep < 3; ++rep) {                                                                      \
+            hipLaunchKernelGGL((step_timeline<2, 4, BS, MO>), dim3(nl / BS), dim3(BS), 0, s, L, sa, sb, act, ex, coll, tl); \
+            CK(hipStreamSynchronize(s));                                                                         \
+        }                                                                                                        \
+        CK(hipMemcpy(host.data(), tl, host.size() * 8, hipMemcpyDeviceToHost));                                  \
+        timeline_report(NAME, host, nw);
+        TL("timeline step sc1 128", 128, false);
+        TL("timeline memonly sc1 128", 128, true);
     }
     return 0;
 }
