@@ -588,49 +588,67 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
         psel |= (ch >= 3u ? 0x0Cu : ch) << (8 * c);
     }
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    for (int i = threadIdx.x; i < items; i += kBlock) {
-        const int r = i / G, g = i - r * G;
-        const int py = ty * tile + r, px0 = kRenderPx * g;
-        const u32x4* bsrc = (const u32x4*)(bg + (int64_t)py * row_px + px0);
-        uint32_t p[kRenderPx];
+    // The block's output rows are contiguous and group i lands at byte 48 i, so a wave's 64
+    // groups are 3 KB contiguous.  Each lane packs its 48 bytes into the wave's LDS slice, and
+    // the wave then stores the slice as three fully contiguous 1 KB instructions (16 B per
+    // lane) instead of three 16 B-per-lane instructions at a 48 B stride.
+    __shared__ u32x4 stage[kBlock / 64][64 * 3];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint8_t* const blk_out = img + (int64_t)ty * tile * row_px * 3;
+    for (int base = 0; base < items; base += kBlock) {
+        const int i = base + threadIdx.x;
+        if (i < items) {
+            const int r = i / G, g = i - r * G;
+            const int py = ty * tile + r, px0 = kRenderPx * g;
+            const u32x4* bsrc = (const u32x4*)(bg + (int64_t)py * row_px + px0);
+            uint32_t p[kRenderPx];
 #pragma unroll
-        for (int q = 0; q < kRenderPx / 4; ++q) {
-            const u32x4 v = bsrc[q];
-            p[4 * q] = v.x;
-            p[4 * q + 1] = v.y;
-            p[4 * q + 2] = v.z;
-            p[4 * q + 3] = v.w;
-        }
-        const int tx = px0 / tile, lx0 = px0 - tx * tile;  // a group never straddles two cells
-        const int n = dl_n[tx];
-        for (int d = 0; d < n; ++d) {
-            const uint32_t geo = dl_geo[tx][d];
-            const int sz = (int)(geo & 0xFFFFu), o = (int)(geo >> 16);
-            const int dy = r - o;
-            if ((unsigned)dy >= (unsigned)sz || lx0 + kRenderPx <= o || lx0 >= o + sz) continue;
-            const uint32_t* spr = atlas + dl_off[tx][d] + dy * sz;
-#pragma unroll
-            for (int k = 0; k < kRenderPx; ++k) {
-                const int dx = lx0 + k - o;
-                if ((unsigned)dx < (unsigned)sz) p[k] = sdl_blend(p[k], spr[dx]);
+            for (int q = 0; q < kRenderPx / 4; ++q) {
+                const u32x4 v = bsrc[q];
+                p[4 * q] = v.x;
+                p[4 * q + 1] = v.y;
+                p[4 * q + 2] = v.z;
+                p[4 * q + 3] = v.w;
             }
-        }
-        // 16 pixels -> 48 bytes: per 4 pixels three dwords of packed 3-byte pixels
-        u32x4* dst = (u32x4*)(img + ((int64_t)py * row_px + px0) * 3);
-        uint32_t w[12];
+            const int tx = px0 / tile, lx0 = px0 - tx * tile;  // a group never straddles two cells
+            const int n = dl_n[tx];
+            for (int d = 0; d < n; ++d) {
+                const uint32_t geo = dl_geo[tx][d];
+                const int sz = (int)(geo & 0xFFFFu), o = (int)(geo >> 16);
+                const int dy = r - o;
+                if ((unsigned)dy >= (unsigned)sz || lx0 + kRenderPx <= o || lx0 >= o + sz) continue;
+                const uint32_t* spr = atlas + dl_off[tx][d] + dy * sz;
 #pragma unroll
-        for (int q = 0; q < kRenderPx / 4; ++q) {
-            const uint32_t a0 = __builtin_amdgcn_perm(0u, p[4 * q], psel), a1 = __builtin_amdgcn_perm(0u, p[4 * q + 1], psel),
-                           a2 = __builtin_amdgcn_perm(0u, p[4 * q + 2], psel), a3 = __builtin_amdgcn_perm(0u, p[4 * q + 3], psel);
-            w[3 * q] = a0 | (a1 << 24);
-            w[3 * q + 1] = (a1 >> 8) | (a2 << 16);
-            w[3 * q + 2] = (a2 >> 16) | (a3 << 8);
+                for (int k = 0; k < kRenderPx; ++k) {
+                    const int dx = lx0 + k - o;
+                    if ((unsigned)dx < (unsigned)sz) p[k] = sdl_blend(p[k], spr[dx]);
+                }
+            }
+            // 16 pixels -> 48 bytes: per 4 pixels three dwords of packed 3-byte pixels
+            uint32_t w[12];
+#pragma unroll
+            for (int q = 0; q < kRenderPx / 4; ++q) {
+                const uint32_t a0 = __builtin_amdgcn_perm(0u, p[4 * q], psel),
+                               a1 = __builtin_amdgcn_perm(0u, p[4 * q + 1], psel),
+                               a2 = __builtin_amdgcn_perm(0u, p[4 * q + 2], psel),
+                               a3 = __builtin_amdgcn_perm(0u, p[4 * q + 3], psel);
+                w[3 * q] = a0 | (a1 << 24);
+                w[3 * q + 1] = (a1 >> 8) | (a2 << 16);
+                w[3 * q + 2] = (a2 >> 16) | (a3 << 8);
+            }
+#pragma unroll
+            for (int q = 0; q < 3; ++q) stage[wave][3 * lane + q] = u32x4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
         }
+        __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave; keep the compiler from moving reads up
+        const int w0 = base + wave * 64;  // the wave's first group
+        const int nbytes = 48 * (items - w0 < 64 ? (items - w0 > 0 ? items - w0 : 0) : 64);
+        u32x4* dst = (u32x4*)(blk_out + (int64_t)w0 * 48);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            const u32x4 v = {w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
-            __builtin_nontemporal_store(v, dst + q);  // streamed once: keep L2 for the level image and sprites
+            const int off = q * 64 + lane;  // 16-byte units
+            if (off * 16 < nbytes) __builtin_nontemporal_store(stage[wave][off], dst + off);
         }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
