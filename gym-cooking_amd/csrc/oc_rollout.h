@@ -17,7 +17,10 @@
 
 #include <stdint.h>
 
-#define OC_RH __host__ __device__ inline
+// Every row function is force-inlined: a GPU call spills the caller's live registers to
+// scratch (the bound walk was being emitted as s_swappc calls with ~100 B of scratch per lane).
+#define OC_RH __host__ __device__ inline __attribute__((always_inline))
+#define OC_RL __attribute__((always_inline))
 
 namespace ocro {
 
@@ -334,18 +337,18 @@ struct RowOps {
 #pragma unroll
         for (int a = 0; a < A; ++a)
             if (r.ah(a) != kNone) held |= 1u << r.ah(a);
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const int c = r.il(j);
-            if (c == kNone || r.im(j) != m || ((held >> j) & 1u)) continue;
-            if (skip_deliv && ((L.deliv_cells >> c) & 1u)) continue;
-            f(c);
-        }
-#pragma unroll
-        for (int a = 0; a < A; ++a) {
-            const int h = r.ah(a);
-            if (!((active >> a) & 1u) || h == kNone || r.im(h) != m) continue;
-            const int c = agent_cell(r, a);
+        // one rolled loop with one call site: f (a bound walk) is inlined once, not K + A times
+#pragma unroll 1
+        for (int k = 0; k < K + A; ++k) {
+            int c;
+            if (k < K) {
+                c = r.il(k);
+                if (c == kNone || r.im(k) != m || ((held >> k) & 1u)) continue;
+            } else {
+                const int a = k - K, h = r.ah(a);
+                if (!((active >> a) & 1u) || h == kNone || r.im(h) != m) continue;
+                c = agent_cell(r, a);
+            }
             if (skip_deliv && ((L.deliv_cells >> c) & 1u)) continue;
             f(c);
         }
@@ -374,15 +377,15 @@ struct RowOps {
         float lower = (float)L.perimeter + 1.0f;
         if (s.kind == 1 || s.kind == 3) {
             const uint64_t bset = s.kind == 1 ? L.cut_cells : L.deliv_cells;
-            visit_objs(r, s.start[0], s.kind == 3, [&](int Ac) {
+            visit_objs(r, s.start[0], s.kind == 3, [&](int Ac) OC_RL {
                 for (uint64_t m = bset; m; m &= m - 1) {
                     const float b = helper(s, ag0, ag1, Ac, __builtin_ctzll(m));
                     if (b < lower) lower = b;
                 }
             });
         } else if (s.kind == 2) {
-            visit_objs(r, s.start[0], false, [&](int Ac) {
-                visit_objs(r, s.start[1], false, [&](int Bc) {
+            visit_objs(r, s.start[0], false, [&](int Ac) OC_RL {
+                visit_objs(r, s.start[1], false, [&](int Bc) OC_RL {
                     const float b = helper(s, ag0, ag1, Ac, Bc);
                     if (b < lower) lower = b;
                 });
@@ -475,8 +478,12 @@ struct RowOps {
         // pass 1: max of beta * (old_q - Q) over the valid actions; pass 2: softmax sum
         double m = -1.0e300, S = 0.0, xt = 0.0;
         bool found = false;
+        // kept rolled: each candidate is a whole rollout (interact + goal + bound walk)
+#pragma unroll 1
         for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll 1
             for (int a0 = 0; a0 < 5; ++a0)
+#pragma unroll 1
                 for (int a1 = 0; a1 < (s.n == 2 ? 5 : 1); ++a1) {
                     const int c1 = s.n == 2 ? a1 : kNoop;
                     if (!action_legal(r, s, a0, c1)) continue;
