@@ -217,6 +217,39 @@ def load_traffic(path: str, kernel: str = "oc_step_n_kernel"):
         return None, None
 
 
+def measure_c3(dev, world, B: int = 1 << 20, n: int = 100) -> dict:
+    """Secondary line, config C3: 3-agent full-divider_tl (the collision-heavy path), 2^20 envs
+    per GPU, one oc_step_n launch of n steps with every step's outputs written."""
+    from gym_cooking_amd.engine import OvercookedBatch
+    eb = OvercookedBatch("full-divider_tl", 3, B, max_T=100, device=dev)
+    P, A, S = eb.pitch, eb.A, eb.layout.state_bytes
+    acts = torch.empty((n, A * P), dtype=torch.uint8, device=dev)
+    for i in range(n):
+        eb.gen_actions(acts[i], step=i, seed=3)
+    traj = torch.empty(n * S, dtype=torch.uint8, device=dev)
+    ex, coll = torch.empty(n * A * P, dtype=torch.uint8, device=dev), torch.empty(n * P, dtype=torch.uint8, device=dev)
+    s, s2, stats = eb.new_state(), eb.new_state(), eb.new_stats()
+    eb.reset(s)
+    eb.step_n(s, s2, acts.reshape(-1), n, traj, ex, coll, stats)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    eb.reset(s)
+    stats.zero_()
+    e0.record()
+    eb.step_n(s, s2, acts.reshape(-1), n, traj, ex, coll, stats)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) * 1e-3, dev) * 1e3
+    tot = eb.reduce_stats(stats).cpu().tolist()
+    nS = eb.layout.num_planes
+    bytes_step = (nS + n * (nS + 2 * A + 1)) / n
+    return {"value": world * B * n / (ms * 1e-3), "unit": "env-steps/s", "envs_per_gpu": B, "steps": n,
+            "ms_per_step": ms / n, "kernel": "oc_step_n_kernel<3,4>", "algorithmic_bytes_per_env_step": bytes_step,
+            "achieved_GBs": bytes_step * B * n / (ms * 1e-3) / 1e9,
+            "frac_hbm": bytes_step * B * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "collision_pairs": int(tot[3]), "workload": "C3: full-divider_tl, 3 agents, random actions"}
+
+
 def per_step_launch(eb, acts, n_act, W, dev, world, use_graph=True) -> dict:
     """Secondary line: one oc_step launch per step, K steps replayed from a hipGraph (or eager),
     ping-pong state buffers; kernel duration = event window / K on the launch stream."""
@@ -277,6 +310,7 @@ def main() -> int:
     ap.add_argument("--no-per-step", action="store_true", help="skip the secondary one-launch-per-step line")
     ap.add_argument("--no-rollout", action="store_true", help="skip the secondary oc_rollout (C5) measurement")
     ap.add_argument("--no-render", action="store_true", help="skip the secondary oc_render measurement")
+    ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 (3-agent full-divider_tl) line")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -397,6 +431,8 @@ def main() -> int:
         line["rollout"] = measure_rollout(dev, world)
     if not args.no_render:
         line["render"] = measure_render(dev, world, args.level, args.agents)
+    if not args.no_c3:
+        line["c3"] = measure_c3(dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget, threads)

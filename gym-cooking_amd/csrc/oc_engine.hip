@@ -92,8 +92,9 @@ struct Bufs {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
+template <int CP = 0>
 __device__ __forceinline__ uint32_t bld32(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0);
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, CP);
 }
 // Store cache policy (gfx950 CPol bits of the buffer intrinsics): 0 plain, 2 nt, 16 sc1,
 // 17 sc0 sc1.  sc1 stores leave no dirty line in the XCD's L2, so the bytes go out to HBM
@@ -240,7 +241,7 @@ __global__ __launch_bounds__(kStepBlock) void oc_step_kernel(LevelArgs L, const 
 // and writes the step's outputs: the full state into traj[r] (when given), the executed
 // actions and the collision mask; the state after the last step goes to sout.  Outputs are
 // byte-identical to n oc_step launches with ping-pong buffers.
-template <int A, int K, int CP = 0>
+template <int A, int K, int CP = 0, int LCP = 0>
 __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
                                                            uint8_t* __restrict__ sout,
                                                            const uint8_t* __restrict__ actions,
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
         const int64_t rem = L.B - (int64_t)g * kEPL;
         const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (rem <= 0 ? 0u : (1u << (8 * (uint32_t)rem)) - 1u);
 #pragma unroll
-        for (int a = 0; a < A; ++a) nxt[a] = n > 1 ? bld32(b.act, vo, (uint32_t)(A + a) * P) : 0u;
+        for (int a = 0; a < A; ++a) nxt[a] = n > 1 ? bld32<LCP>(b.act, vo, (uint32_t)(A + a) * P) : 0u;
         for (int r = 0; r < n; ++r) {
             uint32_t act[A], ex[A], cm;
 #pragma unroll
@@ -286,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
             }
             if (r + 2 < n) {
 #pragma unroll
-                for (int a = 0; a < A; ++a) nxt[a] = bld32(b.act, vo, (uint32_t)((r + 2) * A + a) * P);
+                for (int a = 0; a < A; ++a) nxt[a] = bld32<LCP>(b.act, vo, (uint32_t)((r + 2) * A + a) * P);
             }
             const uint32_t f_in = c.wf;
             ocsw::step4<A, K>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, act, ex, cm, cls_of);

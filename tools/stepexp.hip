@@ -246,21 +246,39 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((step_flat<2, 4, CH, BS, __VA_ARGS__>), dim3(nl / CH / BS), dim3(BS), 0, s, L, i, o, a, ex, coll, stats); \
     })
     ref.clear();
-    FLATX("MEMONLY sc1    block 128", 1, 128, 1, 0, true, 16);
+    // oc_step_n cache policies: 2 launches x 100 steps, trajectory written (the bench headline)
     {
-        const int nw = (int)(nl / 64);
-        uint64_t* tl;
-        CK(hipMalloc(&tl, (size_t)nw * 5 * 8));
-        std::vector<uint64_t> host((size_t)nw * 5);
-#define TL(NAME, BS, MO)                                                                                         \
-        for (int rep = 0; rep < 3; ++rep) {                                                                      \
-            hipLaunchKernelGGL((step_timeline<2, 4, BS, MO>), dim3(nl / BS), dim3(BS), 0, s, L, sa, sb, act, ex, coll, tl); \
-            CK(hipStreamSynchronize(s));                                                                         \
-        }                                                                                                        \
-        CK(hipMemcpy(host.data(), tl, host.size() * 8, hipMemcpyDeviceToHost));                                  \
-        timeline_report(NAME, host, nw);
-        TL("timeline step sc1 128", 128, false);
-        TL("timeline memonly sc1 128", 128, true);
+        uint8_t* traj;
+        uint8_t *exn, *colln;
+        CK(hipMalloc(&traj, (int64_t)R * NP * P));
+        CK(hipMalloc(&exn, (int64_t)R * A * P));
+        CK(hipMalloc(&colln, (int64_t)R * P));
+        const int64_t need = P / kEnvsPerBlock, cap = (int64_t)kCUs * 5;
+        const dim3 grid((unsigned)(need < cap ? need : cap));
+        auto stepn = [&](auto kern, const char* name) {
+            float best = 1e30f;
+            for (int rep = 0; rep < 6; ++rep) {
+                oc_reset(h, sa, B, s);
+                CK(hipEventRecord(e0, s));
+                hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, sa, sb, act, traj, exn, colln, stats, R);
+                hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, sb, sa, act, traj, exn, colln, stats, R);
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (rep > 0 && ms < best) best = ms;
+            }
+            const double us = best * 1000.0 / (2 * R);
+            printf("%-40s %7.2f us/step  %6.2f TB/s alg (22.17 B/env-step)\n", name, us, 22.17 * B / us / 1e6);
+        };
+        stepn(oc_step_n_kernel<2, 4, 2, 0>, "step_n nt stores (product)");
+        stepn(oc_step_n_kernel<2, 4, 2, 2>, "step_n nt stores, nt action loads");
+        stepn(oc_step_n_kernel<2, 4, 2, 16>, "step_n nt stores, sc1 action loads");
+        stepn(oc_step_n_kernel<2, 4, 2, 17>, "step_n nt stores, sc0 sc1 action loads");
+        stepn(oc_step_n_kernel<2, 4, 2, 0>, "step_n nt stores (product)");
+        stepn(oc_step_n_kernel<2, 4, 2, 2>, "step_n nt stores, nt action loads");
+        stepn(oc_step_n_kernel<2, 4, 3, 0>, "step_n nt+sc0 stores");
+        stepn(oc_step_n_kernel<2, 4, 18, 0>, "step_n nt+sc1 stores");
     }
     return 0;
 }
