@@ -217,6 +217,35 @@ def load_traffic(path: str, kernel: str = "oc_step_n_kernel"):
         return None, None
 
 
+def measure_planner(dev, world) -> dict:
+    """Secondary line: the engine-backed navigation planner (gym_cooking_amd.planner.E2E_BRTDP,
+    Level 0, main.py's default hyper-parameters) on C1's level: one get_next_action call from
+    the reset state for Chop(Tomato) by agent-1 alone and by both agents jointly (np.random
+    seeded 1).  The reference planner takes 0.31 s and 13.2 s for these two calls on the
+    survey container's CPU."""
+    import numpy as np
+    from gym_cooking_amd import envs, recipes
+    from gym_cooking_amd.planner import E2E_BRTDP
+    env = envs.OvercookedEnvironment(level="open-divider_salad", num_agents=2, device=dev)
+    env.reset()
+    out = {}
+    for tag, agn in (("single", ("agent-1",)), ("joint", ("agent-1", "agent-2"))):
+        best = None
+        for rep in range(3):
+            p = E2E_BRTDP(alpha=0.01, tau=2, cap=75, main_cap=100, device=dev)
+            np.random.seed(1)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            a = p.get_next_action(env, recipes.Chop("Tomato"), agn, {})
+            dt = time.perf_counter() - t0
+            if best is None or dt < best[0]:
+                best = (dt, a, len(p.v_l), p._exp.launches)
+        out[tag] = {"ms_per_call": best[0] * 1e3, "action": list(best[1]), "states": best[2],
+                    "rollout_launches": best[3]}
+    out["workload"] = "C1 level open-divider_salad, reset state, Chop(Tomato), alpha 0.01 tau 2 cap 75 main_cap 100"
+    return out
+
+
 def measure_c3(dev, world, B: int = 1 << 20, n: int = 100) -> dict:
     """Secondary line, config C3: 3-agent full-divider_tl (the collision-heavy path), 2^20 envs
     per GPU, one oc_step_n launch of n steps with every step's outputs written."""
@@ -311,6 +340,7 @@ def main() -> int:
     ap.add_argument("--no-rollout", action="store_true", help="skip the secondary oc_rollout (C5) measurement")
     ap.add_argument("--no-render", action="store_true", help="skip the secondary oc_render measurement")
     ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 (3-agent full-divider_tl) line")
+    ap.add_argument("--no-planner", action="store_true", help="skip the secondary navigation-planner line")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -433,6 +463,8 @@ def main() -> int:
         line["render"] = measure_render(dev, world, args.level, args.agents)
     if not args.no_c3:
         line["c3"] = measure_c3(dev, world)
+    if not args.no_planner:
+        line["planner"] = measure_planner(dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget, threads)

@@ -1,0 +1,83 @@
+"""The engine-backed navigation planner (gym_cooking_amd.planner.E2E_BRTDP, Level 0) against
+the reference planner's own decisions (tests/golden/brtdp.json, gen_brtdp.py): for every
+recorded get_next_action call -- fresh planners, and planners kept across an episode's calls
+-- the same returned action, the same cur_obj_count, bit-identical v_l / v_u of the start
+state, and the same number of states initialised (so the search explored exactly the
+reference's states and drew exactly its random numbers)."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oc_testlib as tl
+from gym_cooking_amd import capi, recipes
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+_STATIC = {"Counter", "Floor", "Delivery", "Cutboard"}
+_NAV = [(0, 1), (0, -1), (-1, 0), (1, 0), (0, 0)]
+
+
+def _fixture():
+    with open(os.path.join(tl.GOLDEN, "brtdp.json")) as f:
+        return json.load(f)
+
+
+def _subtask(text):
+    m = re.fullmatch(r"(\w+)\((.*)\)", text)
+    cls = {"Chop": recipes.Chop, "Merge": recipes.Merge, "Deliver": recipes.Deliver}[m.group(1)]
+    return cls(*[a.strip() for a in m.group(2).split(",")])
+
+
+def _env_at(level, A, call, cache={}):
+    from gym_cooking_amd import envs
+    key = (level, A)
+    if key not in cache:
+        e = envs.OvercookedEnvironment(level=level, num_agents=A)
+        e.reset()
+        cache[key] = e
+    env = cache[key]
+    lv = env.level
+    K = capi.item_slots(lv)
+    P = capi.pitch_for(1)
+    s = tl.state_from_canonical(lv, A, K, P, np.array([call["agents"]], np.uint8),
+                                np.array([call["items"]], np.uint8), np.array([call["env_t"]]))
+    env.load_state(tl.env_view(s, A, K, P, 1)[:, 0])
+    env._group_names = frozenset(g for g in call["groups"] if g not in _STATIC)
+    return env
+
+
+@pytest.mark.parametrize("mode", ["fresh", "chain"])
+def test_planner_matches_reference_calls(mode):
+    from gym_cooking_amd.planner import E2E_BRTDP
+    fx = _fixture()
+    params = fx["params"]
+    chains, errs, n = {}, [], 0
+    for i, c in enumerate(fx["calls"]):
+        if c["mode"] != mode:
+            continue
+        cfg = fx["configs"][c["cfg"]]
+        env = _env_at(cfg["level"], cfg["A"], c)
+        names = env.get_agent_names()
+        agn = tuple(names[a] for a in c["sub_agents"])
+        if mode == "fresh":
+            p = E2E_BRTDP(**params)
+        else:
+            p = chains.setdefault((c["cfg"], c["episode"], c["subtask"], agn), E2E_BRTDP(**params))
+        np.random.seed(c["seed"])
+        action = p.get_next_action(env=env, subtask=_subtask(c["subtask"]), subtask_agent_names=agn,
+                                   other_agent_planners={})
+        exp = None if c["action"] is None else (_NAV[c["action"][0]] if len(c["action"]) == 1
+                                                else tuple(_NAV[k] for k in c["action"]))
+        v_l, v_u = p.start_values()
+        got = (action, p.cur_obj_count, v_l, v_u, len(p.v_l))
+        want = (exp, c["goal_count"], c["v_l"], c["v_u"], c["n_states"])
+        if got != want:
+            errs.append("call %d (%s, %s %s, seed %d): got %s want %s" % (i, cfg["level"], c["subtask"], agn,
+                                                                      c["seed"], got, want))
+        n += 1
+    assert n > 0
+    assert not errs, "%d of %d calls differ:\n%s" % (len(errs), n, "\n".join(errs[:15]))

@@ -1,0 +1,91 @@
+"""CPU check of the engine-backed navigation planner's host search
+(gym_cooking_amd.planner.E2E_BRTDP: get_next_action / main / runSampleTrial / backups /
+argmin tie-breaks) against the reference planner's recorded decisions
+(tests/golden/brtdp.json), with the CPU oracle's rollout rows standing in for the oc_rollout
+launches (TEST INFRASTRUCTURE: the product planner always expands on the GPU).  The same
+calls run through the HIP engine in tests/test_planner_gpu.py."""
+import json
+import os
+import types
+
+import numpy as np
+import pytest
+
+import oc_testlib as tl
+import test_planner_gpu as tg
+from gym_cooking_amd import capi, envs, levels
+
+from oracle import oracle
+
+
+class OracleExpander:
+    ROWS = 32
+
+    def __init__(self, level, num_agents, device):
+        self.ob = oracle.OracleBatch(level, num_agents, 0, self.ROWS)
+        self.A, self.K = num_agents, self.ob.K
+        P = capi.layout_planes(num_agents, self.K)
+        self.NP, self.t_plane, self.P = P["num_planes"], P["t"], self.ob.pitch
+        self.launches = 0
+
+    def rows(self, state, codes, sub):
+        n = len(codes)
+        sin = np.zeros((self.NP, self.P), np.uint8)
+        sin[:, :n] = state[:, None]
+        sin[self.t_plane:, :] = 0
+        act = np.full((self.A, self.P), 4, np.uint8)
+        for r, c in enumerate(codes):
+            for q in range(sub.num_agents):
+                act[sub.agent[q], r] = c[q]
+        sout = np.zeros_like(sin)
+        fl, lb = self.ob.rollout(sin.reshape(-1), sout.reshape(-1), act.reshape(-1), [sub], None, nthreads=1)
+        self.launches += 1
+        nxt = sout[:, :n].T.copy()
+        nxt[:, self.t_plane:] = 0
+        return nxt, fl[:n], lb[:n]
+
+
+def _env(level_name, A, call):
+    lv = levels.load_level(level_name)
+    K = capi.item_slots(lv)
+    P = capi.pitch_for(1)
+    s = tl.state_from_canonical(lv, A, K, P, np.array([call["agents"]], np.uint8),
+                                np.array([call["items"]], np.uint8), np.array([call["env_t"]]))
+    b = tl.env_view(s, A, K, P, 1)[:, 0].copy()
+    agents, world, _, _ = envs.build_views(lv, A, K, b)
+    return types.SimpleNamespace(level=lv, _device="cpu", state_bytes=lambda: b.copy(),
+                                 _group_names=frozenset(g for g in call["groups"] if g not in tg._STATIC),
+                                 world=world, get_agent_names=lambda: [a.name for a in agents])
+
+
+@pytest.mark.parametrize("mode", ["fresh", "chain"])
+def test_host_planner_matches_reference_calls(mode):
+    from gym_cooking_amd.planner import E2E_BRTDP
+    fx = tg._fixture()
+    params = fx["params"]
+    chains, errs, n = {}, [], 0
+    for i, c in enumerate(fx["calls"]):
+        if c["mode"] != mode:
+            continue
+        cfg = fx["configs"][c["cfg"]]
+        env = _env(cfg["level"], cfg["A"], c)
+        names = env.get_agent_names()
+        agn = tuple(names[a] for a in c["sub_agents"])
+        if mode == "fresh":
+            p = E2E_BRTDP(**params, expander=OracleExpander)
+        else:
+            p = chains.setdefault((c["cfg"], c["episode"], c["subtask"], agn), E2E_BRTDP(**params, expander=OracleExpander))
+        np.random.seed(c["seed"])
+        action = p.get_next_action(env=env, subtask=tg._subtask(c["subtask"]), subtask_agent_names=agn,
+                                   other_agent_planners={})
+        exp = None if c["action"] is None else (tg._NAV[c["action"][0]] if len(c["action"]) == 1
+                                                else tuple(tg._NAV[k] for k in c["action"]))
+        v_l, v_u = p.start_values()
+        got = (action, p.cur_obj_count, v_l, v_u, len(p.v_l))
+        want = (exp, c["goal_count"], c["v_l"], c["v_u"], c["n_states"])
+        if got != want:
+            errs.append("call %d (%s, %s %s, seed %d): got %s want %s" % (i, cfg["level"], c["subtask"], agn,
+                                                                      c["seed"], got, want))
+        n += 1
+    assert n > 0
+    assert not errs, "%d of %d calls differ:\n%s" % (len(errs), n, "\n".join(errs[:15]))
