@@ -243,7 +243,44 @@ def measure_planner(dev, world) -> dict:
         out[tag] = {"ms_per_call": best[0] * 1e3, "action": list(best[1]), "states": best[2],
                     "rollout_launches": best[3]}
     out["workload"] = "C1 level open-divider_salad, reset state, Chop(Tomato), alpha 0.01 tau 2 cap 75 main_cap 100"
+    out["batch"] = measure_plan_batch(dev)
     return out
+
+
+def measure_plan_batch(dev, B: int = 1024, steps: int = 12) -> dict:
+    """plan_batch: B independent Level-0 searches (Chop(Tomato) by agent-1 on C1's level) from
+    the states of B random-play envs after `steps` steps, each with its own RandomState; the
+    searches share oc_rollout launches."""
+    import numpy as np
+    from gym_cooking_amd.engine import OvercookedBatch
+    from gym_cooking_amd import recipes
+    from gym_cooking_amd.planner import E2E_BRTDP, PlanEnv, plan_batch
+    eb = OvercookedBatch("open-divider_salad", 2, B, max_T=0, device=dev)
+    s, s2, a = eb.new_state(), eb.new_state(), eb.new_actions()
+    eb.reset(s)
+    for t in range(steps):
+        eb.gen_actions(a, t, 21)
+        eb.step(s, s2, a)
+        s, s2 = s2, s
+    NP, P, tp = eb.layout.num_planes, eb.pitch, eb.layout.plane_t
+    host = s.view(NP, P).cpu().numpy()
+    tv = host[tp:tp + 2].reshape(-1).view(np.uint16)
+    names = ["Tomato", "Lettuce", "Plate"]
+    envs_, planners = [], []
+    for b in range(B):
+        by = host[:, b].copy()
+        by[tp], by[tp + 1] = tv[b] & 0xFF, tv[b] >> 8
+        envs_.append(PlanEnv(eb.level, 2, by, names, device=dev))
+        planners.append(E2E_BRTDP(alpha=0.01, tau=2, cap=75, main_cap=100, device=dev, rng=np.random.RandomState(b)))
+    sub = recipes.Chop("Tomato")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    acts = plan_batch(planners, envs_, [sub] * B, [("agent-1",)] * B)
+    dt = time.perf_counter() - t0
+    exp = planners[0]._exp
+    return {"searches": B, "seconds": dt, "plans_per_s": B / dt, "launches": exp.launches, "rows": exp.rows_done,
+            "states_initialised": int(sum(len(p.v_l) for p in planners)), "none_actions": sum(x is None for x in acts),
+            "workload": "B random-play states of open-divider_salad after %d steps, Chop(Tomato) by agent-1" % steps}
 
 
 def measure_c3(dev, world, B: int = 1 << 20, n: int = 100) -> dict:

@@ -26,6 +26,7 @@ moves with their own planners; it is not restated here and raises ``NotImplement
 from __future__ import annotations
 
 import itertools
+import types
 from typing import Dict, FrozenSet, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -50,18 +51,35 @@ def _group_name(mask: int) -> str:
     return n
 
 
-def argmin(vector):
+_CAND = {n: list(itertools.product(range(5), repeat=n)) for n in (1, 2)}
+
+
+def _cost(action) -> float:  # E2E_BRTDP.cost (e2e_brtdp.py:816-826): 1.0, + 0.1 per moving agent, in order
+    cost = 1.0
+    for a in action:
+        if a != _NOOP:
+            cost += 0.1
+    return cost
+
+
+_COST = {c: _cost(c) for n in (1, 2) for c in _CAND[n]}
+
+
+def argmin(vector, rng=np.random):
     """e2e_brtdp.py:27-30: the index of a minimum, ties broken by numpy's global generator
-    (one ``np.random.multinomial`` draw per call, ties or not)."""
+    (one ``multinomial`` draw per call, ties or not).  `rng` is the module ``np.random`` (the
+    reference's generator) or a ``np.random.RandomState`` of a batched search."""
     e_x = np.array(vector) == min(vector)
-    return np.where(np.random.multinomial(1, e_x / e_x.sum()))[0][0]
+    return np.where(rng.multinomial(1, e_x / e_x.sum()))[0][0]
 
 
 class _Expander:
-    """One engine batch of ROWS rows for a level: expands a state for all its joint actions in
-    one oc_rollout launch."""
+    """An engine batch of up to ROWS rollout rows for a level.  ``run(requests)`` evaluates
+    any number of expansion requests -- (state bytes, joint actions, subtask configuration) --
+    in as few oc_rollout launches as the row and configuration limits allow (one, for up to
+    ROWS rows and 64 distinct configurations)."""
 
-    ROWS = 32  # >= 25 joint actions
+    ROWS = 4096
 
     def __init__(self, level, num_agents: int, device):
         from .engine import OvercookedBatch  # raises without liboc_engine.so / a GPU
@@ -73,41 +91,78 @@ class _Expander:
         self.s_in = self.eb.new_state()
         self.s_out = self.eb.new_state()
         self.act = self.eb.new_actions()
+        self.alloc = torch.empty(self.P, dtype=torch.uint8, device=dev)
         self.flags = torch.empty(self.P, dtype=torch.uint8, device=dev)
         self.lb = torch.empty(self.P, dtype=torch.float32, device=dev)
-        self._host_in = torch.empty((self.NP, self.ROWS), dtype=torch.uint8).pin_memory()
-        self._host_act = torch.empty((self.A, self.ROWS), dtype=torch.uint8).pin_memory()
-        self._host_out = torch.empty((self.NP, self.ROWS), dtype=torch.uint8).pin_memory()
-        self._host_fl = torch.empty(self.ROWS, dtype=torch.uint8).pin_memory()
-        self._host_lb = torch.empty(self.ROWS, dtype=torch.float32).pin_memory()
+
+        def pin(*shape, dt=torch.uint8):
+            return torch.empty(shape, dtype=dt).pin_memory()
+
+        self._h_in, self._h_act, self._h_alloc = pin(self.NP, self.ROWS), pin(self.A, self.ROWS), pin(self.ROWS)
+        self._h_out, self._h_fl, self._h_lb = pin(self.NP, self.ROWS), pin(self.ROWS), pin(self.ROWS, dt=torch.float32)
         self.launches = 0
+        self.rows_done = 0
 
     def rows(self, state: np.ndarray, codes: Sequence[Tuple[int, ...]], sub: capi.OcSubtask):
-        """Rollout rows of `state` (engine bytes, env_view order) under `sub` for each joint
-        action in `codes` (tuples of the subtask agents' codes).  Returns (next states
-        [n, NP] u8, flags [n], lower bounds [n])."""
-        n = len(codes)
-        assert 0 < n <= self.ROWS
-        hi = self._host_in.numpy()
-        hi[:, :] = state[:, None]
-        hi[self.t_plane:, :] = 0  # t and flags: copied through by the kernel, not part of a planner state
-        ha = self._host_act.numpy()
-        ha[:, :] = _NOOP
-        for r, c in enumerate(codes):
-            for q, a in enumerate(sub.agent[:sub.num_agents]):
-                ha[a, r] = c[q]
-        self.s_in.view(self.NP, self.P)[:, :self.ROWS].copy_(self._host_in, non_blocking=True)
-        self.act.view(self.A, self.P)[:, :self.ROWS].copy_(self._host_act, non_blocking=True)
-        self.eb.rollout(self.s_in, self.s_out, self.act, [sub], None, self.flags, self.lb)
+        """One request: (next states [n, NP], flags [n], lower bounds [n])."""
+        return self.run([(state, codes, sub)])[0]
+
+    def run(self, requests):
+        out, chunk, nrows, subs = [], [], 0, {}
+        for req in requests:
+            n = len(req[1])
+            key = bytes(req[2])
+            if chunk and (nrows + n > self.ROWS or (key not in subs and len(subs) == capi.MAX_SUBTASKS)):
+                out += self._launch(chunk, subs)
+                chunk, nrows, subs = [], 0, {}
+            subs.setdefault(key, (len(subs), req[2]))
+            chunk.append(req)
+            nrows += n
+        if chunk:
+            out += self._launch(chunk, subs)
+        return out
+
+    def _launch(self, reqs, subs):
+        hi, ha, hal = self._h_in.numpy(), self._h_act.numpy(), self._h_alloc.numpy()
+        r0, spans = 0, []
+        for state, codes, sub in reqs:
+            n = len(codes)
+            hi[:, r0:r0 + n] = state[:, None]
+            ha[:, r0:r0 + n] = _NOOP
+            for r, c in enumerate(codes):
+                for q in range(sub.num_agents):
+                    ha[sub.agent[q], r0 + r] = c[q]
+            hal[r0:r0 + n] = subs[bytes(sub)][0]
+            spans.append((r0, n))
+            r0 += n
+        n = r0
+        hi[self.t_plane:, :n] = 0  # t and flags: copied through by the kernel, not part of a planner state
+        table = [sub for _, sub in sorted(subs.values(), key=lambda v: v[0])]
+        self.s_in.view(self.NP, self.P)[:, :n].copy_(self._h_in[:, :n], non_blocking=True)
+        self.act.view(self.A, self.P)[:, :n].copy_(self._h_act[:, :n], non_blocking=True)
+        self.alloc[:n].copy_(self._h_alloc[:n], non_blocking=True)
+        lib, eb = self.eb.lib, self.eb
+        capi.check(lib.oc_rollout(eb._h, _ptr(self.s_in), _ptr(self.s_out), _ptr(self.act), _ptr(self.alloc),
+                                  capi.subtask_array(table), len(table), _ptr(self.flags), _ptr(self.lb), n,
+                                  eb._stream()))
         self.launches += 1
-        # three async copies into pinned memory, one wait
-        self._host_out.copy_(self.s_out.view(self.NP, self.P)[:, :self.ROWS], non_blocking=True)
-        self._host_fl.copy_(self.flags[:self.ROWS], non_blocking=True)
-        self._host_lb.copy_(self.lb[:self.ROWS], non_blocking=True)
-        torch.cuda.current_stream(self.eb.device).synchronize()
-        nxt = self._host_out.numpy()[:, :n].T.copy()
-        nxt[:, self.t_plane:] = 0
-        return nxt, self._host_fl.numpy()[:n].copy(), self._host_lb.numpy()[:n].copy()
+        self.rows_done += n
+        self._h_out[:, :n].copy_(self.s_out.view(self.NP, self.P)[:, :n], non_blocking=True)
+        self._h_fl[:n].copy_(self.flags[:n], non_blocking=True)
+        self._h_lb[:n].copy_(self.lb[:n], non_blocking=True)
+        torch.cuda.current_stream(eb.device).synchronize()
+        ho, hf, hl = self._h_out.numpy(), self._h_fl.numpy(), self._h_lb.numpy()
+        res = []
+        for r0, n in spans:
+            nxt = ho[:, r0:r0 + n].T.copy()
+            nxt[:, self.t_plane:] = 0
+            res.append((nxt, hf[r0:r0 + n].copy(), hl[r0:r0 + n].copy()))
+        return res
+
+
+def _ptr(t):
+    import ctypes
+    return ctypes.c_void_p(t.data_ptr())
 
 
 class E2E_BRTDP:
@@ -117,14 +172,20 @@ class E2E_BRTDP:
     other_agent_planners)``, same value tables ``v_l`` / ``v_u`` (keyed by (state, subtask)),
     ``cur_state``, ``cur_obj_count``, ``is_joint``.  ``env`` is the engine-backed
     :class:`gym_cooking_amd.envs.OvercookedEnvironment`.
+
+    The search is written as a generator that yields an expansion request whenever it meets a
+    state it has not expanded; :meth:`get_next_action` serves each request with its own launch,
+    :func:`plan_batch` serves the requests of many searches with shared launches.
     """
 
-    def __init__(self, alpha, tau, cap, main_cap, device: Optional[str] = None, expander=None):
+    def __init__(self, alpha, tau, cap, main_cap, device: Optional[str] = None, expander=None, rng=None):
         """`expander(level, num_agents, device)` builds the row evaluator; the default is the
         HIP engine (``oc_rollout``).  Tests pass the CPU oracle's rollout here to check the
-        host search without a GPU."""
+        host search without a GPU.  `rng`: the tie-breaking generator (default numpy's global
+        one, as the reference)."""
         self.alpha, self.tau, self.cap, self.main_cap = alpha, tau, cap, main_cap
         self._make_expander = expander or _Expander
+        self._rng = rng if rng is not None else np.random
         self.v_l: Dict = {}
         self.v_u: Dict = {}
         self.time_cost = 1.0
@@ -132,13 +193,12 @@ class E2E_BRTDP:
         self.is_joint = False
         self.subtask = None
         self.device = device
-        self._exp: Optional[_Expander] = None
+        self._exp = None
         self._exp_key = None
-        self._succ: Dict = {}  # (state key, subtask key) -> (actions, [(next key, next state)])
-        self._states: Dict = {}  # state key -> (bytes, groups)
+        self._succ: Dict = {}  # (state key, subtask key) -> (actions, successors, costs, value keys)
 
     # ---- configuration (set_settings, e2e_brtdp.py:582-652) --------------------------------
-    def set_settings(self, env, subtask, subtask_agent_names, other_agent_planners=None):
+    def _configure(self, env, subtask, subtask_agent_names, other_agent_planners=None):
         if other_agent_planners:
             raise NotImplementedError("Level-1 planning (other_agent_planners) is not restated")
         if subtask is None:
@@ -152,7 +212,7 @@ class E2E_BRTDP:
         assert agents == sorted(agents), "subtask agent names are not in order"
         self._agents = agents
         level, A = env.level, len(names)
-        key = (id(level), A, str(self.device or env._device))
+        key = (level.width, tuple(level.tiles), A, str(self.device or env._device))
         if self._exp is None or self._exp_key != key:
             self._exp = self._make_expander(level, A, self.device or env._device)
             self._exp_key = key
@@ -166,14 +226,22 @@ class E2E_BRTDP:
         start[exp.t_plane:] = 0
         self.cur_obj_count = self._obj_count(start, exp, env.level)  # _define_goal_state on the Level-0 env
         self._sub = capi.subtask(kind, agents, list(starts), goal, self.cur_obj_count)
-        # the start state: a no-op row gives its goal flag and lower bound
-        nxt, fl, lb = exp.rows(start, [(_NOOP,) * len(agents)], self._sub)
         self.start = self._key(start, groups)
-        self._states.setdefault(self.start, (start, groups))
+        # the start state: a no-op row gives its goal flag and lower bound
+        return (start, [(_NOOP,) * len(agents)], self._sub)
+
+    def _configured(self, res) -> None:
+        _, fl, lb = res
         self._start_goal = bool(fl[0] & capi.ROLL_GOAL)  # is_goal_state with this call's cur_obj_count
         self._value_init(self.start, self._start_goal, float(lb[0]))
 
-    def _level0(self, full: np.ndarray, exp: _Expander) -> np.ndarray:
+    def set_settings(self, env, subtask, subtask_agent_names, other_agent_planners=None):
+        self._configured(self._exp_run(self._configure(env, subtask, subtask_agent_names, other_agent_planners)))
+
+    def _exp_run(self, req):
+        return self._exp.run([req])[0]
+
+    def _level0(self, full: np.ndarray, exp) -> np.ndarray:
         """E2E_BRTDP._configure_planner_level, Level 0 (e2e_brtdp.py:383-406): the items held by
         agents outside the subtask leave the world (their frozen cells stay in the bytes; the
         kernel treats them as AgentCounters)."""
@@ -188,7 +256,7 @@ class E2E_BRTDP:
                 s[2 * A + a] = 0xFF
         return s
 
-    def _obj_count(self, s: np.ndarray, exp: _Expander, level) -> int:
+    def _obj_count(self, s: np.ndarray, exp, level) -> int:
         """cur_obj_count of _define_goal_state (e2e_brtdp.py:435-566) on a Level-0 state."""
         A, K = exp.A, exp.K
         held = {int(s[2 * A + a]) for a in range(A)} - {0xFF}
@@ -228,41 +296,59 @@ class E2E_BRTDP:
         self.v_l[vk] = lower - 1.09
         self.v_u[vk] = lower * 5 * (self.time_cost + self.action_cost)
 
+    # ---- transitions: one request per new state --------------------------------------------
+    def _need(self, key):
+        """Generator: make sure `key` is expanded (yields one request if it is not)."""
+        if (key, self._sub_key) not in self._succ:
+            cand = _CAND[len(self._agents)]  # product order of get_actions
+            res = yield (np.frombuffer(key[0], np.uint8), cand, self._sub)
+            self._expanded(key, cand, res)
 
-    # ---- transitions: one launch per state -------------------------------------------------
-    def _expand(self, key):
-        ek = (key, self._sub_key)
-        got = self._succ.get(ek)
-        if got is not None:
-            return got
-        s, groups = self._states[key]
-        n = len(self._agents)
-        cand = list(itertools.product(range(5), repeat=n))  # product order of get_actions
-        nxt, fl, lb = self._exp.rows(s, cand, self._sub)
-        K = self._exp.K
-        l0, m0 = 3 * self._exp.A, 3 * self._exp.A + K
+    def _expanded(self, key, cand, res) -> None:
+        nxt, fl, lb = res
+        sb, groups, agents = key
+        NP, K, A = len(sb), self._exp.K, self._exp.A
+        l0, m0 = 3 * A, 3 * A + K
+        raw = nxt.tobytes()
+        pmask = sb[m0:m0 + K]
+        sk = self._sub_key
+        v_l, v_u = self.v_l, self.v_u
         actions, succ = [], []
         for r, c in enumerate(cand):
-            if not fl[r] & capi.ROLL_LEGAL:
+            f = int(fl[r])
+            if not f & capi.ROLL_LEGAL:
                 continue
-            if fl[r] & capi.ROLL_ASSERT:  # T raises (e2e_brtdp.py:143)
+            if f & capi.ROLL_ASSERT:  # T raises (e2e_brtdp.py:143)
                 raise AssertionError("action {} led to co-located subtask agents".format(c))
-            ns = nxt[r]
-            ng = groups | frozenset(_group_name(int(m)) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
-            nk = self._key(ns, ng)
-            self._states.setdefault(nk, (ns, ng))
-            self._value_init(nk, bool(fl[r] & capi.ROLL_GOAL), float(lb[r]))
+            ns = raw[r * NP:(r + 1) * NP]
+            ng = groups
+            if ns[m0:m0 + K] != pmask:  # a merge made a new object group (world.py:304-306)
+                ng = groups | frozenset(_group_name(m) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
+            nk = (ns, ng, agents)
+            if (nk, sk) not in v_l or (nk, sk) not in v_u:
+                self._value_init(nk, bool(f & capi.ROLL_GOAL), float(lb[r]))
             actions.append(c)
             succ.append(nk)
-        got = (actions, succ)
-        self._succ[ek] = got
-        return got
+        self._succ[(key, sk)] = (actions, succ, [_COST[c] for c in actions], [(nk, sk) for nk in succ])
+
+    def _drive(self, gen):
+        """Run a search generator to completion, one launch per request."""
+        try:
+            req = next(gen)
+            while True:
+                req = gen.send(self._exp_run(req))
+        except StopIteration as stop:
+            return stop.value
+
+    def _expand(self, key):
+        self._drive(self._need(key))
+        return self._succ[(key, self._sub_key)]
 
     def get_actions(self, key) -> List[tuple]:  # e2e_brtdp.py:151-206
         return self._expand(key)[0]
 
     def T(self, key, action):  # e2e_brtdp.py:103-149
-        actions, succ = self._expand(key)
+        actions, succ = self._expand(key)[:2]
         return succ[actions.index(action)]
 
     def cost(self, action) -> float:  # e2e_brtdp.py:816-826
@@ -278,12 +364,19 @@ class E2E_BRTDP:
         expected_value = 1.0 * value_f[(nk, self._sub_key)]
         return float(cost + expected_value)
 
-    def get_expected_diff(self, key, action):  # e2e_brtdp.py:828-840
-        nk = self.T(key, action)
+    def _q_all(self, key, value_f) -> List[float]:
+        """[Q(key, a, value_f) for a in get_actions(key)] in one pass (same float64 ops);
+        `key` must be expanded."""
+        got = self._succ[(key, self._sub_key)]
+        return [float(c + 1.0 * value_f[vk]) for c, vk in zip(got[2], got[3])]
+
+    def _expected_diff(self, key, action):  # get_expected_diff, e2e_brtdp.py:828-840
+        got = self._succ[(key, self._sub_key)]
+        nk = got[1][got[0].index(action)]
         return {nk: 1.0 * (self.v_u[(nk, self._sub_key)] - self.v_l[(nk, self._sub_key)])}
 
-    # ---- search (e2e_brtdp.py:208-331, 842-878) ----------------------------------------------
-    def runSampleTrial(self) -> None:
+    # ---- search (e2e_brtdp.py:208-331, 842-878), as generators --------------------------------
+    def _sample_trial(self):  # runSampleTrial
         x = self.start
         traj = []
         counter = 0
@@ -293,14 +386,16 @@ class E2E_BRTDP:
             if counter > self.cap:
                 break
             traj.append(x)
-            actions = self.get_actions(x)
-            new_upper = min([self.Q(x, a, self.v_u) for a in actions])
+            yield from self._need(x)
+            actions = self._succ[(x, sk)][0]
+            new_upper = min(self._q_all(x, self.v_u))
             self.v_u[(x, sk)] = new_upper
-            action_index = argmin([self.Q(x, a, self.v_l) for a in actions])
+            ql = self._q_all(x, self.v_l)
+            action_index = argmin(ql, self._rng)
             a = actions[action_index]
-            new_lower = self.Q(x, a, self.v_l)
+            new_lower = ql[action_index]  # = Q(x, a, v_l): that table did not change since
             self.v_l[(x, sk)] = new_lower
-            b = self.get_expected_diff(x, a)
+            b = self._expected_diff(x, a)
             B = sum(b.values())
             diff = (self.v_u[(self.start, sk)] - self.v_l[(self.start, sk)]) / self.tau
             if B <= diff:
@@ -308,42 +403,110 @@ class E2E_BRTDP:
             x = list(b.keys())[0]
         while traj:
             x = traj.pop()
-            actions = self.get_actions(x)
-            self.v_u[(x, sk)] = min([self.Q(x, a, self.v_u) for a in actions])
-            self.v_l[(x, sk)] = min([self.Q(x, a, self.v_l) for a in actions])
+            self.v_u[(x, sk)] = min(self._q_all(x, self.v_u))
+            self.v_l[(x, sk)] = min(self._q_all(x, self.v_l))
 
-    def main(self) -> None:
+    def _main(self):  # main
         main_counter = 0
         sk = (self.start, self._sub_key)
         diff = self.v_u[sk] - self.v_l[sk]
         while diff > self.alpha and main_counter < self.main_cap:
             diff = self.v_u[sk] - self.v_l[sk]
             main_counter += 1
-            self.runSampleTrial()
+            yield from self._sample_trial()
+
+    def _next_action(self, env, subtask, subtask_agent_names, other_agent_planners):
+        self._configured((yield self._configure(env, subtask, subtask_agent_names, other_agent_planners)))
+        cur = self.start
+        self.cur_state = cur
+        yield from self._need(cur)
+        actions = self._succ[(cur, self._sub_key)][0]
+        action_index = argmin(self._q_all(cur, self.v_l), self._rng)
+        a = actions[action_index]
+        B = sum(self._expected_diff(cur, a).values())
+        sk = (cur, self._sub_key)
+        diff = (self.v_u[sk] - self.v_l[sk]) / self.tau
+        if B > diff:
+            yield from self._main()
+        if self._start_goal:  # is_goal_state(cur_state)
+            return None
+        qvals = self._q_all(cur, self.v_l)
+        a = actions[argmin(np.array(qvals), self._rng)]
+        return _NAV[a[0]] if len(a) == 1 else tuple(_NAV[c] for c in a)
+
+    def runSampleTrial(self) -> None:
+        self._drive(self._sample_trial())
+
+    def main(self) -> None:
+        self._drive(self._main())
 
     def get_next_action(self, env, subtask, subtask_agent_names, other_agent_planners=None):
         """The next (joint) action for the subtask agents, as the reference's
         ``get_next_action`` returns it: a (dx, dy) tuple for one agent, a pair of them for two,
         ``None`` when the start state already satisfies the subtask."""
-        self.set_settings(env, subtask, subtask_agent_names, other_agent_planners)
-        cur = self.start
-        self.cur_state = cur
-        actions = self.get_actions(cur)
-        action_index = argmin([self.Q(cur, a, self.v_l) for a in actions])
-        a = actions[action_index]
-        B = sum(self.get_expected_diff(cur, a).values())
-        sk = (cur, self._sub_key)
-        diff = (self.v_u[sk] - self.v_l[sk]) / self.tau
-        if B > diff:
-            self.main()
-        if self._start_goal:  # is_goal_state(cur_state)
-            return None
-        actions = self.get_actions(cur)
-        qvals = [self.Q(cur, a, self.v_l) for a in actions]
-        a = actions[argmin(np.array(qvals))]
-        return _NAV[a[0]] if len(a) == 1 else tuple(_NAV[c] for c in a)
+        return self._drive(self._next_action(env, subtask, subtask_agent_names, other_agent_planners))
 
     def start_values(self) -> Tuple[float, float]:
         """(v_l, v_u) of the current start state."""
         sk = (self.start, self._sub_key)
         return self.v_l[sk], self.v_u[sk]
+
+
+class PlanEnv:
+    """A planning start state without a live env (what :meth:`E2E_BRTDP.get_next_action` reads
+    from one): the level, the agent count, the env's state bytes (``ax[A] ay[A] ah[A] loc[K]
+    mask[K] t_lo t_hi flags``) and the object-group names the env has had since reset."""
+
+    def __init__(self, level, num_agents: int, state_bytes, group_names=(), device="cuda:0"):
+        self.level = level
+        self._device = device
+        self._A = num_agents
+        self._bytes = np.asarray(state_bytes, dtype=np.uint8).copy()
+        K = (len(self._bytes) - 3 * num_agents - 3) // 2
+        loc = self._bytes[3 * num_agents:3 * num_agents + K]
+        mask = self._bytes[3 * num_agents + K:3 * num_agents + 2 * K]
+        items = [_envs.ItemView(j, int(m), None, False) for j, (l, m) in enumerate(zip(loc, mask)) if l != 0xFF]
+        self.world = types.SimpleNamespace(items=items)
+        self._group_names = frozenset(group_names)
+
+    def get_agent_names(self) -> List[str]:
+        return ["agent-%d" % (a + 1) for a in range(self._A)]
+
+    def state_bytes(self) -> np.ndarray:
+        return self._bytes.copy()
+
+
+def plan_batch(planners: Sequence[E2E_BRTDP], envs_, subtasks, agent_names) -> list:
+    """get_next_action of many independent searches at once (Level 0): planner i plans
+    `subtasks[i]` for `agent_names[i]` in `envs_[i]`.  The searches run in lockstep; every
+    round, the states all of them need expanded go to the GPU in shared oc_rollout launches
+    (up to 4,096 rows and 64 subtask configurations each), so the number of launches is about
+    that of the longest single search.  Each search gives exactly its sequential result when
+    its planner has its own generator (``rng=np.random.RandomState(seed)``).  All planners must
+    share one level and agent count; they share the first planner's expander."""
+    assert len(planners) == len(envs_) == len(subtasks) == len(agent_names)
+    if not planners:
+        return []
+    gens = [p._next_action(e, st, an, None) for p, e, st, an in zip(planners, envs_, subtasks, agent_names)]
+    out = [None] * len(gens)
+    pending = {}
+    exp = None
+    for i, g in enumerate(gens):  # the first request of each search builds (or shares) its expander
+        if exp is not None:
+            planners[i]._exp, planners[i]._exp_key = exp, planners[0]._exp_key
+        try:
+            pending[i] = next(g)
+        except StopIteration as stop:
+            out[i] = stop.value
+        exp = exp or planners[i]._exp
+    while pending:
+        idx = list(pending)
+        results = exp.run([pending[i] for i in idx])
+        nxt = {}
+        for i, res in zip(idx, results):
+            try:
+                nxt[i] = gens[i].send(res)
+            except StopIteration as stop:
+                out[i] = stop.value
+        pending = nxt
+    return out

@@ -81,3 +81,43 @@ def test_planner_matches_reference_calls(mode):
         n += 1
     assert n > 0
     assert not errs, "%d of %d calls differ:\n%s" % (len(errs), n, "\n".join(errs[:15]))
+
+
+def test_plan_batch_matches_reference_calls_in_shared_launches():
+    """plan_batch on the GPU: every 'fresh' call of a config as one lockstep batch, each search
+    with its own RandomState(seed) -> the reference's results, in far fewer launches than the
+    searches make one by one."""
+    from gym_cooking_amd.planner import E2E_BRTDP, plan_batch
+    fx = _fixture()
+    params = fx["params"]
+    errs, n = [], 0
+    for cfg_i, cfg in enumerate(fx["configs"]):
+        calls = [c for c in fx["calls"] if c["mode"] == "fresh" and c["cfg"] == cfg_i]
+        if not calls:
+            continue
+        envs_, agn = [], []
+        for c in calls:
+            from gym_cooking_amd import envs
+            e = envs.OvercookedEnvironment(level=cfg["level"], num_agents=cfg["A"])
+            e.reset()
+            lv = e.level
+            K = capi.item_slots(lv)
+            P = capi.pitch_for(1)
+            s = tl.state_from_canonical(lv, cfg["A"], K, P, np.array([c["agents"]], np.uint8),
+                                        np.array([c["items"]], np.uint8), np.array([c["env_t"]]))
+            e.load_state(tl.env_view(s, cfg["A"], K, P, 1)[:, 0])
+            e._group_names = frozenset(g for g in c["groups"] if g not in _STATIC)
+            envs_.append(e)
+            agn.append(tuple(e.get_agent_names()[a] for a in c["sub_agents"]))
+        planners = [E2E_BRTDP(**params, rng=np.random.RandomState(c["seed"])) for c in calls]
+        got = plan_batch(planners, envs_, [_subtask(c["subtask"]) for c in calls], agn)
+        for p, a, c in zip(planners, got, calls):
+            exp = None if c["action"] is None else (_NAV[c["action"][0]] if len(c["action"]) == 1
+                                                    else tuple(_NAV[k] for k in c["action"]))
+            if (a, *p.start_values(), len(p.v_l)) != (exp, c["v_l"], c["v_u"], c["n_states"]):
+                errs.append("%s %s: %s vs %s" % (cfg["level"], c["subtask"], a, exp))
+            n += 1
+        batch_launches = planners[0]._exp.launches
+        assert batch_launches < sum(1 + len(p._succ) for p in planners)
+    assert n > 0
+    assert not errs, "\n".join(errs[:10])

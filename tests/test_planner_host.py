@@ -28,6 +28,9 @@ class OracleExpander:
         self.NP, self.t_plane, self.P = P["num_planes"], P["t"], self.ob.pitch
         self.launches = 0
 
+    def run(self, requests):
+        return [self.rows(*req) for req in requests]
+
     def rows(self, state, codes, sub):
         n = len(codes)
         sin = np.zeros((self.NP, self.P), np.uint8)
@@ -89,3 +92,28 @@ def test_host_planner_matches_reference_calls(mode):
         n += 1
     assert n > 0
     assert not errs, "%d of %d calls differ:\n%s" % (len(errs), n, "\n".join(errs[:15]))
+
+
+def test_host_plan_batch_matches_reference_calls():
+    """plan_batch: every 'fresh' call of the fixture as one lockstep batch (per config), each
+    search with its own RandomState(seed) -> exactly the reference's results."""
+    from gym_cooking_amd.planner import E2E_BRTDP, plan_batch
+    fx = tg._fixture()
+    params = fx["params"]
+    errs, n = [], 0
+    for cfg_i, cfg in enumerate(fx["configs"]):
+        calls = [c for c in fx["calls"] if c["mode"] == "fresh" and c["cfg"] == cfg_i]
+        if not calls:
+            continue
+        envs_ = [_env(cfg["level"], cfg["A"], c) for c in calls]
+        agn = [tuple(e.get_agent_names()[a] for a in c["sub_agents"]) for e, c in zip(envs_, calls)]
+        planners = [E2E_BRTDP(**params, expander=OracleExpander, rng=np.random.RandomState(c["seed"])) for c in calls]
+        got = plan_batch(planners, envs_, [tg._subtask(c["subtask"]) for c in calls], agn)
+        for p, a, c in zip(planners, got, calls):
+            exp = None if c["action"] is None else (tg._NAV[c["action"][0]] if len(c["action"]) == 1
+                                                    else tuple(tg._NAV[k] for k in c["action"]))
+            if (a, *p.start_values(), len(p.v_l)) != (exp, c["v_l"], c["v_u"], c["n_states"]):
+                errs.append("%s %s: %s vs %s" % (cfg["level"], c["subtask"], a, exp))
+            n += 1
+    assert n > 0
+    assert not errs, "\n".join(errs[:10])
