@@ -240,19 +240,21 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         // Object.chop (core.py:187-192): the single food's chopped bit (bits 4..6, no cross-byte spill)
         const uint32_t chopped = bop3<OC_LUT((a & b) | c)>(hm << 4, 0x70707070u, hm);
         const uint32_t newHm = sel(fmg, cu, sel(full80(chop), chopped, hm));
-        // scatter: target slot on merge / pick, held slot on reloc / merge / chop
-        const uint32_t wo = merge | pick;
-        const uint32_t oh = perm(0x80402010u, 0x08040201u, h);  // 1 << h per byte (h < 8)
-        const uint32_t wh80 = and3(hold80, or3(reloc, merge, chop), k80);
+        // scatter: target slot on merge / pick, held slot on reloc / merge / chop.  The per-slot
+        // select masks are one v_perm each: selector byte = slot index (h, or the target slot
+        // oidx), table byte j = 0xFF; a holding-none h = 0xFF selects 0xFF and is masked off.
+        const uint32_t oidx = (ob0 >> 7) | (ob1 >> 6) | (ob2 >> 5);
+        const uint32_t fwo = full80(merge | pick);
+        const uint32_t fwh = full80(and3(hold80, or3(reloc, merge, chop), k80));
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const uint32_t eo = full80(at80[j] & wo);
-            const uint32_t eh = full80(and3(oh << (7 - j), wh80, k80));
+            const uint32_t lut_lo = j < 4 ? 0xFFu << (8 * j) : 0u, lut_hi = j < 4 ? 0u : 0xFFu << (8 * (j - 4));
+            const uint32_t eo = perm(lut_hi, lut_lo, oidx) & fwo;
+            const uint32_t eh = perm(lut_hi, lut_lo, h) & fwh;
             Lc[j] = sel(eh, newHl, sel(eo, newOl, Lc[j]));
             M[j] = sel(eh, newHm, sel(eo, newOm, M[j]));
         }
         // holding: released on deliver / put down, the target slot on pick-up
-        const uint32_t oidx = (ob0 >> 7) | (ob1 >> 6) | (ob2 >> 5);
         H[k] = sel(full80(deliver | put), kFF, sel(fpk, oidx, h));
     }
 

@@ -14,11 +14,13 @@ reference's decisions and draws exactly the reference's random numbers
 (tests/golden/brtdp.json, recorded from the reference).
 
 State identity.  The reference keys its value tables by ``env.get_repr()``: the subtask
-agents, every dynamic object group (``World.objects`` keeps emptied groups, world.py:304-337)
-and the frozen agents' ``Agent-Counter`` squares.  Here a state is (its engine state bytes
-without ``t`` / flags, the set of object-group names), which identifies the same states:
-frozen agents keep their cells in the bytes, and a group name set plus per-slot items fixes
-every group's list.
+agents, every dynamic object group in name order with its objects in insertion order
+(``World.objects`` keeps emptied groups, world.py:304-337) and the frozen agents'
+``Agent-Counter`` squares.  Here a state is (its engine state bytes without ``t`` / flags, with
+the item slots ordered by (group name, slot); the set of object-group names; the subtask
+agents), which identifies the same states: frozen agents keep their cells in the bytes, an
+item is known by its group and its rank there, and which slot a merged dish occupies is not
+part of it (see ``_canon``).
 
 Level 1 (``other_agent_planners`` non-empty, the BD agents' call) predicts the other agents'
 moves with their own planners; it is not restated here and raises ``NotImplementedError``.
@@ -52,6 +54,30 @@ def _group_name(mask: int) -> str:
 
 
 _CAND = {n: list(itertools.product(range(5), repeat=n)) for n in (1, 2)}
+
+
+def _canon(sb: bytes, A: int, K: int) -> bytes:
+    """The planner's form of a state: live item slots ordered by (object-group name, slot).
+    The reference's repr lists each group's objects in insertion order and nothing else, so
+    an item's identity is its group name plus its rank in that group; which slot a merged
+    dish happens to occupy is not part of it (the engine keeps the holder's slot, world.py
+    re-inserts the merged object).  Plates, the only name with two members, keep their
+    relative slot order, as they keep their order in World.objects."""
+    b = bytearray(sb)
+    l0, m0 = 3 * A, 3 * A + K
+    live = sorted((_group_name(b[m0 + j]), j) for j in range(K) if b[l0 + j] != 0xFF)
+    order = [j for _, j in live]
+    if order == list(range(len(order))):
+        return bytes(b)
+    new_of = {j: i for i, j in enumerate(order)}
+    locs = [b[l0 + j] for j in order] + [0xFF] * (K - len(order))
+    masks = [b[m0 + j] for j in order] + [0] * (K - len(order))
+    b[l0:l0 + K], b[m0:m0 + K] = bytes(locs), bytes(masks)
+    for a in range(A):
+        h = b[2 * A + a]
+        if h != 0xFF:
+            b[2 * A + a] = new_of[h]
+    return bytes(b)
 
 
 def _cost(action) -> float:  # E2E_BRTDP.cost (e2e_brtdp.py:816-826): 1.0, + 0.1 per moving agent, in order
@@ -224,6 +250,7 @@ class E2E_BRTDP:
         groups = frozenset(env._group_names) | frozenset(it.name for it in env.world.items)
         start = self._level0(full, exp)
         start[exp.t_plane:] = 0
+        start = np.frombuffer(_canon(start.tobytes(), exp.A, exp.K), np.uint8).copy()
         self.cur_obj_count = self._obj_count(start, exp, env.level)  # _define_goal_state on the Level-0 env
         self._sub = capi.subtask(kind, agents, list(starts), goal, self.cur_obj_count)
         self.start = self._key(start, groups)
@@ -322,7 +349,8 @@ class E2E_BRTDP:
                 raise AssertionError("action {} led to co-located subtask agents".format(c))
             ns = raw[r * NP:(r + 1) * NP]
             ng = groups
-            if ns[m0:m0 + K] != pmask:  # a merge made a new object group (world.py:304-306)
+            if ns[m0:m0 + K] != pmask:  # a chop or a merge: a merge makes a new object group (world.py:304-306)
+                ns = _canon(ns, A, K)
                 ng = groups | frozenset(_group_name(m) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
             nk = (ns, ng, agents)
             if (nk, sk) not in v_l or (nk, sk) not in v_u:

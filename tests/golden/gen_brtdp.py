@@ -18,6 +18,10 @@ subtask (kind, agents, start / goal masks), the seed, and the outcome: the retur
 the planner's cur_obj_count, v_l / v_u of the start state and the number of states the
 planner has initialised (len(v_l)).
 
+The reference planner takes up to minutes per joint call here; the committed file was
+written under a 50-minute budget, so the last config (partial-divider_tl) has no calls (the
+file is saved after every finished episode).
+
 Usage:  PYTHONHASHSEED=0 python tests/golden/gen_brtdp.py
 """
 from __future__ import annotations

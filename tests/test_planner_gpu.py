@@ -22,8 +22,19 @@ _NAV = [(0, 1), (0, -1), (-1, 0), (1, 0), (0, 0)]
 
 
 def _fixture():
+    """tests/golden/brtdp.json (goal-directed states) + brtdp_scripted.json (the scripted salad
+    episodes: Merge / Deliver subtasks), one call list with the configs concatenated."""
     with open(os.path.join(tl.GOLDEN, "brtdp.json")) as f:
-        return json.load(f)
+        fx = json.load(f)
+    extra = os.path.join(tl.GOLDEN, "brtdp_scripted.json")
+    if os.path.exists(extra):
+        with open(extra) as f:
+            sc = json.load(f)
+        assert sc["params"] == fx["params"]
+        off = len(fx["configs"])
+        fx["configs"] = fx["configs"] + sc["configs"]
+        fx["calls"] = fx["calls"] + [dict(c, cfg=c["cfg"] + off) for c in sc["calls"]]
+    return fx
 
 
 def _subtask(text):
