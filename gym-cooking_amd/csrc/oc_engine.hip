@@ -1018,7 +1018,11 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
 }
 
 // Shared argument block of oc_rollout / oc_nav_likelihood: level tables + validated subtasks.
-static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num_subtasks, int64_t B, RollArgs& R) {
+static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num_subtasks, int64_t B, RollArgs& R,
+                     bool level1_ok = false) {
+    for (int i = 0; i < num_subtasks && subtasks != nullptr; ++i)
+        if (subtasks[i].level != OC_LEVEL0 && !level1_ok)
+            return fail(OC_EINVAL, "subtask %d: only oc_rollout takes OC_LEVEL1", i);
     if (num_subtasks < 1 || num_subtasks > OC_MAX_SUBTASKS) return fail(OC_EINVAL, "num_subtasks %d", num_subtasks);
     if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes", ocro::kMaxNodes);
     if (h->roll_dist == nullptr) return fail(OC_EHIP, "rollout tables not on the device");
@@ -1040,9 +1044,11 @@ static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num
         d.agent[1] = s.num_agents == 2 ? s.agent[1] : s.agent[0];
         d.start[0] = s.start_mask[0];
         d.start[1] = s.start_mask[1];
+        if (s.level > OC_LEVEL1) return fail(OC_EINVAL, "subtask %d: level %d", i, s.level);
         d.goal = s.goal_mask;
         d.count = s.goal_count;
-        d.pad[0] = d.pad[1] = 0;
+        d.level = s.level;
+        d.pad = 0;
     }
     return OC_OK;
 }
@@ -1057,7 +1063,7 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     if (((uintptr_t)lower_bound & 3u) || ((uintptr_t)state_in & 1u) || ((uintptr_t)state_out & 1u))
         return fail(OC_EINVAL, "misaligned buffer");
     RollArgs R;
-    if (const int rc = roll_args(h, subtasks, num_subtasks, B, R)) return rc;
+    if (const int rc = roll_args(h, subtasks, num_subtasks, B, R, true)) return rc;
     if (B == 0) return OC_OK;
     const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)kCUs * 8;
     const dim3 grid((unsigned)(need < cap ? need : cap));

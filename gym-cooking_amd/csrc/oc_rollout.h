@@ -39,7 +39,7 @@ struct RollLevel {
 
 struct Sub {  // oc_subtask, device copy
     int32_t kind, n;
-    uint8_t agent[2], start[2], goal, count, pad[2];
+    uint8_t agent[2], start[2], goal, count, level, pad;
 };
 
 // One row's state, packed so that run-time slot / agent indices are shifts, not memory:
@@ -141,8 +141,9 @@ template <int A, int K>
 struct RowOps {
     const RollLevel& L;
     const uint8_t* dist;  // LDS on the device
-    uint64_t ac = 0;      // AgentCounter cells of this row's Level-0 view
-    uint32_t active = 0;  // bit a: agent a is a subtask agent
+    uint64_t ac = 0;        // AgentCounter cells of this row's Level-0 view
+    uint32_t active = 0;    // bit a: agent a is a subtask agent
+    uint32_t blockers = 0;  // bit a: agent a's cell may not be moved into (get_single_actions)
 
     OC_RH RowOps(const RollLevel& l, const uint8_t* d) : L(l), dist(d) {}
 
@@ -157,6 +158,11 @@ struct RowOps {
         active = 0;
         bool raised = false;
         for (int i = 0; i < s.n; ++i) active |= 1u << s.agent[i];
+        if (s.level != 0) {  // Level 1: every agent stays in sim_agents, nothing is removed
+            blockers = (1u << A) - 1u;
+            return false;
+        }
+        blockers = active;
 #pragma unroll
         for (int a = 0; a < A; ++a) {
             if ((active >> a) & 1u) continue;
@@ -250,7 +256,7 @@ struct RowOps {
         ny = ny < 0 ? 0 : (ny > L.H - 1 ? L.H - 1 : ny);
 #pragma unroll
         for (int b = 0; b < A; ++b)
-            if (((active >> b) & 1u) && r.ax(b) == nx && r.ay(b) == ny) return false;
+            if (((blockers >> b) & 1u) && r.ax(b) == nx && r.ay(b) == ny) return false;
         const int c = cell(nx, ny), t = tile(c);
         if (t == kFloor || t == kDelivery) return true;
         const int o = item_at(r, c);
@@ -401,6 +407,7 @@ struct RowOps {
         ac = 0;
         active = 1u << s.agent[0];
         if (s.n == 2) active |= 1u << s.agent[1];
+        blockers = active;
         float pen;
         const float d = lower_bound_parts(r, s, pen);
         lb = d + pen;
@@ -454,7 +461,7 @@ struct RowOps {
         out = 0.0;
         if (s.kind == 0) {  // None: one agent, the self agent's movable actions in the full state
             if (s.n != 1) return 4;
-            active = (1u << A) - 1u;
+            active = blockers = (1u << A) - 1u;
             ac = 0;
             int n = 0;
             for (int c = 0; c < 4; ++c) n += single_legal(r, self_agent, c) ? 1 : 0;

@@ -68,7 +68,7 @@ class OcSubtask(ctypes.Structure):
     """oc_subtask (include/oc_engine.h): one navigation-planner configuration."""
     _fields_ = [("kind", ctypes.c_int32), ("num_agents", ctypes.c_int32), ("agent", ctypes.c_uint8 * 2),
                 ("start_mask", ctypes.c_uint8 * 2), ("goal_mask", ctypes.c_uint8),
-                ("goal_count", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 2)]
+                ("goal_count", ctypes.c_uint8), ("level", ctypes.c_uint8), ("reserved", ctypes.c_uint8)]
 
 
 OC_RENDER_SIZES = 4
@@ -84,8 +84,9 @@ class OcRenderDesc(ctypes.Structure):
                 ("food_sprite", ctypes.c_uint8 * 128), ("chan_map", ctypes.c_uint32)]
 
 
-def subtask(kind: int, agents, start_masks, goal_mask: int, goal_count: int = 0) -> OcSubtask:
+def subtask(kind: int, agents, start_masks, goal_mask: int, goal_count: int = 0, level: int = 0) -> OcSubtask:
     s = OcSubtask()
+    s.level = level
     s.kind = kind
     s.num_agents = len(agents)
     for i, a in enumerate(agents):

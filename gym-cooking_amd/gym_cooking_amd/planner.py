@@ -1,5 +1,5 @@
 """Engine-backed navigation planner: a drop-in for
-gym_cooking/navigation_planner/planners/e2e_brtdp.py ``E2E_BRTDP`` at Level 0.
+gym_cooking/navigation_planner/planners/e2e_brtdp.py ``E2E_BRTDP`` (Level 0 and Level 1).
 
 The reference planner's time goes into its environment rollouts: every ``T(state, action)``
 deep-copies a whole ``OvercookedEnvironment`` and runs ``interact`` on it, and every new
@@ -22,8 +22,12 @@ agents), which identifies the same states: frozen agents keep their cells in the
 item is known by its group and its rank there, and which slot a merged dish occupies is not
 part of it (see ``_canon``).
 
-Level 1 (``other_agent_planners`` non-empty, the BD agents' call) predicts the other agents'
-moves with their own planners; it is not restated here and raises ``NotImplementedError``.
+Level 1 (``other_agent_planners`` non-empty, the Bayesian-delegation agents' call): every
+agent stays in the planner's states (the rollout rows run with ``OC_LEVEL1``), and at every
+state the search visits, each other agent's planner -- a shallow copy of this one, sharing
+its value tables, as ``BayesianDelegator.get_other_agent_planners`` makes them -- is set up
+there and picks its greedy action (``_get_modified_state_with_other_agent_actions``,
+e2e_brtdp.py:842-878), drawing the same random numbers as the reference.
 """
 from __future__ import annotations
 
@@ -192,7 +196,7 @@ def _ptr(t):
 
 
 class E2E_BRTDP:
-    """Bounded RTDP navigation planner (e2e_brtdp.py:38-878), Level 0, over the HIP engine.
+    """Bounded RTDP navigation planner (e2e_brtdp.py:38-878), Levels 0 and 1, over the HIP engine.
 
     Same constructor, same ``get_next_action(env, subtask, subtask_agent_names,
     other_agent_planners)``, same value tables ``v_l`` / ``v_u`` (keyed by (state, subtask)),
@@ -224,9 +228,16 @@ class E2E_BRTDP:
         self._succ: Dict = {}  # (state key, subtask key) -> (actions, successors, costs, value keys)
 
     # ---- configuration (set_settings, e2e_brtdp.py:582-652) --------------------------------
+    def __copy__(self):  # e2e_brtdp.py:97-101: a shallow copy shares the value tables (and here the caches)
+        new = object.__new__(E2E_BRTDP)
+        new.__dict__ = self.__dict__.copy()
+        return new
+
     def _configure(self, env, subtask, subtask_agent_names, other_agent_planners=None):
-        if other_agent_planners:
-            raise NotImplementedError("Level-1 planning (other_agent_planners) is not restated")
+        # _configure_planner_level (e2e_brtdp.py:383-406): Level 1 when other agents' planners
+        # are given -- every agent stays -- else Level 0
+        self.other_agent_planners = dict(other_agent_planners or {})
+        self._level = 1 if self.other_agent_planners else 0
         if subtask is None:
             raise NotImplementedError("the reference agents do not plan the None subtask")
         assert len(subtask_agent_names) <= 2, "Cannot have more than 2 agents! Hm... {}".format(subtask_agent_names)
@@ -248,11 +259,14 @@ class E2E_BRTDP:
         self._kind, self._goal_mask = kind, goal
         full = env.state_bytes()
         groups = frozenset(env._group_names) | frozenset(it.name for it in env.world.items)
-        start = self._level0(full, exp)
+        start = full.copy() if self._level else self._level0(full, exp)
         start[exp.t_plane:] = 0
         start = np.frombuffer(_canon(start.tobytes(), exp.A, exp.K), np.uint8).copy()
         self.cur_obj_count = self._obj_count(start, exp, env.level)  # _define_goal_state on the Level-0 env
-        self._sub = capi.subtask(kind, agents, list(starts), goal, self.cur_obj_count)
+        self._sub = capi.subtask(kind, agents, list(starts), goal, self.cur_obj_count, self._level)
+        self._level_name = env.level
+        self._A = A
+        self._dev = self.device or env._device
         self.start = self._key(start, groups)
         # the start state: a no-op row gives its goal flag and lower bound
         return (start, [(_NOOP,) * len(agents)], self._sub)
@@ -307,7 +321,7 @@ class E2E_BRTDP:
         """A planner state: its bytes, its object-group names and which agents are the subtask
         agents (the reference's Level-0 repr lists those as agents and the others as
         Agent-Counter squares)."""
-        return (s.tobytes(), groups, tuple(self._agents))
+        return (s.tobytes(), groups, tuple(self._agents), self._level)
 
     # ---- values (value_init, e2e_brtdp.py:678-729) --------------------------------------------
     def _value_init(self, key, goal: bool, lb: float) -> None:
@@ -333,7 +347,7 @@ class E2E_BRTDP:
 
     def _expanded(self, key, cand, res) -> None:
         nxt, fl, lb = res
-        sb, groups, agents = key
+        sb, groups, agents, lvl = key
         NP, K, A = len(sb), self._exp.K, self._exp.A
         l0, m0 = 3 * A, 3 * A + K
         raw = nxt.tobytes()
@@ -352,7 +366,7 @@ class E2E_BRTDP:
             if ns[m0:m0 + K] != pmask:  # a chop or a merge: a merge makes a new object group (world.py:304-306)
                 ns = _canon(ns, A, K)
                 ng = groups | frozenset(_group_name(m) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
-            nk = (ns, ng, agents)
+            nk = (ns, ng, agents, lvl)
             if (nk, sk) not in v_l or (nk, sk) not in v_u:
                 self._value_init(nk, bool(f & capi.ROLL_GOAL), float(lb[r]))
             actions.append(c)
@@ -414,6 +428,7 @@ class E2E_BRTDP:
             if counter > self.cap:
                 break
             traj.append(x)
+            yield from self._modified_state(x)
             yield from self._need(x)
             actions = self._succ[(x, sk)][0]
             new_upper = min(self._q_all(x, self.v_u))
@@ -447,6 +462,7 @@ class E2E_BRTDP:
         self._configured((yield self._configure(env, subtask, subtask_agent_names, other_agent_planners)))
         cur = self.start
         self.cur_state = cur
+        yield from self._modified_state(cur)
         yield from self._need(cur)
         actions = self._succ[(cur, self._sub_key)][0]
         action_index = argmin(self._q_all(cur, self.v_l), self._rng)
@@ -473,6 +489,24 @@ class E2E_BRTDP:
         ``get_next_action`` returns it: a (dx, dy) tuple for one agent, a pair of them for two,
         ``None`` when the start state already satisfies the subtask."""
         return self._drive(self._next_action(env, subtask, subtask_agent_names, other_agent_planners))
+
+    def _modified_state(self, key):
+        """_get_modified_state_with_other_agent_actions (e2e_brtdp.py:842-878) as a generator.
+        Level 0: nothing.  Level 1: every other agent's planner is set up on the state (a Level-0
+        planner of its own subtask) and picks its greedy action by argmin over its Q values --
+        drawing from the same generator as the reference.  The chosen actions only mark the
+        agents (agent.action is not part of T or of a repr), so the state itself is unchanged
+        and already initialised."""
+        if not self._level:
+            return
+        groups = key[1]
+        for name, op in self.other_agent_planners.items():
+            env = PlanEnv(self._level_name, self._A, np.frombuffer(key[0], np.uint8), groups, device=self._dev)
+            op._exp, op._exp_key, op._rng = self._exp, self._exp_key, self._rng
+            op._configured((yield op._configure(env, op.subtask, op.subtask_agent_names)))
+            yield from op._need(op.start)
+            acts = op._succ[(op.start, op._sub_key)][0]
+            argmin(op._q_all(op.start, op.v_l), op._rng)
 
     def start_values(self) -> Tuple[float, float]:
         """(v_l, v_u) of the current start state."""
@@ -505,7 +539,7 @@ class PlanEnv:
 
 
 def plan_batch(planners: Sequence[E2E_BRTDP], envs_, subtasks, agent_names) -> list:
-    """get_next_action of many independent searches at once (Level 0): planner i plans
+    """get_next_action of many independent Level-0 searches at once: planner i plans
     `subtasks[i]` for `agent_names[i]` in `envs_[i]`.  The searches run in lockstep; every
     round, the states all of them need expanded go to the GPU in shared oc_rollout launches
     (up to 4,096 rows and 64 subtask configurations each), so the number of launches is about

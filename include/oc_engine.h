@@ -196,6 +196,8 @@ int oc_stats_reduce(const oc_handle* h, const uint64_t* stats, int64_t B, uint64
 #define OC_SUB_CHOP 1    /* Chop(food)     gym_cooking/recipe_planner/utils.py:128 */
 #define OC_SUB_MERGE 2   /* Merge(a, b)    recipe_planner/utils.py:142 */
 #define OC_SUB_DELIVER 3 /* Deliver(dish)  recipe_planner/utils.py:157 */
+#define OC_LEVEL0 0      /* E2E_BRTDP planner levels, oc_subtask.level */
+#define OC_LEVEL1 1
 
 /* One planner configuration (set_settings(env, subtask, subtask_agent_names)). */
 typedef struct {
@@ -205,7 +207,11 @@ typedef struct {
     uint8_t start_mask[2]; /* start_obj content mask (Chop, Deliver: [0]); Merge: start_obj[0], [1] */
     uint8_t goal_mask;     /* goal_obj content mask (navigation_planner/utils.py:181-246) */
     uint8_t goal_count;    /* cur_obj_count of _define_goal_state at set_settings */
-    uint8_t reserved[2];
+    uint8_t level;         /* planner level (e2e_brtdp.py:383-406): OC_LEVEL0 (agents outside the
+                              subtask become AgentCounters, their items leave) or OC_LEVEL1 (every
+                              agent stays; none may be moved into).  oc_rollout only; the other
+                              entry points take OC_LEVEL0 */
+    uint8_t reserved;
 } oc_subtask;
 
 /* rollout flags (per row) */
@@ -229,6 +235,8 @@ typedef struct {
  *   out_flags  : u8 [pitch] OC_ROLL_* ;  lower_bound : f32 [pitch], the lower bound of the
  *                next state before the planner's cost factor (value_init: v_l = 1.1*lb - 1.09,
  *                v_u = 6.05*lb; goal states have value 0) */
+/* Level: with OC_LEVEL1 in a configuration's `level` the row keeps every agent (the planner's
+ * Level-1 env, e2e_brtdp.py:383-392): nothing is removed, no agent's cell may be moved into. */
 int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
                const uint8_t* alloc, const oc_subtask* subtasks, int32_t num_subtasks,
                uint8_t* out_flags, float* lower_bound, int64_t B, void* stream);

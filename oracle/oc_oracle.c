@@ -826,7 +826,7 @@ static void* run_roll(void* p) {
         Env env;
         int fl;
         unpack(&j->c, j->sin, e, &env, &fl);
-        if (level0_view(&env, s)) { /* the reference raises configuring the planner: row copied */
+        if (s->level == OC_LEVEL0 && level0_view(&env, s)) { /* the reference raises configuring the planner */
             unpack(&j->c, j->sin, e, &env, &fl);
             pack(&j->c, &env, fl, j->sout, e);
             j->flags[e] = OC_ROLL_RAISES;

@@ -20,7 +20,12 @@ joint) the row records:
   * v_l/v_u -- the planner's value_init of the next state (e2e_brtdp.py:678-729)
 The subtask is stored as (kind, agent indices, start masks, goal mask, cur_obj_count).
 
-Usage:  python tests/golden/gen_rollout.py
+With --level1 the planners are configured at Level 1 (a non-empty other_agent_planners:
+every agent stays in the planner's env, e2e_brtdp.py:383-392; the other planners themselves
+are only consulted by get_next_action, never by T / get_actions / value_init) and the rows go
+to tests/golden/rollout_level1.npz.
+
+Usage:  python tests/golden/gen_rollout.py [--level1]
 """
 from __future__ import annotations
 
@@ -48,12 +53,15 @@ SAMPLE_EVERY, MAX_T = 4, 48
 KIND = {"Chop": 1, "Merge": 2, "Deliver": 3}
 
 
+LEVEL1 = "--level1" in sys.argv
+
+
 def main():
     ref = gg.load_reference()
     from navigation_planner.planners.e2e_brtdp import E2E_BRTDP  # noqa: E402
 
     rows = {k: [] for k in ("cfg", "state", "kind", "agents", "start", "goal_mask", "goal_count",
-                            "action", "legal", "assert_", "next", "goal", "lb", "v_l", "v_u")}
+                            "action", "legal", "assert_", "copy_raise", "next", "goal", "lb", "v_l", "v_u")}
     states = []  # (cfg index, canonical agents, items, t)
     for ci, (level, A, n_eps, seed0) in enumerate(CONFIGS):
         info = gg.RefEnv(ref, level, 4, 100).level_info()
@@ -73,7 +81,7 @@ def main():
     n = len(rows["cfg"])
     out = {k: np.array(v) for k, v in rows.items()}
     np.savez_compressed(
-        os.path.join(HERE, "rollout.npz"),
+        os.path.join(HERE, "rollout_level1.npz" if LEVEL1 else "rollout.npz"),
         cfg_level=np.array([c[0] for c in CONFIGS]), cfg_A=np.array([c[1] for c in CONFIGS], np.int32),
         st_cfg=np.array([s[0] for s in states], np.int32), st_agents=np.array([s[1] for s in states], np.uint8),
         st_items=np.array([s[2] for s in states], np.uint8), st_t=np.array([s[3] for s in states], np.int32),
@@ -94,7 +102,9 @@ def record_state(rows, E2E_BRTDP, ref, env, A, ci, si):
                 sub_names = tuple(names[i] for i in sub)
                 p = E2E_BRTDP(alpha=0.01, tau=2, cap=75, main_cap=100)
                 with contextlib.redirect_stdout(io.StringIO()):
-                    p.set_settings(env=copy.copy(env), subtask=st, subtask_agent_names=sub_names)
+                    others = {n: None for n in names if n not in sub_names} if LEVEL1 else {}
+                    p.set_settings(env=copy.copy(env), subtask=st, subtask_agent_names=sub_names,
+                                   other_agent_planners=others)
                 srepr = p.start.get_repr()
                 with contextlib.redirect_stdout(io.StringIO()):
                     legal = set(p.get_actions(srepr))
@@ -105,12 +115,17 @@ def record_state(rows, E2E_BRTDP, ref, env, A, ci, si):
                 for codes in acts:
                     action = gg.NAV[codes[0]] if size == 1 else tuple(gg.NAV[c] for c in codes)
                     nxt_canon = np.full((4, 3), gg.PAD, np.uint8), np.full((4, 4), gg.PAD, np.uint8)
-                    asserted, goal, lb, v_l, v_u = 0, 0, -1.0, 0.0, 0.0
+                    asserted, copy_raise, goal, lb, v_l, v_u = 0, 0, 0, -1.0, 0.0, 0.0
                     try:
                         with contextlib.redirect_stdout(io.StringIO()):
                             nxt = p.T(srepr, action)
                     except AssertionError:
                         asserted = 1
+                    except AttributeError:
+                        # Level 1 only, actions outside get_actions: an agent steps onto another
+                        # agent's Floor and both hold items; T's repr_init copy raises as
+                        # env.step's does (overcooked_environment.py:108-113 -> world.py:417)
+                        copy_raise = 1
                     else:
                         nxt_canon = canon(nxt, names)
                         nrepr = nxt.get_repr()
@@ -134,6 +149,7 @@ def record_state(rows, E2E_BRTDP, ref, env, A, ci, si):
                     rows["action"].append(ac)
                     rows["legal"].append(int(action in legal))
                     rows["assert_"].append(asserted)
+                    rows["copy_raise"].append(copy_raise)
                     rows["next"].append(np.concatenate([nxt_canon[0].reshape(-1), nxt_canon[1].reshape(-1)]))
                     rows["goal"].append(goal)
                     rows["lb"].append(lb)

@@ -226,9 +226,10 @@ def state_from_canonical(level, A: int, K: int, pitch: int, agents: np.ndarray, 
 
 
 class RolloutRows:
-    """Rows of tests/golden/rollout.npz for one (level, A) config, with their subtask table."""
+    """Rows of tests/golden/rollout.npz (planner Level 0) or rollout_level1.npz (Level 1) for
+    one (level, A) config, with their subtask table."""
 
-    def __init__(self, fx, cfg: int, limit=None):
+    def __init__(self, fx, cfg: int, limit=None, planner_level: int = 0):
         sel = np.nonzero(fx["cfg"] == cfg)[0]
         if limit is not None and len(sel) > limit:
             sel = sel[np.linspace(0, len(sel) - 1, limit).astype(int)]
@@ -247,13 +248,16 @@ class RolloutRows:
                    tuple(int(m) for m in fx["start"][i]), int(fx["goal_mask"][i]), int(fx["goal_count"][i]))
             if key not in keys:
                 keys[key] = len(self.subtasks)
-                self.subtasks.append(capi.subtask(key[0], key[1], key[2], key[3], key[4]))
+                self.subtasks.append(capi.subtask(key[0], key[1], key[2], key[3], key[4], planner_level))
             self.alloc[r] = keys[key]
         self.sub_agents = [tuple(int(a) for a in fx["agents"][i] if a != PAD) for i in sel]
         self.codes = fx["action"][sel]
         self.exp_flags = (fx["legal"][sel] * capi.ROLL_LEGAL | fx["goal"][sel] * capi.ROLL_GOAL
                           | fx["assert_"][sel] * capi.ROLL_ASSERT).astype(np.uint8)
         self.exp_lb = fx["lb"][sel]
+        # rows where the reference's T raised copying a state with two co-located holders
+        # (Level 1, actions outside get_actions only): only get_actions membership is compared
+        self.copy_raise = fx["copy_raise"][sel] if "copy_raise" in fx else np.zeros(len(sel), np.int64)
         self.exp_next = fx["next"][sel]
         self.exp_vl, self.exp_vu = fx["v_l"][sel], fx["v_u"][sel]
 
@@ -264,7 +268,8 @@ class RolloutRows:
             sel = np.nonzero((self.alloc >= c0) & (self.alloc < c0 + max_sub))[0]
             part = object.__new__(RolloutRows)
             part.__dict__ = dict(self.__dict__)
-            for k in ("idx", "agents", "items", "t", "codes", "exp_flags", "exp_lb", "exp_next", "exp_vl", "exp_vu"):
+            for k in ("idx", "agents", "items", "t", "codes", "exp_flags", "exp_lb", "exp_next", "exp_vl", "exp_vu",
+                      "copy_raise"):
                 setattr(part, k, getattr(self, k)[sel])
             part.sub_agents = [self.sub_agents[i] for i in sel]
             part.alloc = (self.alloc[sel] - c0).astype(np.uint8)
@@ -285,6 +290,10 @@ class RolloutRows:
         errs = []
         c = canonical(sout, self.A, self.K, pitch, self.level.width, self.B)
         for r in range(self.B):
+            if self.copy_raise[r]:
+                if (flags[r] ^ self.exp_flags[r]) & capi.ROLL_LEGAL or self.exp_flags[r] & capi.ROLL_LEGAL:
+                    errs.append("row %d: legal flag on a raising row" % self.idx[r])
+                continue
             if flags[r] != self.exp_flags[r]:
                 errs.append("row %d: flags %d vs %d" % (self.idx[r], flags[r], self.exp_flags[r]))
                 continue
@@ -388,6 +397,9 @@ class BoundRows:
             self.row_sub[r] = keys[key]
         self.idx = sel
         self.exp_lb = fx["lb"][sel]
+        # rows where the reference's T raised copying a state with two co-located holders
+        # (Level 1, actions outside get_actions only): only get_actions membership is compared
+        self.copy_raise = fx["copy_raise"][sel] if "copy_raise" in fx else np.zeros(len(sel), np.int64)
         self.exp_doable = fx["doable"][sel].astype(np.uint8)
 
     def state(self, pitch: int) -> np.ndarray:

@@ -35,7 +35,7 @@ static void run(const oc_level_desc* lv, const uint8_t* sin, uint8_t* sout, cons
         if (ai < nsub) {
             const oc_subtask& o = subs[ai];
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
-                        {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, {0, 0}};
+                        {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
             const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
             ocro::RowOps<A, K> ops(L, dist);
             f = ops.run(r, s, c0, c1, bound);
@@ -84,7 +84,7 @@ static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* take
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
             const oc_subtask& o = subs[ai];
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
-                        {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, {0, 0}};
+                        {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
             ocro::RowOps<A, K> ops(L, dist);
             f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
         }
@@ -136,7 +136,7 @@ static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask
         for (int i = 0; i < nsub; ++i) {
             const oc_subtask& o = subs[i];
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
-                        {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, {0, 0}};
+                        {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
             float v;
             doable[i * P + e] = ops.full_bound(r, s, v) ? 1 : 0;
             lb[i * P + e] = v;

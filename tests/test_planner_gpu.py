@@ -132,3 +132,29 @@ def test_plan_batch_matches_reference_calls_in_shared_launches():
         assert batch_launches < sum(1 + len(p._succ) for p in planners)
     assert n > 0
     assert not errs, "\n".join(errs[:10])
+
+
+def test_planner_level1_matches_reference_calls():
+    """Level 1 (the Bayesian-delegation agents' call): other agents' planners are shallow
+    copies of the main planner set up for their subtasks; every recorded call reproduced."""
+    import test_planner_host as th
+    from gym_cooking_amd.planner import E2E_BRTDP, PlanEnv
+    from gym_cooking_amd import levels as _lv
+    fx = th._level1_calls()
+
+    def make_env(level_name, A, c):
+        lv = _lv.load_level(level_name)
+        K = capi.item_slots(lv)
+        P = capi.pitch_for(1)
+        s = tl.state_from_canonical(lv, A, K, P, np.array([c["agents"]], np.uint8),
+                                    np.array([c["items"]], np.uint8), np.array([c["env_t"]]))
+        return PlanEnv(lv, A, tl.env_view(s, A, K, P, 1)[:, 0], [g for g in c["groups"] if g not in _STATIC],
+                       device="cuda:0")
+
+    errs = []
+    for i, c in enumerate(fx["calls"]):
+        got, want = th.run_level1_call(fx, c, E2E_BRTDP, make_env)
+        if got != want:
+            errs.append("call %d (%s, others %s): got %s want %s" % (i, c["subtask"], c["others"], got, want))
+    assert fx["calls"]
+    assert not errs, "%d of %d calls differ:\n%s" % (len(errs), len(fx["calls"]), "\n".join(errs[:10]))

@@ -117,3 +117,44 @@ def test_host_plan_batch_matches_reference_calls():
             n += 1
     assert n > 0
     assert not errs, "\n".join(errs[:10])
+
+
+def _level1_calls():
+    path = os.path.join(tl.GOLDEN, "brtdp_level1.json")
+    if not os.path.exists(path):
+        pytest.skip("brtdp_level1.json not generated")
+    with open(path) as f:
+        return json.load(f)
+
+
+def run_level1_call(fx, c, E2E_BRTDP, make_env, **kw):
+    """One recorded Level-1 call: the other agents' planners are shallow copies of the main
+    planner set up for their subtasks (BayesianDelegator.get_other_agent_planners)."""
+    import copy
+    cfg = fx["configs"][c["cfg"]]
+    env = make_env(cfg["level"], cfg["A"], c)
+    names = env.get_agent_names()
+    p = E2E_BRTDP(**fx["params"], **kw)
+    others = {}
+    for j, sub, _, _, _ in c["others"]:
+        op = copy.copy(p)
+        op.set_settings(make_env(cfg["level"], cfg["A"], c), tg._subtask(sub), (names[j],))
+        others[names[j]] = op
+    np.random.seed(c["seed"])
+    a = p.get_next_action(env, tg._subtask(c["subtask"]), tuple(names[i] for i in c["sub_agents"]), others)
+    exp = None if c["action"] is None else (tg._NAV[c["action"][0]] if len(c["action"]) == 1
+                                            else tuple(tg._NAV[k] for k in c["action"]))
+    return (a, p.cur_obj_count, *p.start_values(), len(p.v_l)), (exp, c["goal_count"], c["v_l"], c["v_u"],
+                                                                 c["n_states"])
+
+
+def test_host_planner_level1_matches_reference_calls():
+    from gym_cooking_amd.planner import E2E_BRTDP
+    fx = _level1_calls()
+    errs = []
+    for i, c in enumerate(fx["calls"]):
+        got, want = run_level1_call(fx, c, E2E_BRTDP, _env, expander=OracleExpander)
+        if got != want:
+            errs.append("call %d (%s, others %s): got %s want %s" % (i, c["subtask"], c["others"], got, want))
+    assert fx["calls"]
+    assert not errs, "%d of %d calls differ:\n%s" % (len(errs), len(fx["calls"]), "\n".join(errs[:10]))

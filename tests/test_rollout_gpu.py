@@ -25,11 +25,12 @@ def _gpu_rollout(level, A, B, sin_host, acts_host, subs, alloc_host):
     return sout.cpu().numpy(), fl[:B].cpu().numpy(), lb[:B].cpu().numpy()
 
 
+@pytest.mark.parametrize("name,level", [("rollout.npz", 0), ("rollout_level1.npz", 1)])
 @pytest.mark.parametrize("cfg", range(5))
-def test_rollout_matches_reference_rows(cfg):
-    fx = tl.load_fixture("rollout.npz")
+def test_rollout_matches_reference_rows(name, level, cfg):
+    fx = tl.load_fixture(name)
     n = 0
-    for rows in tl.RolloutRows(fx, cfg).split(capi.MAX_SUBTASKS):
+    for rows in tl.RolloutRows(fx, cfg, planner_level=level).split(capi.MAX_SUBTASKS):
         P = capi.pitch_for(rows.B)
         sin = tl.state_from_canonical(rows.level, rows.A, rows.K, P, rows.agents, rows.items, rows.t)
         alloc = np.zeros(P, np.uint8)
@@ -43,7 +44,7 @@ def test_rollout_matches_reference_rows(cfg):
 
 def _random_case(level, A, B, seed):
     import test_rollout_host as th
-    return th.random_rollout_case(level, A, B, seed)
+    return th.random_rollout_case(level, A, B, seed, planner_levels=(0, 1))
 
 
 @pytest.mark.parametrize("level,A,B", [("open-divider_salad", 2, 5000), ("partial-divider_tl", 3, 4099),

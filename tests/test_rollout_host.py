@@ -46,10 +46,13 @@ def host_rollout(ob, sin, act, subtasks, alloc):
     return sout, flags[:ob.B], lb[:ob.B]
 
 
+@pytest.mark.parametrize("name,level", [("rollout.npz", 0), ("rollout_level1.npz", 1)])
 @pytest.mark.parametrize("cfg", range(5))
-def test_host_rollout_matches_reference_rows(cfg):
-    fx = tl.load_fixture("rollout.npz")
-    rows = tl.RolloutRows(fx, cfg)
+def test_host_rollout_matches_reference_rows(name, level, cfg):
+    if not os.path.exists(os.path.join(tl.GOLDEN, name)):
+        pytest.skip("%s not generated" % name)
+    fx = tl.load_fixture(name)
+    rows = tl.RolloutRows(fx, cfg, planner_level=level)
     ob = oracle.OracleBatch(rows.level, rows.A, 100, rows.B)
     sin = tl.state_from_canonical(rows.level, rows.A, ob.K, ob.pitch, rows.agents, rows.items, rows.t)
     alloc = np.zeros(ob.pitch, np.uint8)
@@ -59,7 +62,7 @@ def test_host_rollout_matches_reference_rows(cfg):
     assert not errs, "\n".join(errs[:20])
 
 
-def random_rollout_case(level_name, A, B, seed, steps=40):
+def random_rollout_case(level_name, A, B, seed, steps=40, planner_levels=(0,)):
     """Random mid-episode states (oracle goal-free random streams) x random subtask tables."""
     rng = np.random.default_rng(seed)
     lv = levels.load_level(level_name)
@@ -81,7 +84,7 @@ def random_rollout_case(level_name, A, B, seed, steps=40):
         ags = sorted(rng.choice(A, n, replace=False).tolist())
         kind = int(rng.integers(0, 4))
         subs.append(capi.subtask(kind, ags, [int(rng.choice(cand)), int(rng.choice(cand))], int(rng.choice(cand)),
-                                 int(rng.integers(0, 3))))
+                                 int(rng.integers(0, 3)), int(rng.choice(planner_levels))))
     alloc = rng.integers(0, len(subs), ob.pitch).astype(np.uint8)
     acts = rng.integers(0, 7, A * ob.pitch).astype(np.uint8)  # codes > 4 act as no-ops
     return ob, s, acts, subs, alloc
@@ -91,7 +94,7 @@ def random_rollout_case(level_name, A, B, seed, steps=40):
 @pytest.mark.parametrize("A", [1, 2, 3, 4])
 def test_host_rollout_matches_oracle_random(level, A):
     _load()
-    ob, s, acts, subs, alloc = random_rollout_case(level, A, 3000, seed=A * 17 + len(level))
+    ob, s, acts, subs, alloc = random_rollout_case(level, A, 3000, seed=A * 17 + len(level), planner_levels=(0, 1))
     o_out = ob.new_state()
     o_fl, o_lb = ob.rollout(s, o_out, acts, subs, alloc)
     h_out, h_fl, h_lb = host_rollout(ob, s, acts, subs, alloc)

@@ -2,6 +2,8 @@
 the rows recorded from the reference planner (tests/golden/rollout.npz, gen_rollout.py):
 legality, co-location assert, goal test, next state and lower bound, bit-exact; and the
 planner's value_init arithmetic on top of the lower bound."""
+import os
+
 import numpy as np
 import pytest
 
@@ -16,9 +18,15 @@ def fx():
     return tl.load_fixture("rollout.npz")
 
 
+FIXTURES = [("rollout.npz", 0), ("rollout_level1.npz", 1)]  # (file, planner level)
+
+
+@pytest.mark.parametrize("name,level", FIXTURES)
 @pytest.mark.parametrize("cfg", range(5))
-def test_oracle_rollout_matches_reference_rows(fx, cfg):
-    rows = tl.RolloutRows(fx, cfg)
+def test_oracle_rollout_matches_reference_rows(name, level, cfg):
+    if not os.path.exists(os.path.join(tl.GOLDEN, name)):
+        pytest.skip("%s not generated" % name)
+    rows = tl.RolloutRows(tl.load_fixture(name), cfg, planner_level=level)
     ob = oracle.OracleBatch(rows.level, rows.A, 100, rows.B)
     sin = tl.state_from_canonical(rows.level, rows.A, ob.K, ob.pitch, rows.agents, rows.items, rows.t)
     sout = ob.new_state()
