@@ -242,6 +242,24 @@ def measure_planner(dev, world) -> dict:
                 best = (dt, a, len(p.v_l), p._exp.launches)
         out[tag] = {"ms_per_call": best[0] * 1e3, "action": list(best[1]), "states": best[2],
                     "rollout_launches": best[3]}
+    # Level 1 (a Bayesian-delegation agent's call): agent-1 plans Chop(Tomato) while agent-2's
+    # planner (a shallow copy, as the delegator makes it) is believed to do Chop(Lettuce).
+    import copy as _copy
+    best = None
+    for rep in range(3):
+        p = E2E_BRTDP(alpha=0.01, tau=2, cap=75, main_cap=100, device=dev)
+        op = _copy.copy(p)
+        op.set_settings(env, recipes.Chop("Lettuce"), ("agent-2",))
+        np.random.seed(1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        a = p.get_next_action(env, recipes.Chop("Tomato"), ("agent-1",), {"agent-2": op})
+        dt = time.perf_counter() - t0
+        if best is None or dt < best[0]:
+            best = (dt, a, len(p.v_l), p._exp.launches)
+    out["level1"] = {"ms_per_call": best[0] * 1e3, "action": list(best[1]), "states": best[2],
+                     "rollout_launches": best[3], "other_planners": {"agent-2": "Chop(Lettuce)"}}
+    out["reference_seconds_survey_container"] = {"single": 0.31, "joint": 13.2, "level1": 0.58}
     out["workload"] = "C1 level open-divider_salad, reset state, Chop(Tomato), alpha 0.01 tau 2 cap 75 main_cap 100"
     out["batch"] = measure_plan_batch(dev)
     return out

@@ -40,6 +40,7 @@ import torch
 
 from . import capi
 from . import envs as _envs
+from .engine import _ptr
 from . import recipes as _recipes
 
 _NAV = [(0, 1), (0, -1), (-1, 0), (1, 0), (0, 0)]  # action codes 0..4 (World.NAV_ACTIONS + no-op)
@@ -188,11 +189,6 @@ class _Expander:
             nxt[:, self.t_plane:] = 0
             res.append((nxt, hf[r0:r0 + n].copy(), hl[r0:r0 + n].copy()))
         return res
-
-
-def _ptr(t):
-    import ctypes
-    return ctypes.c_void_p(t.data_ptr())
 
 
 class E2E_BRTDP:
