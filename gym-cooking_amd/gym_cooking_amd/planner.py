@@ -138,6 +138,20 @@ class _Expander:
         """One request: (next states [n, NP], flags [n], lower bounds [n])."""
         return self.run([(state, codes, sub)])[0]
 
+    def bounds(self, state: np.ndarray, subs):
+        """oc_subtask_bounds of one state (env_view bytes) under each configuration:
+        (lower bounds [S], doable [S])."""
+        hi = self._h_in.numpy()
+        hi[:, 0] = state
+        hi[self.t_plane:, 0] = 0
+        self.s_in.view(self.NP, self.P)[:, :1].copy_(self._h_in[:, :1])
+        S = len(subs)
+        lbt = torch.empty((S, self.P), dtype=torch.float32, device=self.eb.device)
+        okt = torch.empty((S, self.P), dtype=torch.uint8, device=self.eb.device)
+        capi.check(self.eb.lib.oc_subtask_bounds(self.eb._h, _ptr(self.s_in), capi.subtask_array(subs), S, _ptr(lbt),
+                                                 _ptr(okt), 1, self.eb._stream()))
+        return lbt[:, 0].cpu().numpy(), okt[:, 0].cpu().numpy()
+
     def run(self, requests):
         out, chunk, nrows, subs = [], [], 0, {}
         for req in requests:
@@ -221,12 +235,16 @@ class E2E_BRTDP:
         self.device = device
         self._exp = None
         self._exp_key = None
-        self._succ: Dict = {}  # (state key, subtask key) -> (actions, successors, costs, value keys)
+        self._succ: Dict = {}  # (state key, subtask key) -> [actions, successors, costs, value keys, goal flags, lower bounds, initialised]
+        self._reprs: Dict = {}  # state key -> the reference's env repr of that state (value-table key)
+        self._tmemo: Dict = {}  # this object's T memo: (repr, action) -> successor (bytes, groups)
+        self._illegal: Dict = {}  # (state key, subtask key) -> {action outside get_actions: (next bytes, flags)}
 
     # ---- configuration (set_settings, e2e_brtdp.py:582-652) --------------------------------
     def __copy__(self):  # e2e_brtdp.py:97-101: a shallow copy shares the value tables (and here the caches)
         new = object.__new__(E2E_BRTDP)
         new.__dict__ = self.__dict__.copy()
+        new._tmemo = {}  # T's lru_cache is keyed by the planner object
         return new
 
     def _configure(self, env, subtask, subtask_agent_names, other_agent_planners=None):
@@ -319,9 +337,25 @@ class E2E_BRTDP:
         Agent-Counter squares)."""
         return (s.tobytes(), groups, tuple(self._agents), self._level)
 
+    def _repr(self, key):
+        """The reference's ``env.get_repr()`` of a planner state (overcooked_environment.py:50-62):
+        the dynamic objects -- at Level 0 including the Agent-Counter squares that stand for the
+        agents outside the subtask (utils/core.py:79-87) -- and the agents present in the
+        planner's env: all of them at Level 1, the subtask agents at Level 0.  So a Level-0
+        state of every agent and the Level-1 state of the same bytes share one repr.  The value
+        tables are keyed by (repr, subtask) as the reference's are, so that planners of
+        different agent sets or levels meet in them exactly where the reference's do (the
+        delegator's planner and its copies share one table pair)."""
+        r = self._reprs.get(key)
+        if r is None:
+            sb, groups, agents, lvl = key
+            r = (sb, groups, None if lvl or len(agents) == self._exp.A else agents)
+            self._reprs[key] = r
+        return r
+
     # ---- values (value_init, e2e_brtdp.py:678-729) --------------------------------------------
     def _value_init(self, key, goal: bool, lb: float) -> None:
-        vk = (key, self._sub_key)
+        vk = (self._repr(key), self._sub_key)
         if vk in self.v_l and vk in self.v_u:
             return
         if goal:
@@ -349,11 +383,12 @@ class E2E_BRTDP:
         raw = nxt.tobytes()
         pmask = sb[m0:m0 + K]
         sk = self._sub_key
-        v_l, v_u = self.v_l, self.v_u
-        actions, succ = [], []
+        actions, succ, goals, lbs = [], [], [], []
+        illegal = {}
         for r, c in enumerate(cand):
             f = int(fl[r])
             if not f & capi.ROLL_LEGAL:
+                illegal[c] = r
                 continue
             if f & capi.ROLL_ASSERT:  # T raises (e2e_brtdp.py:143)
                 raise AssertionError("action {} led to co-located subtask agents".format(c))
@@ -363,11 +398,17 @@ class E2E_BRTDP:
                 ns = _canon(ns, A, K)
                 ng = groups | frozenset(_group_name(m) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
             nk = (ns, ng, agents, lvl)
-            if (nk, sk) not in v_l or (nk, sk) not in v_u:
-                self._value_init(nk, bool(f & capi.ROLL_GOAL), float(lb[r]))
             actions.append(c)
             succ.append(nk)
-        self._succ[(key, sk)] = (actions, succ, [_COST[c] for c in actions], [(nk, sk) for nk in succ])
+            goals.append(bool(f & capi.ROLL_GOAL))
+            lbs.append(float(lb[r]))
+        # T's value_init of a successor runs when T is first asked for it (e2e_brtdp.py:145-148):
+        # _init_succ / _init_one, so that value tables shared between planners fill in the
+        # reference's order
+        self._succ[(key, sk)] = [actions, succ, [_COST[c] for c in actions],
+                                 [(self._repr(nk), sk) for nk in succ], goals, lbs, False]
+        if illegal:  # what T would do with them (only asked for by taken_action_error)
+            self._illegal[(key, sk)] = {c: (raw[r * NP:(r + 1) * NP], int(fl[r])) for c, r in illegal.items()}
 
     def _drive(self, gen):
         """Run a search generator to completion, one launch per request."""
@@ -385,9 +426,40 @@ class E2E_BRTDP:
     def get_actions(self, key) -> List[tuple]:  # e2e_brtdp.py:151-206
         return self._expand(key)[0]
 
+    def _init_succ(self, got) -> None:
+        """value_init of every successor of an expanded state, in action order (what a pass of
+        Q over get_actions does through T)."""
+        v_l, v_u = self.v_l, self.v_u
+        for nk, vk, g, lb in zip(got[1], got[3], got[4], got[5]):
+            if vk not in v_l or vk not in v_u:
+                self._value_init(nk, g, lb)
+        got[6] = True
+
     def T(self, key, action):  # e2e_brtdp.py:103-149
-        actions, succ = self._expand(key)[:2]
-        return succ[actions.index(action)]
+        """The successor of a legal action.  The reference memoises T per planner object by
+        (state repr, action) only (``@lru_cache`` on the method), whatever subtask, agents or
+        level the object is configured for at the time: a planner reconfigured on the same
+        state -- the delegator's planner across prob_nav_actions calls -- gets the successor
+        its first configuration computed.  This T keeps that memo (per object, as the
+        reference's); such a successor is value-initialised under the current configuration
+        (Q's value_init, e2e_brtdp.py:768-770) from one no-op row of it."""
+        memo = (self._repr(key), action)
+        hit = self._tmemo.get(memo)
+        if hit is not None:
+            nk = (hit[0], hit[1], tuple(self._agents), self._level)
+            vk = (self._repr(nk), self._sub_key)
+            if vk not in self.v_l or vk not in self.v_u:
+                _, fl, lb = self._exp_run((np.frombuffer(hit[0], np.uint8), [(_NOOP,) * len(self._agents)], self._sub))
+                self._value_init(nk, bool(fl[0] & capi.ROLL_GOAL), float(lb[0]))
+            return nk
+        got = self._expand(key)
+        i = got[0].index(action)
+        if not got[6]:
+            self._value_init(got[1][i], got[4][i], got[5][i])
+        nk = got[1][i]
+        if len(self._tmemo) < 10000:  # lru_cache(maxsize=10000)
+            self._tmemo[memo] = (nk[0], nk[1])
+        return nk
 
     def cost(self, action) -> float:  # e2e_brtdp.py:816-826
         cost = self.time_cost
@@ -399,19 +471,24 @@ class E2E_BRTDP:
     def Q(self, key, action, value_f) -> float:  # e2e_brtdp.py:736-760
         cost = self.cost(action)
         nk = self.T(key, action)
-        expected_value = 1.0 * value_f[(nk, self._sub_key)]
+        expected_value = 1.0 * value_f[(self._repr(nk), self._sub_key)]
         return float(cost + expected_value)
 
     def _q_all(self, key, value_f) -> List[float]:
         """[Q(key, a, value_f) for a in get_actions(key)] in one pass (same float64 ops);
         `key` must be expanded."""
         got = self._succ[(key, self._sub_key)]
+        if not got[6]:
+            self._init_succ(got)
         return [float(c + 1.0 * value_f[vk]) for c, vk in zip(got[2], got[3])]
 
     def _expected_diff(self, key, action):  # get_expected_diff, e2e_brtdp.py:828-840
         got = self._succ[(key, self._sub_key)]
-        nk = got[1][got[0].index(action)]
-        return {nk: 1.0 * (self.v_u[(nk, self._sub_key)] - self.v_l[(nk, self._sub_key)])}
+        i = got[0].index(action)
+        if not got[6]:
+            self._value_init(got[1][i], got[4][i], got[5][i])
+        vk = got[3][i]
+        return {got[1][i]: 1.0 * (self.v_u[vk] - self.v_l[vk])}
 
     # ---- search (e2e_brtdp.py:208-331, 842-878), as generators --------------------------------
     def _sample_trial(self):  # runSampleTrial
@@ -428,26 +505,29 @@ class E2E_BRTDP:
             yield from self._need(x)
             actions = self._succ[(x, sk)][0]
             new_upper = min(self._q_all(x, self.v_u))
-            self.v_u[(x, sk)] = new_upper
+            rx = (self._repr(x), sk)
+            self.v_u[rx] = new_upper
             ql = self._q_all(x, self.v_l)
             action_index = argmin(ql, self._rng)
             a = actions[action_index]
             new_lower = ql[action_index]  # = Q(x, a, v_l): that table did not change since
-            self.v_l[(x, sk)] = new_lower
+            self.v_l[rx] = new_lower
             b = self._expected_diff(x, a)
             B = sum(b.values())
-            diff = (self.v_u[(self.start, sk)] - self.v_l[(self.start, sk)]) / self.tau
+            rs = (self._repr(self.start), sk)
+            diff = (self.v_u[rs] - self.v_l[rs]) / self.tau
             if B <= diff:
                 break
             x = list(b.keys())[0]
         while traj:
             x = traj.pop()
-            self.v_u[(x, sk)] = min(self._q_all(x, self.v_u))
-            self.v_l[(x, sk)] = min(self._q_all(x, self.v_l))
+            rx = (self._repr(x), sk)
+            self.v_u[rx] = min(self._q_all(x, self.v_u))
+            self.v_l[rx] = min(self._q_all(x, self.v_l))
 
     def _main(self):  # main
         main_counter = 0
-        sk = (self.start, self._sub_key)
+        sk = (self._repr(self.start), self._sub_key)
         diff = self.v_u[sk] - self.v_l[sk]
         while diff > self.alpha and main_counter < self.main_cap:
             diff = self.v_u[sk] - self.v_l[sk]
@@ -464,7 +544,7 @@ class E2E_BRTDP:
         action_index = argmin(self._q_all(cur, self.v_l), self._rng)
         a = actions[action_index]
         B = sum(self._expected_diff(cur, a).values())
-        sk = (cur, self._sub_key)
+        sk = (self._repr(cur), self._sub_key)
         diff = (self.v_u[sk] - self.v_l[sk]) / self.tau
         if B > diff:
             yield from self._main()
@@ -486,6 +566,38 @@ class E2E_BRTDP:
         ``None`` when the start state already satisfies the subtask."""
         return self._drive(self._next_action(env, subtask, subtask_agent_names, other_agent_planners))
 
+    def taken_action_error(self, key, action) -> Optional[type]:
+        """For an action outside get_actions(key): the exception the reference raises on
+        Q(state, action) followed by ``assert action in valid_nav_actions``
+        (bayesian_delegator.py:657-673) -- AttributeError when T's copy of the next state
+        meets two co-located agents that both hold (world.py:417), else AssertionError (T's
+        joint co-location assert, or the membership assert).  None for a legal action."""
+        self._expand(key)
+        got = self._illegal.get((key, self._sub_key), {})
+        if action not in got:
+            return None
+        if (self._repr(key), action) in self._tmemo:  # T answers from its memo; the assert raises
+            return AssertionError
+        ns, f = got[action]
+        A = self._exp.A
+        held = [(ns[a], ns[A + a]) for a in range(A) if ns[2 * A + a] != 0xFF]
+        if len(held) != len(set(held)):
+            return AttributeError
+        return AssertionError
+
+    def modified_state(self, env) -> None:
+        """_get_modified_state_with_other_agent_actions(state=env) under the planner's current
+        configuration (what BayesianDelegator.prob_nav_actions calls first, :435-459): at Level
+        1 the other agents' planners are set up on env's state and pick their actions."""
+        if not getattr(self, "_level", 0):
+            return
+        exp = self._exp
+        full = env.state_bytes()
+        full[exp.t_plane:] = 0
+        groups = frozenset(env._group_names) | frozenset(it.name for it in env.world.items)
+        key = (_canon(full.tobytes(), exp.A, exp.K), groups, tuple(self._agents), self._level)
+        self._drive(self._modified_state(key))
+
     def _modified_state(self, key):
         """_get_modified_state_with_other_agent_actions (e2e_brtdp.py:842-878) as a generator.
         Level 0: nothing.  Level 1: every other agent's planner is set up on the state (a Level-0
@@ -506,7 +618,7 @@ class E2E_BRTDP:
 
     def start_values(self) -> Tuple[float, float]:
         """(v_l, v_u) of the current start state."""
-        sk = (self.start, self._sub_key)
+        sk = (self._repr(self.start), self._sub_key)
         return self.v_l[sk], self.v_u[sk]
 
 

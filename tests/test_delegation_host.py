@@ -1,0 +1,63 @@
+"""CPU check of the Bayesian-delegation belief update over the engine
+(gym_cooking_amd.delegation.BayesianDelegator.bayes_update, Level-1 inverse planning through
+gym_cooking_amd.planner) against the reference's own updates (tests/golden/bayes.json,
+gen_bayes.py), with the CPU oracle's rollout rows and bounds standing in for the kernels
+(TEST INFRASTRUCTURE).  tests/test_delegation_gpu.py runs the same updates on the GPU."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oc_testlib as tl
+import test_planner_gpu as tg
+
+
+def load():
+    path = os.path.join(tl.GOLDEN, "bayes.json")
+    if not os.path.exists(path):
+        pytest.skip("bayes.json not generated")
+    with open(path) as f:
+        return json.load(f)
+
+
+def _alloc(rec):
+    from gym_cooking_amd.delegation import SubtaskAllocation
+    return tuple(SubtaskAllocation(None if s is None else tg._subtask(s), tuple(a)) for s, a in rec)
+
+
+def run_update(fx, c, make_env, **planner_kw):
+    """One recorded update: returns (posterior list or exception name, expected)."""
+    from gym_cooking_amd.delegation import BayesianDelegator, SubtaskAllocDistribution
+    from gym_cooking_amd.planner import E2E_BRTDP
+    cfg = fx["configs"][c["cfg"]]
+    obs = make_env(cfg["level"], cfg["A"], c)
+    names = obs.get_agent_names()
+    d = BayesianDelegator(c["self"], names, "bd", E2E_BRTDP(**fx["params"], **planner_kw), fx["none_action_prob"])
+    allocs = [_alloc(a) for a, _ in c["before"]]
+    d.probs = SubtaskAllocDistribution(allocs)
+    for k, (_, p) in zip(allocs, c["before"]):
+        d.probs.probs[k] = p
+    random.seed(c["random_seed"])
+    np.random.seed(c["np_seed"])
+    try:
+        d.bayes_update(obs_tm1=obs, actions_tm1={n: tuple(a) for n, a in c["actions"].items()}, beta=fx["beta"])
+    except (AssertionError, AttributeError) as ex:
+        return type(ex).__name__, c["raised"]
+    got = [[[[None if t.subtask is None else str(t.subtask), list(t.subtask_agent_names)] for t in k], p]
+           for k, p in d.probs.get_list()]
+    return got, c["after"] if c["raised"] is None else c["raised"]
+
+
+def test_host_bayes_update_matches_reference():
+    import test_planner_host as th
+    fx = load()
+    errs = []
+    for i, c in enumerate(fx["calls"]):
+        got, want = run_update(fx, c, th._env, expander=th.OracleExpander)
+        if got != want:
+            errs.append("update %d (cfg %d t %d self %s): got %s\n   want %s" % (i, c["cfg"], c["t"], c["self"],
+                                                                          str(got)[:300], str(want)[:300]))
+    assert fx["calls"]
+    assert not errs, "%d of %d updates differ:\n%s" % (len(errs), len(fx["calls"]), "\n".join(errs[:6]))

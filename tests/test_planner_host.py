@@ -31,6 +31,13 @@ class OracleExpander:
     def run(self, requests):
         return [self.rows(*req) for req in requests]
 
+    def bounds(self, state, subs):
+        sin = np.zeros((self.NP, self.P), np.uint8)
+        sin[:, 0] = state
+        sin[self.t_plane:, :] = 0
+        lb, ok = self.ob.subtask_bounds(sin.reshape(-1), subs, nthreads=1)
+        return lb[:, 0], ok[:, 0]
+
     def rows(self, state, codes, sub):
         n = len(codes)
         sin = np.zeros((self.NP, self.P), np.uint8)
