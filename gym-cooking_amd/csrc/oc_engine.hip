@@ -300,28 +300,28 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
             const uint32_t sa = T0 & __builtin_amdgcn_perm(0u, efull, 0x01010000u);
             const uint32_t sb2 = T1 & __builtin_amdgcn_perm(0u, efull, 0x03030202u);
             st.steps += (sa & 0xFFFFu) + (sa >> 16) + (sb2 & 0xFFFFu) + (sb2 >> 16);
-            if (has_tr) {
-                const uint32_t base = (uint32_t)r * NP * P;
+            // Unconditional stores: an absent output's descriptor has num_records 0, so its
+            // stores are dropped by the buffer range check.  Guarding them with branches made
+            // the waitcnt pass merge a store-free path into the loop back-edge and wait for
+            // every store of the step (vmcnt(0)) before taking the next step's action words.
+            const uint32_t base = (uint32_t)r * NP * P;
 #pragma unroll
-                for (int a = 0; a < A; ++a) {
-                    bst32<CP>(tr, c.wx[a], vo, base + a * P);
-                    bst32<CP>(tr, c.wy[a], vo, base + (kPY + a) * P);
-                    bst32<CP>(tr, c.wh[a], vo, base + (kPH + a) * P);
-                }
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    bst32<CP>(tr, c.wl[j], vo, base + (kPL + j) * P);
-                    bst32<CP>(tr, c.wm[j], vo, base + (kPM + j) * P);
-                }
-                const u32x2 tw = {T0, T1};
-                __builtin_amdgcn_raw_buffer_store_b64(tw, tr, (int)(g * 8u), (int)(base + kPT * P), CP);
-                bst32<CP>(tr, c.wf, vo, base + kPF * P);
+            for (int a = 0; a < A; ++a) {
+                bst32<CP>(tr, c.wx[a], vo, base + a * P);
+                bst32<CP>(tr, c.wy[a], vo, base + (kPY + a) * P);
+                bst32<CP>(tr, c.wh[a], vo, base + (kPH + a) * P);
             }
-            if (has_ex) {
 #pragma unroll
-                for (int a = 0; a < A; ++a) bst32<CP>(b.ex, ex[a], vo, (uint32_t)(r * A + a) * P);
+            for (int j = 0; j < K; ++j) {
+                bst32<CP>(tr, c.wl[j], vo, base + (kPL + j) * P);
+                bst32<CP>(tr, c.wm[j], vo, base + (kPM + j) * P);
             }
-            if (has_coll) bst32<CP>(b.coll, cm, vo, (uint32_t)r * P);
+            const u32x2 tw = {T0, T1};
+            __builtin_amdgcn_raw_buffer_store_b64(tw, tr, (int)(g * 8u), (int)(base + kPT * P), CP);
+            bst32<CP>(tr, c.wf, vo, base + kPF * P);
+#pragma unroll
+            for (int a = 0; a < A; ++a) bst32<CP>(b.ex, ex[a], vo, (uint32_t)(r * A + a) * P);
+            bst32<CP>(b.coll, cm, vo, (uint32_t)r * P);
         }
 #pragma unroll
         for (int a = 0; a < A; ++a) {

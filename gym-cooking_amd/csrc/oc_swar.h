@@ -144,7 +144,7 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
     for (int a = 0; a < A; ++a) {
         uint32_t c = ACT[a];
         const uint32_t ge5 = bop3<OC_LUT((a | b) & c)>((c & k7F) + 0x7B7B7B7Bu, c, k80);
-        if (ge5 != 0u) c = sel(full80(ge5), k04, c);  // codes > 4 act as (0, 0)
+        c = sel(full80(ge5), k04, c);  // codes > 4 act as (0, 0)
         act[a] = c;
         nn80[a] = nz80(c ^ k04);
         uint32_t yw;
@@ -242,15 +242,17 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         const uint32_t newHm = sel(fmg, cu, sel(full80(chop), chopped, hm));
         // scatter: target slot on merge / pick, held slot on reloc / merge / chop.  The per-slot
         // select masks are one v_perm each: selector byte = slot index (h, or the target slot
-        // oidx), table byte j = 0xFF; a holding-none h = 0xFF selects 0xFF and is masked off.
+        // oidx), table byte j = 0xFF.  Envs that write no slot get selector 0x0C, which v_perm
+        // turns into a zero byte (a holding-none h = 0xFF never writes: fwh includes hold80).
         const uint32_t oidx = (ob0 >> 7) | (ob1 >> 6) | (ob2 >> 5);
         const uint32_t fwo = full80(merge | pick);
         const uint32_t fwh = full80(and3(hold80, or3(reloc, merge, chop), k80));
+        const uint32_t so = sel(fwo, oidx, 0x0C0C0C0Cu), shw = sel(fwh, h, 0x0C0C0C0Cu);
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const uint32_t lut_lo = j < 4 ? 0xFFu << (8 * j) : 0u, lut_hi = j < 4 ? 0u : 0xFFu << (8 * (j - 4));
-            const uint32_t eo = perm(lut_hi, lut_lo, oidx) & fwo;
-            const uint32_t eh = perm(lut_hi, lut_lo, h) & fwh;
+            const uint32_t eo = perm(lut_hi, lut_lo, so);
+            const uint32_t eh = perm(lut_hi, lut_lo, shw);
             Lc[j] = sel(eh, newHl, sel(eo, newOl, Lc[j]));
             M[j] = sel(eh, newHm, sel(eo, newOm, M[j]));
         }
