@@ -403,8 +403,8 @@ class E2E_BRTDP:
             goals.append(bool(f & capi.ROLL_GOAL))
             lbs.append(float(lb[r]))
         # T's value_init of a successor runs when T is first asked for it (e2e_brtdp.py:145-148):
-        # _init_succ / _init_one, so that value tables shared between planners fill in the
-        # reference's order
+        # all of them by _init_succ on the first full Q pass, one by T / _expected_diff before
+        # that, so that value tables shared between planners fill in the reference's order
         self._succ[(key, sk)] = [actions, succ, [_COST[c] for c in actions],
                                  [(self._repr(nk), sk) for nk in succ], goals, lbs, False]
         if illegal:  # what T would do with them (only asked for by taken_action_error)
