@@ -646,18 +646,23 @@ class PlanEnv:
         return self._bytes.copy()
 
 
-def plan_batch(planners: Sequence[E2E_BRTDP], envs_, subtasks, agent_names) -> list:
-    """get_next_action of many independent Level-0 searches at once: planner i plans
-    `subtasks[i]` for `agent_names[i]` in `envs_[i]`.  The searches run in lockstep; every
-    round, the states all of them need expanded go to the GPU in shared oc_rollout launches
-    (up to 4,096 rows and 64 subtask configurations each), so the number of launches is about
-    that of the longest single search.  Each search gives exactly its sequential result when
-    its planner has its own generator (``rng=np.random.RandomState(seed)``).  All planners must
-    share one level and agent count; they share the first planner's expander."""
+def plan_batch(planners: Sequence[E2E_BRTDP], envs_, subtasks, agent_names, other_agent_planners=None) -> list:
+    """get_next_action of many independent searches at once: planner i plans `subtasks[i]` for
+    `agent_names[i]` in `envs_[i]`, at Level 0, or at Level 1 with `other_agent_planners[i]`
+    (a dict of the other agents' planners, as get_next_action takes; None or {} for Level 0).
+    The searches run in lockstep; every round, the states all of them need expanded -- their
+    own and, at Level 1, their other agents' planners' -- go to the GPU in shared oc_rollout
+    launches (up to 4,096 rows and 64 subtask configurations each), so the number of launches
+    is about that of the longest single search.  Each search gives exactly its sequential
+    result when its planner has its own generator (``rng=np.random.RandomState(seed)``; its
+    other agents' planners draw from the same one).  All planners must share one level and
+    agent count; they share the first planner's expander."""
     assert len(planners) == len(envs_) == len(subtasks) == len(agent_names)
     if not planners:
         return []
-    gens = [p._next_action(e, st, an, None) for p, e, st, an in zip(planners, envs_, subtasks, agent_names)]
+    others = other_agent_planners or [None] * len(planners)
+    assert len(others) == len(planners)
+    gens = [p._next_action(e, st, an, o) for p, e, st, an, o in zip(planners, envs_, subtasks, agent_names, others)]
     out = [None] * len(gens)
     pending = {}
     exp = None

@@ -158,3 +158,27 @@ def test_planner_level1_matches_reference_calls():
             errs.append("call %d (%s, others %s): got %s want %s" % (i, c["subtask"], c["others"], got, want))
     assert fx["calls"]
     assert not errs, "%d of %d calls differ:\n%s" % (len(errs), len(fx["calls"]), "\n".join(errs[:10]))
+
+
+def test_plan_batch_level1_matches_reference_calls():
+    """Level-1 searches in lockstep (plan_batch with other agents' planners): every recorded
+    Level-1 call reproduced, the other agents' planners' expansions sharing the launches."""
+    import time
+    import test_planner_host as th
+    from gym_cooking_amd.planner import PlanEnv
+    from gym_cooking_amd import levels as _lv
+    fx = th._level1_calls()
+
+    def make_env(level_name, A, c):
+        lv = _lv.load_level(level_name)
+        K = capi.item_slots(lv)
+        P = capi.pitch_for(1)
+        s = tl.state_from_canonical(lv, A, K, P, np.array([c["agents"]], np.uint8),
+                                    np.array([c["items"]], np.uint8), np.array([c["env_t"]]))
+        return PlanEnv(lv, A, tl.env_view(s, A, K, P, 1)[:, 0], [g for g in c["groups"] if g not in _STATIC],
+                       device="cuda:0")
+
+    t0 = time.perf_counter()
+    errs = th.level1_batch(fx, make_env)
+    print("\n%d Level-1 searches in batches per config: %.2f s" % (len(fx["calls"]), time.perf_counter() - t0))
+    assert not errs, "\n".join(errs[:10])

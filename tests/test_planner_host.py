@@ -155,6 +155,48 @@ def run_level1_call(fx, c, E2E_BRTDP, make_env, **kw):
                                                                  c["n_states"])
 
 
+def level1_batch(fx, make_env, **kw):
+    """Every recorded Level-1 call as one plan_batch per config (each search with its own
+    RandomState(seed), its other agents' planners copies of its planner); returns the list of
+    mismatches."""
+    import copy
+    from gym_cooking_amd.planner import E2E_BRTDP, plan_batch
+    errs = []
+    for cfg_i, cfg in enumerate(fx["configs"]):
+        calls = [c for c in fx["calls"] if c["cfg"] == cfg_i]
+        if not calls:
+            continue
+        planners, envs_, subs, agn, others = [], [], [], [], []
+        for c in calls:
+            env = make_env(cfg["level"], cfg["A"], c)
+            names = env.get_agent_names()
+            p = E2E_BRTDP(**fx["params"], rng=np.random.RandomState(c["seed"]), **kw)
+            o = {}
+            for j, sub, _, _, _ in c["others"]:
+                op = copy.copy(p)
+                op.set_settings(make_env(cfg["level"], cfg["A"], c), tg._subtask(sub), (names[j],))
+                o[names[j]] = op
+            planners.append(p)
+            envs_.append(env)
+            subs.append(tg._subtask(c["subtask"]))
+            agn.append(tuple(names[i] for i in c["sub_agents"]))
+            others.append(o)
+        got = plan_batch(planners, envs_, subs, agn, others)
+        for p, a, c in zip(planners, got, calls):
+            exp = None if c["action"] is None else (tg._NAV[c["action"][0]] if len(c["action"]) == 1
+                                                    else tuple(tg._NAV[k] for k in c["action"]))
+            if (a, p.cur_obj_count, *p.start_values(), len(p.v_l)) != (exp, c["goal_count"], c["v_l"], c["v_u"],
+                                                                        c["n_states"]):
+                errs.append("%s %s others %s: %s vs %s" % (cfg["level"], c["subtask"], c["others"], a, exp))
+    return errs
+
+
+def test_host_plan_batch_level1_matches_reference_calls():
+    fx = _level1_calls()
+    errs = level1_batch(fx, _env, expander=OracleExpander)
+    assert not errs, "\n".join(errs[:10])
+
+
 def test_host_planner_level1_matches_reference_calls():
     from gym_cooking_amd.planner import E2E_BRTDP
     fx = _level1_calls()
