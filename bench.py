@@ -420,22 +420,26 @@ def main() -> int:
     n_per = -(-K // n_launch)
     segs = [(i, min(n_per, K - i)) for i in range(0, K, n_per)]
     # outputs of one launch (every step's state, executed actions, collision mask), reused per launch
-    traj = torch.empty(n_per * S, dtype=torch.uint8, device=dev)
-    ex_all = torch.empty(n_per * A * P, dtype=torch.uint8, device=dev)
-    coll_all = torch.empty(n_per * P, dtype=torch.uint8, device=dev)
+    # two output sets, alternated between consecutive launches (OC_BENCH_OUT_SETS=1: one set reused)
+    n_sets = int(os.environ.get("OC_BENCH_OUT_SETS", "2"))
+    outs = [(torch.empty(n_per * S, dtype=torch.uint8, device=dev),
+             torch.empty(n_per * A * P, dtype=torch.uint8, device=dev),
+             torch.empty(n_per * P, dtype=torch.uint8, device=dev)) for _ in range(n_sets)]
     s_a, s_b = eb.new_state(), eb.new_state()
     stats = eb.new_stats()
 
     def run(n_steps_total, first=0):
         src, dst = s_a, s_b
-        done = 0
+        done, li = 0, 0
         while done < n_steps_total:
             n = min(n_per, n_steps_total - done)
             i0 = (first + done) % K
             n = min(n, K - i0)
+            traj, ex_all, coll_all = outs[li % n_sets]
             eb.step_n(src, dst, acts[i0:i0 + n].reshape(-1), n, traj, ex_all, coll_all, stats)
             src, dst = dst, src
             done += n
+            li += 1
         return src
 
     # warmup: W untimed steps, rounded up to whole launches of the timed length so that every
