@@ -205,6 +205,24 @@ class _Expander:
         return res
 
 
+def _copy_crashes(sb: bytes, A: int) -> bool:
+    """Two agents on one square that both hold an item: the reference's copy of such a state
+    raises (overcooked_environment.py:108-113 -> world.py:417).  At Level 1 every agent is in the
+    planner's env, so T's repr_init copy of a successor like that raises (e2e_brtdp.py:147)."""
+    for i in range(A):
+        if sb[2 * A + i] == 0xFF:
+            continue
+        for j in range(i + 1, A):
+            if sb[2 * A + j] != 0xFF and sb[i] == sb[j] and sb[A + i] == sb[A + j]:
+                return True
+    return False
+
+
+def _raise_copy_crash(action):
+    raise AttributeError("T{}: the next state has two co-located agents holding items; the reference's "
+                         "copy of it raises (world.py:417)".format(action))
+
+
 class E2E_BRTDP:
     """Bounded RTDP navigation planner (e2e_brtdp.py:38-878), Levels 0 and 1, over the HIP engine.
 
@@ -385,6 +403,7 @@ class E2E_BRTDP:
         sk = self._sub_key
         actions, succ, goals, lbs = [], [], [], []
         illegal = {}
+        crash = None
         for r, c in enumerate(cand):
             f = int(fl[r])
             if not f & capi.ROLL_LEGAL:
@@ -398,6 +417,9 @@ class E2E_BRTDP:
                 ns = _canon(ns, A, K)
                 ng = groups | frozenset(_group_name(m) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
             nk = (ns, ng, agents, lvl)
+            if lvl and _copy_crashes(ns, A):
+                crash = crash or set()
+                crash.add(len(actions))
             actions.append(c)
             succ.append(nk)
             goals.append(bool(f & capi.ROLL_GOAL))
@@ -406,7 +428,7 @@ class E2E_BRTDP:
         # all of them by _init_succ on the first full Q pass, one by T / _expected_diff before
         # that, so that value tables shared between planners fill in the reference's order
         self._succ[(key, sk)] = [actions, succ, [_COST[c] for c in actions],
-                                 [(self._repr(nk), sk) for nk in succ], goals, lbs, False]
+                                 [(self._repr(nk), sk) for nk in succ], goals, lbs, False, crash]
         if illegal:  # what T would do with them (only asked for by taken_action_error)
             self._illegal[(key, sk)] = {c: (raw[r * NP:(r + 1) * NP], int(fl[r])) for c, r in illegal.items()}
 
@@ -429,6 +451,8 @@ class E2E_BRTDP:
     def _init_succ(self, got) -> None:
         """value_init of every successor of an expanded state, in action order (what a pass of
         Q over get_actions does through T)."""
+        if got[7]:
+            _raise_copy_crash(got[0][min(got[7])])
         v_l, v_u = self.v_l, self.v_u
         for nk, vk, g, lb in zip(got[1], got[3], got[4], got[5]):
             if vk not in v_l or vk not in v_u:
@@ -446,6 +470,8 @@ class E2E_BRTDP:
         memo = (self._repr(key), action)
         hit = self._tmemo.get(memo)
         if hit is not None:
+            if self._level and _copy_crashes(hit[0], self._exp.A):
+                _raise_copy_crash(action)
             nk = (hit[0], hit[1], tuple(self._agents), self._level)
             vk = (self._repr(nk), self._sub_key)
             if vk not in self.v_l or vk not in self.v_u:
@@ -454,6 +480,8 @@ class E2E_BRTDP:
             return nk
         got = self._expand(key)
         i = got[0].index(action)
+        if got[7] and i in got[7]:
+            _raise_copy_crash(action)
         if not got[6]:
             self._value_init(got[1][i], got[4][i], got[5][i])
         nk = got[1][i]
@@ -485,6 +513,8 @@ class E2E_BRTDP:
     def _expected_diff(self, key, action):  # get_expected_diff, e2e_brtdp.py:828-840
         got = self._succ[(key, self._sub_key)]
         i = got[0].index(action)
+        if got[7] and i in got[7]:
+            _raise_copy_crash(action)
         if not got[6]:
             self._value_init(got[1][i], got[4][i], got[5][i])
         vk = got[3][i]

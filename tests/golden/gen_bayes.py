@@ -38,6 +38,8 @@ CONFIGS = [  # (level, A, seed, steps)
     ("open-divider_salad", 2, 6100, 30),
     ("partial-divider_tomato", 2, 6200, 30),
     ("open-divider_tl", 3, 6300, 18),
+    ("partial-divider_salad", 3, 6500, 24),
+    ("full-divider_salad", 4, 6400, 16),
 ]
 SAMPLE_EVERY = 2
 BETA, NONE_P = 1.3, 0.5
