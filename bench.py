@@ -16,7 +16,8 @@ as "per_step_launch".  The timed region is bracketed by a barrier + synchronize 
 sides; the per-GPU episode summaries are all-gathered (RCCL) inside it.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
-      (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+      N>1 starts N ranks itself (children of torch.distributed.run on 127.0.0.1); under an
+      external torchrun (WORLD_SIZE set) it runs as the given rank.
 """
 from __future__ import annotations
 
@@ -207,14 +208,29 @@ def measure_render(dev, world, level: str, A: int, B: int = 1024, reps: int = 10
             "frac_hbm": gbs / HBM_PEAK_GBS, "bound": "hbm (writes)"}
 
 
-def load_traffic(path: str, kernel: str = "oc_step_n_kernel"):
-    """Calibrated HBM bytes per launch of `kernel` from tools/pmc_report.py's output."""
+def load_traffic(path: str, kernel: str = "oc_step_n_kernel", steps_per_launch=None, algorithmic=None):
+    """Calibrated HBM bytes per launch of `kernel` (tools/pmc_report.py's output) for the timed
+    launch shape: the PMC record of exactly `steps_per_launch` steps when profiles/ holds one,
+    else the nearest recorded shape's traffic/algorithmic ratio applied to this launch's
+    algorithmic bytes (the source says so).  Returns (bytes or None, source)."""
     try:
         with open(path) as f:
             d = json.load(f)
-        return d[kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+        k = d[kernel]
     except (OSError, ValueError, KeyError):
         return None, None
+    src = os.path.relpath(path, ROOT)
+    if steps_per_launch is None:
+        return k["hbm_bytes_per_launch"], src
+    shapes = {int(n): v for n, v in k.get("by_steps_per_launch", {}).items()}
+    if steps_per_launch in shapes:
+        return shapes[steps_per_launch]["hbm_bytes_per_launch"], "%s [%s, %d steps/launch]" % (src, kernel,
+                                                                                               steps_per_launch)
+    if not shapes or algorithmic is None:
+        return None, None
+    n0 = min(shapes, key=lambda n: abs(n - steps_per_launch))
+    return (shapes[n0]["ratio"] * algorithmic,
+            "%s [%s, ratio of the %d-step record x this launch's algorithmic bytes]" % (src, kernel, n0))
 
 
 def measure_planner(dev, world) -> dict:
@@ -377,6 +393,64 @@ def per_step_launch(eb, acts, n_act, W, dev, world, use_graph=True) -> dict:
             "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS}
 
 
+def host_cores() -> dict:
+    """The host cores this job may use: the CPU affinity set, capped by the cgroup CPU quota
+    and by OMP_NUM_THREADS when the box sets it (the GPU pool gives each GPU's job a share of
+    the machine: nproc there shows every core of the host, not the share)."""
+    nproc = os.cpu_count() or 1
+    share, limits = nproc, {"nproc": nproc}
+    try:
+        share = len(os.sched_getaffinity(0))
+        limits["affinity"] = share
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, -(-int(q) // int(per)))
+            limits["cgroup_quota"] = quota
+            share = min(share, quota)
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        limits["OMP_NUM_THREADS"] = omp
+        share = min(share, omp)
+    return {"threads": share, "limits": limits}
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` outside torchrun: start the N ranks as child processes of
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and exit with their
+    status.  The parent never touches the GPU, and nothing is exec'd: the ranks are fresh
+    processes, rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def selftest_ranks(args) -> int:
+    """--selftest-ranks: the launcher and shard/all-gather plumbing on gloo without any GPU
+    work (tests/test_bench_launcher.py): every rank reports its shard, rank 0 prints them."""
+    rank, world, local = ocdist.world_from_env()
+    ocdist.init("gloo")
+    sh = ocdist.shard(args.batch, rank, world, local)
+    g = ocdist.gather_summaries(torch.tensor([rank, world, sh.env_offset, sh.batch, os.getpid()]))
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks": g.tolist()}), flush=True)
+    if torch.distributed.is_initialized():
+        torch.distributed.destroy_process_group()
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -388,6 +462,7 @@ def main() -> int:
     ap.add_argument("--max-T", type=int, default=100)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--steps-per-launch", type=int, default=100, help="oc_step_n launch length (headline)")
+    ap.add_argument("--min-warmup-ms", type=float, default=50.0, help="repeat the untimed warmup for at least this long")
     ap.add_argument("--no-graph", action="store_true", help="per-step line: eager launches instead of a hipGraph")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -397,11 +472,16 @@ def main() -> int:
     ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 (3-agent full-divider_tl) line")
     ap.add_argument("--no-planner", action="store_true", help="skip the secondary navigation-planner line")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--selftest-ranks", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
     rank, world, local = ocdist.world_from_env()
     if world != args.gpus:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    if args.selftest_ranks:
+        return selftest_ranks(args)
     ocdist.init("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -427,42 +507,55 @@ def main() -> int:
              torch.empty(n_per * P, dtype=torch.uint8, device=dev)) for _ in range(n_sets)]
     s_a, s_b = eb.new_state(), eb.new_state()
     stats = eb.new_stats()
+    totals = torch.zeros(5, dtype=torch.int64, device=dev)
 
-    def run(n_steps_total, first=0):
-        src, dst = s_a, s_b
-        done, li = 0, 0
+    def plan(n_steps_total):
+        """The launches of a window, bound once (engine.step_n_launcher: buffers validated
+        here, each launch is then one ctypes call).  The last launch also folds the episode
+        statistics into `totals` (in-launch, no separate reduce kernel)."""
+        out, src, dst, done, li = [], s_a, s_b, 0, 0
         while done < n_steps_total:
             n = min(n_per, n_steps_total - done)
-            i0 = (first + done) % K
+            i0 = done % K
             n = min(n, K - i0)
             traj, ex_all, coll_all = outs[li % n_sets]
-            eb.step_n(src, dst, acts[i0:i0 + n].reshape(-1), n, traj, ex_all, coll_all, stats)
+            last = done + n >= n_steps_total
+            out.append(eb.step_n_launcher(src, dst, acts[i0:i0 + n].reshape(-1), n, traj, ex_all, coll_all, stats,
+                                          totals if last else None))
             src, dst = dst, src
             done += n
             li += 1
-        return src
+        return out
 
-    # warmup: W untimed steps, rounded up to whole launches of the timed length so that every
-    # oc_step_n launch a profiler sees has the timed shape (plus the summary path: reduce + all-gather)
-    warm_steps = -(-max(W, 1) // n_per) * n_per
-    eb.reset(s_a)
-    run(warm_steps)
-    ocdist.gather_summaries(eb.reduce_stats(stats))
-    torch.cuda.synchronize()
+    timed = plan(K)
+    # warmup: at least W untimed steps, rounded up to whole launches of the timed length (every
+    # oc_step_n launch a profiler sees has the timed shape, summary path included), and repeated
+    # for at least --min-warmup-ms so that the clocks have left their idle state
+    warm = plan(-(-max(W, 1) // n_per) * n_per)
+    warm_steps, t_w = 0, time.perf_counter()
+    while True:
+        eb.reset(s_a)
+        for f in warm:
+            f()
+        ocdist.gather_summaries(totals)
+        torch.cuda.synchronize()
+        warm_steps += len(warm) * n_per
+        if warm_steps >= W and (time.perf_counter() - t_w) * 1e3 >= args.min_warmup_ms:
+            break
     eb.reset(s_a)
     stats.zero_()
+    torch.cuda.synchronize()
 
     # ---------------- timed region ----------------
     ocdist.barrier()
     torch.cuda.synchronize()
-    ev0, ev1, ev2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
-    run(K)
+    for f in timed:
+        f()
     ev1.record()
-    totals = eb.reduce_stats(stats)
     gathered = ocdist.gather_summaries(totals)
-    ev2.record()
     torch.cuda.synchronize()
     ocdist.barrier()
     elapsed = time.perf_counter() - t0
@@ -472,19 +565,21 @@ def main() -> int:
     summary = ocdist.summarize(gathered)
 
     # Dominant kernel: oc_step_n_kernel; HIP events on its launch stream bracket the timed
-    # launches (back to back), so window / launches = its mean duration.
+    # launches (back to back, the last one's in-launch statistics fold included), so
+    # window / launches = its mean duration.
     kern_ms = steps_ms / len(segs)
     nS = eb.layout.num_planes  # state bytes per env (the u16 t counts 2)
     bytes_launch = (nS + n_per * (nS + 2 * A + 1)) * sh.batch
     bytes_env_step = bytes_launch / (n_per * sh.batch)
     achieved_gbs = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(args.traffic_json)
+    traffic, traffic_src = load_traffic(args.traffic_json, "oc_step_n_kernel", n_per, bytes_launch)
     value = world * sh.batch * K / elapsed_max
     line = {
         "metric": METRIC,
         "value": value,
         "unit": "env-steps/s",
         "n_gpus": world,
+        "rccl_ranks": world if torch.distributed.is_initialized() else 0,
         "steps": K,
         "warmup": W,
         "ms_per_step": elapsed_max * 1e3 / K,
@@ -509,7 +604,6 @@ def main() -> int:
             "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_env_step": bytes_env_step,
             "kernel_ms_mean": kern_ms, "traffic_source": traffic_src,
         },
-        "gpu_ms_timed_region": ev0.elapsed_time(ev2),
         "episodes": summary,
     }
     if not args.no_per_step:
@@ -525,8 +619,10 @@ def main() -> int:
     if not args.no_planner:
         line["planner"] = measure_planner(dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget, threads)
+        hc = host_cores()
+        line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget,
+                                            hc["threads"])
+        line["cpu_baseline"]["host_cpu_limits"] = hc["limits"]
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:

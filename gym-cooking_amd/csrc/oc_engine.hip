@@ -247,7 +247,8 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
                                                            const uint8_t* __restrict__ actions,
                                                            uint8_t* __restrict__ traj, uint8_t* __restrict__ exec_out,
                                                            uint8_t* __restrict__ coll_out,
-                                                           uint64_t* __restrict__ stats, int n) {
+                                                           uint64_t* __restrict__ stats, uint64_t* __restrict__ totals,
+                                                           uint32_t stat_rows, int n) {
     __shared__ uint8_t tbl[256];
     tbl[threadIdx.x] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, threadIdx.x);
     __syncthreads();
@@ -341,11 +342,40 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
     if (stats != nullptr) {
         const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
                                        wave_sum(st.err)};
+        unsigned long long* const part = (unsigned long long*)stats;
+        uint32_t ticket = 0u;
         if ((threadIdx.x & 63u) == 0u) {
-            unsigned long long* row = (unsigned long long*)stats + (int64_t)blockIdx.x * OC_NSTATS;
+            unsigned long long* row = part + (int64_t)(blockIdx.x % stat_rows) * OC_NSTATS;
 #pragma unroll
             for (int c = 0; c < OC_NSTATS; ++c)
                 if (v[c]) atomicAdd(row + c, (unsigned long long)v[c]);
+            if (totals != nullptr) {
+                // This wave's adds are performed (vmcnt drained: atomics execute at the memory
+                // side, MI355X_MICROARCH.md "Global float atomics") before it takes a ticket; the
+                // wave holding the last ticket has every wave's adds in the partial rows.
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                ticket = (uint32_t)atomicAdd(part + (int64_t)stat_rows * OC_NSTATS, 1ull);
+            }
+        }
+        const uint32_t nwaves = gridDim.x * (uint32_t)(kBlock / 64);
+        if (totals != nullptr && (uint32_t)__builtin_amdgcn_readfirstlane((int)ticket) == nwaves - 1u) {
+            // Last wave: fold the partial rows into totals (what oc_stats_reduce does after the
+            // launch).  The rows are read with returning atomics, which are served at the memory
+            // side, so no XCD's L2 can hand back a stale copy.
+            const uint32_t lane = threadIdx.x & 63u;
+            unsigned long long acc[OC_NSTATS] = {0ull, 0ull, 0ull, 0ull, 0ull};
+            for (uint32_t r = lane; r < stat_rows; r += 64u) {
+#pragma unroll
+                for (int c = 0; c < OC_NSTATS; ++c) acc[c] += atomicAdd(part + (int64_t)r * OC_NSTATS + c, 0ull);
+            }
+#pragma unroll
+            for (int c = 0; c < OC_NSTATS; ++c)
+                for (int off = 32; off > 0; off >>= 1) acc[c] += __shfl_xor(acc[c], off);
+            if (lane == 0u) {
+#pragma unroll
+                for (int c = 0; c < OC_NSTATS; ++c) totals[c] = acc[c];
+                atomicExch(part + (int64_t)stat_rows * OC_NSTATS, 0ull);  // ticket ready for the next launch
+            }
         }
     }
 }
@@ -767,8 +797,9 @@ int hip_check(const char* what) {
     return OC_OK;
 }
 
-// MI355X: 256 CUs (persistent grids of the multi-step, rollout and likelihood kernels).
-constexpr int kCUs = 256;
+// Statistics rows: blocks add into row blockIdx % rows (no-return 64-bit atomics); 256 rows
+// keep the adds to one address to a few dozen per launch and let one wave fold them.
+constexpr int64_t kStatRows = 256;
 
 
 int64_t pitch_for(int64_t B) {
@@ -781,17 +812,18 @@ int64_t pitch_for(int64_t B) {
 struct oc_handle {
     oc_level_desc level;
     int32_t A, K, max_T, device;
+    int32_t cus;                // compute units of the device (persistent grids: <= 5 blocks per CU)
     LevelArgs args;
     ocro::RollLevel roll;       // planner rollout tables (nnodes < 0: graph too large)
     uint8_t* roll_dist = nullptr;  // device: reachability distances [kMaxNodes][kMaxNodes]
     uint8_t roll_dist_host[ocro::kMaxNodes * ocro::kMaxNodes];  // the same table on the host
 };
 
-// Statistics rows: one per block of the oc_step_n grid; oc_step's blocks share them modulo
-// the row count (atomics).
+// Statistics rows, shared by the blocks of every kernel modulo the row count; one more
+// uint64 after them is oc_step_n's ticket counter (zero between launches).
 int64_t stats_rows(const oc_handle*, int64_t B) {
-    const int64_t need = pitch_for(B) / kEnvsPerBlock, cap = (int64_t)kCUs * 5;
-    return need < cap ? need : cap;
+    const int64_t need = pitch_for(B) / kEnvsPerBlock;
+    return need < kStatRows ? need : kStatRows;
 }
 
 extern "C" {
@@ -868,6 +900,14 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     h->max_T = max_T;
     h->device = device;
     h->args = L;
+    h->cus = 256;  // MI355X; replaced by the device's own count when there is a device
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            h->cus = cus;
+        else
+            (void)hipGetLastError();
+    }
     // planner rollout: the static reachability graph's BFS table (world.py:67-108)
     {
         uint8_t* dist = h->roll_dist_host;
@@ -979,10 +1019,13 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
 }
 
 int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions, void* traj,
-              uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, int64_t B, int32_t n, void* stream) {
+              uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, uint64_t* totals, int64_t B, int32_t n,
+              void* stream) {
     if (h == nullptr || state_in == nullptr || state_out == nullptr || actions == nullptr || B < 0 || n < 0)
         return fail(OC_EINVAL, "bad argument");
-    if (B == 0 || n == 0) return OC_OK;
+    if (totals != nullptr && stats == nullptr) return fail(OC_EINVAL, "totals need the stats buffer");
+    if (totals != nullptr && (uintptr_t)totals & 7u) return fail(OC_EINVAL, "totals must be 8-byte aligned");
+    if (B == 0 || n == 0) return totals != nullptr && B > 0 ? oc_stats_reduce(h, stats, B, totals, stream) : OC_OK;
     if (((uintptr_t)state_in | (uintptr_t)state_out | (uintptr_t)actions | (uintptr_t)traj | (uintptr_t)exec_actions |
          (uintptr_t)coll_mask) & 15u)
         return fail(OC_EINVAL, "buffers must be 16-byte aligned");
@@ -996,9 +1039,10 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
     int64_t per = ((1ll << 31) - 1) / (NP * L.pitch);
     if (per > 4096) per = 4096;
     per = (n + (n + per - 1) / per - 1) / ((n + per - 1) / per);  // equal launches
-    const int64_t need = L.pitch / kEnvsPerBlock, cap = (int64_t)kCUs * 5;  // <= 5 waves/SIMD resident
+    const int64_t need = L.pitch / kEnvsPerBlock, cap = (int64_t)h->cus * 5;  // <= 5 waves/SIMD resident
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t s = (hipStream_t)stream;
+    const uint32_t rows = (uint32_t)stats_rows(h, B);
     const uint8_t* src = (const uint8_t*)state_in;
     for (int64_t r0 = 0; r0 < n; r0 += per) {
         const int m = (int)(n - r0 < per ? n - r0 : per);
@@ -1009,7 +1053,7 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
         const uint8_t* ac = actions + off * h->A * L.pitch;
 #define OC_LAUNCH_STEPN(A, K)                                                                                     \
     hipLaunchKernelGGL((oc_step_n_kernel<A, K, kCPnt>), grid, dim3(kBlock), 0, s, L, src, (uint8_t*)state_out, ac, tr, ex, cm, \
-                       stats, m)
+                       stats, totals, rows, m)
         OC_DISPATCH(h->A, h->K, OC_LAUNCH_STEPN)
         src = (const uint8_t*)state_out;
         if (const int rc = hip_check("oc_step_n launch")) return rc;
@@ -1065,7 +1109,7 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     RollArgs R;
     if (const int rc = roll_args(h, subtasks, num_subtasks, B, R, true)) return rc;
     if (B == 0) return OC_OK;
-    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)kCUs * 8;
+    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_ROLL(A, K)                                                                                 \
@@ -1086,7 +1130,7 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     RollArgs R;
     if (const int rc = roll_args(h, subtasks, num_subtasks, B, R)) return rc;
     if (B == 0) return OC_OK;
-    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)kCUs * 8;
+    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_LIK(A, K)                                                                                     \
@@ -1105,7 +1149,7 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
     RollArgs R;
     if (const int rc = roll_args(h, subtasks, num_subtasks, B, R)) return rc;
     if (B == 0) return OC_OK;
-    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)kCUs * 8;
+    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_BOUNDS(A, K)                                                                             \
@@ -1192,7 +1236,7 @@ int oc_state_checksum(const oc_handle* h, const void* state, int64_t B, uint64_t
 
 int oc_stats_size(const oc_handle* h, int64_t B, int64_t* nbytes) {
     if (h == nullptr || nbytes == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
-    *nbytes = stats_rows(h, B) * OC_NSTATS * (int64_t)sizeof(uint64_t);
+    *nbytes = (stats_rows(h, B) * OC_NSTATS + 1) * (int64_t)sizeof(uint64_t);  // + oc_step_n's ticket
     return OC_OK;
 }
 

@@ -20,6 +20,7 @@ OC_MAX_CELLS = 64
 OC_MAX_GOALS = 4
 OC_PITCH_ALIGN = 4096
 OC_NSTATS = 5
+OC_ABI_VERSION = 2  # include/oc_engine.h
 
 OC_FLAG_DONE = 0x01
 OC_FLAG_SUCCESS = 0x02
@@ -181,7 +182,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.oc_reachability.argtypes = [vp, ctypes.POINTER(i32), vp, i64, vp, i64]
     lib.oc_render.argtypes = [vp, vp, vp, vp, ctypes.POINTER(OcRenderDesc), vp, i64, vp]
     lib.oc_step_n.restype = ctypes.c_int
-    lib.oc_step_n.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]
+    lib.oc_step_n.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]
     lib.oc_gen_actions.restype = ctypes.c_int
     lib.oc_gen_actions.argtypes = [vp, vp, i64, i64, i64, u64, vp]
     lib.oc_state_checksum.restype = ctypes.c_int
@@ -190,8 +191,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.oc_stats_size.argtypes = [vp, i64, ctypes.POINTER(i64)]
     lib.oc_stats_reduce.restype = ctypes.c_int
     lib.oc_stats_reduce.argtypes = [vp, vp, i64, vp, vp]
-    if lib.oc_abi_version() != 1:
-        raise RuntimeError("liboc_engine ABI mismatch")
+    if lib.oc_abi_version() != OC_ABI_VERSION:
+        raise RuntimeError("liboc_engine ABI %d, binding expects %d (rebuild)" % (lib.oc_abi_version(), OC_ABI_VERSION))
     _lib = lib
     return lib
 

@@ -30,6 +30,7 @@ import scipy.special
 from . import capi
 from . import recipes as _recipes
 from . import levels as _levels
+from . import planner as _planner
 
 SubtaskAllocation = namedtuple("SubtaskAllocation", "subtask subtask_agent_names")  # bayesian_delegator.py:14
 
@@ -121,10 +122,10 @@ class BayesianDelegator:
 
     def _expander(self, env):
         p = self.planner
-        if p._exp is None:
-            names = env.get_agent_names()
-            p._exp = p._make_expander(env.level, len(names), p.device or env._device)
-            p._exp_key = (env.level.width, tuple(env.level.tiles), len(names), str(p.device or env._device))
+        key = _planner.expander_key(env, p.device)
+        if p._exp is None or p._exp_key != key:  # a planner last used on another level: rebuild
+            p._exp = p._make_expander(env.level, len(env.get_agent_names()), p.device or env._device)
+            p._exp_key = key
         return p._exp
 
     # ---- inverse planning ---------------------------------------------------------------

@@ -18,6 +18,9 @@ from . import capi
 from . import levels as _levels
 
 
+_U64 = (torch.uint64, torch.int64)
+
+
 def _ptr(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -113,15 +116,28 @@ class OvercookedBatch:
         if coll is not None:
             self._check(coll, self.pitch)
         if stats is not None:
-            self._check(stats, self.stats_bytes)
+            self._check(stats, self.stats_bytes, _U64)
         capi.check(self.lib.oc_step(self._h, _ptr(state_in), _ptr(state_out), _ptr(actions), _ptr(exec_out),
                                     _ptr(coll), _ptr(stats), self.B, self._stream()))
         return state_out
 
     def step_n(self, state_in: torch.Tensor, state_out: torch.Tensor, actions: torch.Tensor, n: int,
                traj: Optional[torch.Tensor] = None, exec_out: Optional[torch.Tensor] = None,
-               coll: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """n consecutive steps in one launch (oc_step_n): identical outputs to n step() calls."""
+               coll: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None,
+               totals: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """n consecutive steps in one launch (oc_step_n): identical outputs to n step() calls.
+        With `totals` (int64 [OC_NSTATS], needs `stats`) the launch also folds the statistics
+        into it, as reduce_stats() after it would."""
+        self.step_n_launcher(state_in, state_out, actions, n, traj, exec_out, coll, stats, totals)()
+        return state_out
+
+    def step_n_launcher(self, state_in: torch.Tensor, state_out: torch.Tensor, actions: torch.Tensor, n: int,
+                        traj: Optional[torch.Tensor] = None, exec_out: Optional[torch.Tensor] = None,
+                        coll: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None,
+                        totals: Optional[torch.Tensor] = None):
+        """Validate the buffers of an oc_step_n call once and return a zero-argument callable
+        that issues it on the current stream (the buffers must stay alive and unchanged in
+        shape): a repeated launch then costs one ctypes call, no per-call checks."""
         self._check(state_in, self.layout.state_bytes)
         self._check(state_out, self.layout.state_bytes)
         self._check(actions, n * self.A * self.pitch)
@@ -132,10 +148,18 @@ class OvercookedBatch:
         if coll is not None:
             self._check(coll, n * self.pitch)
         if stats is not None:
-            self._check(stats, self.stats_bytes)
-        capi.check(self.lib.oc_step_n(self._h, _ptr(state_in), _ptr(state_out), _ptr(actions), _ptr(traj),
-                                      _ptr(exec_out), _ptr(coll), _ptr(stats), self.B, n, self._stream()))
-        return state_out
+            self._check(stats, self.stats_bytes, _U64)
+        if totals is not None:
+            if stats is None:
+                raise ValueError("totals need the stats buffer")
+            self._check(totals, 8 * capi.OC_NSTATS, _U64)
+        args = (self._h, _ptr(state_in), _ptr(state_out), _ptr(actions), _ptr(traj), _ptr(exec_out), _ptr(coll),
+                _ptr(stats), _ptr(totals), self.B, int(n), self._stream())
+        fn, check = self.lib.oc_step_n, capi.check
+
+        def launch():
+            check(fn(*args))
+        return launch
 
     def rollout(self, state_in: torch.Tensor, state_out: torch.Tensor, actions: torch.Tensor, subtasks,
                 alloc: Optional[torch.Tensor] = None, flags: Optional[torch.Tensor] = None,
@@ -182,7 +206,7 @@ class OvercookedBatch:
             lower_bound = torch.empty((S, self.pitch), dtype=torch.float32, device=self.device)
         if doable is None:
             doable = torch.empty((S, self.pitch), dtype=torch.uint8, device=self.device)
-        self._check(lower_bound, 4 * S * self.pitch)
+        self._check(lower_bound, 4 * S * self.pitch, (torch.float32,))
         self._check(doable, S * self.pitch)
         capi.check(self.lib.oc_subtask_bounds(self._h, _ptr(state), capi.subtask_array(subtasks), S,
                                               _ptr(lower_bound), _ptr(doable), self.B, self._stream()))
@@ -219,7 +243,12 @@ class OvercookedBatch:
         capi.check(self.lib.oc_stats_reduce(self._h, _ptr(stats), self.B, _ptr(out), self._stream()))
         return out
 
-    def _check(self, t: torch.Tensor, nbytes: int) -> None:
+    def _check(self, t: torch.Tensor, nbytes: int, dtypes=(torch.uint8,)) -> None:
+        """Device, contiguity, size, alignment and element type of a buffer handed to the
+        C-ABI (the kernels read raw bytes: an int64 action tensor would pass a size check
+        and be read as 8 bytes per code)."""
+        if t.dtype not in dtypes:
+            raise TypeError("buffer dtype %s, expected %s" % (t.dtype, " or ".join(str(d) for d in dtypes)))
         if t.device != self.device or not t.is_contiguous():
             raise ValueError("buffer must be contiguous on %s" % self.device)
         if t.numel() * t.element_size() < nbytes:

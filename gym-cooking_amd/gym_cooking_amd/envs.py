@@ -16,8 +16,9 @@ Differences from the reference, by design:
   * stepping after ``done`` continues the episode like the reference (the engine's
     next-step auto-reset is disabled for this single env by clearing DONE on upload);
   * a step that the reference would crash in (two co-located agents both holding,
-    ``copy.copy`` at :289 -> world.py:417) raises ``RuntimeError`` here after updating
-    the state, as the reference raises after ``execute_navigation``;
+    ``copy.copy`` at :289 -> world.py:417) raises :class:`CopyCrash`, an ``AttributeError``
+    as the reference's is, here after updating the state, as the reference raises after
+    ``execute_navigation``;
   * ``world.get_repr()`` keeps an empty group for every object name that existed earlier in
     the episode, as the reference's ``World.objects`` dict does (``remove`` pops from a
     group but never drops it, world.py:304-316, 323-337).  The 17-byte state does not hold
@@ -53,6 +54,13 @@ AgentRepr = namedtuple("AgentRepr", "name location holding")                    
 GridSquareRepr = namedtuple("GridSquareRepr", "name location holding")            # utils/core.py:16
 
 FLAG_DONE, FLAG_SUCCESS, FLAG_ERR = 0x01, 0x02, 0x04  # include/oc_engine.h flags plane
+
+
+class CopyCrash(AttributeError):
+    """The reference's crash when ``copy.copy`` meets two co-located agents that both hold an
+    item: ``World.get_object_at`` returns None and ``None.name`` raises AttributeError
+    (overcooked_environment.py:289 -> :108-113 -> world.py:417).  Callers written against the
+    reference catch AttributeError; this is one."""
 COLORS = ["blue", "magenta", "yellow", "green"]  # utils/agent.py:25
 NAV_ACTIONS = [(0, 1), (0, -1), (-1, 0), (1, 0)]  # utils/world.py:16
 _TILE_NAMES = {_levels.TILE_FLOOR: "Floor", _levels.TILE_COUNTER: "Counter",
@@ -507,8 +515,8 @@ class OvercookedEnvironment:
         self._refresh(executed)
         self.agent_actions = {n: act for n, act in zip(names, executed)}
         if self._flags & FLAG_ERR:
-            raise RuntimeError("two co-located agents both hold items: the reference crashes in copy.copy "
-                               "(overcooked_environment.py:289 -> world.py:417)")
+            raise CopyCrash("two co-located agents both hold items: the reference crashes in copy.copy "
+                            "(overcooked_environment.py:289 -> world.py:417)")
         new_obs = _copy.copy(self)
         image_obs = self.game.get_image_obs() if self.game is not None else None
         done = self.done()
@@ -739,10 +747,10 @@ class OvercookedVecEnv:
 
     def step(self, actions: torch.Tensor):
         B, P = self.num_envs, self.P
-        if actions.shape[-1] == P and actions.is_contiguous():
+        if actions.dtype == torch.uint8 and actions.shape[-1] == P and actions.is_contiguous():
             act = actions.reshape(-1)
-        else:
-            self._act.view(self.A, P)[:, :B].copy_(actions.view(self.A, B))
+        else:  # copy_ converts any integer dtype to the u8 codes the kernel reads
+            self._act.view(self.A, P)[:, :B].copy_(actions.reshape(self.A, B))
             act = self._act
         src, dst = self._s[self._i], self._s[self._i ^ 1]
         self.batch.step(src, dst, act, self.ex, self.coll, self.stats)

@@ -119,18 +119,24 @@ class _Expander:
         self.NP = self.eb.layout.num_planes
         self.t_plane = self.eb.layout.plane_t
         dev = self.eb.device
-        self.s_in = self.eb.new_state()
-        self.s_out = self.eb.new_state()
-        self.act = self.eb.new_actions()
-        self.alloc = torch.empty(self.P, dtype=torch.uint8, device=dev)
-        self.flags = torch.empty(self.P, dtype=torch.uint8, device=dev)
-        self.lb = torch.empty(self.P, dtype=torch.float32, device=dev)
-
-        def pin(*shape, dt=torch.uint8):
-            return torch.empty(shape, dtype=dt).pin_memory()
-
-        self._h_in, self._h_act, self._h_alloc = pin(self.NP, self.ROWS), pin(self.A, self.ROWS), pin(self.ROWS)
-        self._h_out, self._h_fl, self._h_lb = pin(self.NP, self.ROWS), pin(self.ROWS), pin(self.ROWS, dt=torch.float32)
+        NP, A, P = self.NP, self.A, self.P
+        # One contiguous input block (state planes | actions | allocation ids) and one output
+        # block (next-state planes | flags | f32 bounds), each moved by ONE pinned copy per
+        # launch: every buffer is a full-pitch slice (P = ROWS), so no strided per-plane copies.
+        n_in, n_out = (NP + A + 1) * P, (NP + 1 + 4) * P
+        self._d_in = torch.empty(n_in, dtype=torch.uint8, device=dev)
+        self._d_out = torch.empty(n_out, dtype=torch.uint8, device=dev)
+        self._h_in_all = torch.empty(n_in, dtype=torch.uint8).pin_memory()
+        self._h_out_all = torch.empty(n_out, dtype=torch.uint8).pin_memory()
+        self.s_in, self.act, self.alloc = (self._d_in[:NP * P], self._d_in[NP * P:(NP + A) * P],
+                                           self._d_in[(NP + A) * P:])
+        self.s_out, self.flags = self._d_out[:NP * P], self._d_out[NP * P:(NP + 1) * P]
+        self.lb = self._d_out[(NP + 1) * P:].view(torch.float32)
+        hin, hout = self._h_in_all.numpy(), self._h_out_all.numpy()
+        self._hi, self._ha, self._hal = (hin[:NP * P].reshape(NP, P), hin[NP * P:(NP + A) * P].reshape(A, P),
+                                         hin[(NP + A) * P:])
+        self._ho, self._hf = hout[:NP * P].reshape(NP, P), hout[NP * P:(NP + 1) * P]
+        self._hl = hout[(NP + 1) * P:].view(np.float32)
         self.launches = 0
         self.rows_done = 0
 
@@ -141,10 +147,10 @@ class _Expander:
     def bounds(self, state: np.ndarray, subs):
         """oc_subtask_bounds of one state (env_view bytes) under each configuration:
         (lower bounds [S], doable [S])."""
-        hi = self._h_in.numpy()
+        hi = self._hi
         hi[:, 0] = state
         hi[self.t_plane:, 0] = 0
-        self.s_in.view(self.NP, self.P)[:, :1].copy_(self._h_in[:, :1])
+        self._d_in.copy_(self._h_in_all, non_blocking=True)
         S = len(subs)
         lbt = torch.empty((S, self.P), dtype=torch.float32, device=self.eb.device)
         okt = torch.empty((S, self.P), dtype=torch.uint8, device=self.eb.device)
@@ -168,7 +174,7 @@ class _Expander:
         return out
 
     def _launch(self, reqs, subs):
-        hi, ha, hal = self._h_in.numpy(), self._h_act.numpy(), self._h_alloc.numpy()
+        hi, ha, hal = self._hi, self._ha, self._hal
         r0, spans = 0, []
         for state, codes, sub in reqs:
             n = len(codes)
@@ -183,20 +189,16 @@ class _Expander:
         n = r0
         hi[self.t_plane:, :n] = 0  # t and flags: copied through by the kernel, not part of a planner state
         table = [sub for _, sub in sorted(subs.values(), key=lambda v: v[0])]
-        self.s_in.view(self.NP, self.P)[:, :n].copy_(self._h_in[:, :n], non_blocking=True)
-        self.act.view(self.A, self.P)[:, :n].copy_(self._h_act[:, :n], non_blocking=True)
-        self.alloc[:n].copy_(self._h_alloc[:n], non_blocking=True)
+        self._d_in.copy_(self._h_in_all, non_blocking=True)  # one H2D
         lib, eb = self.eb.lib, self.eb
         capi.check(lib.oc_rollout(eb._h, _ptr(self.s_in), _ptr(self.s_out), _ptr(self.act), _ptr(self.alloc),
                                   capi.subtask_array(table), len(table), _ptr(self.flags), _ptr(self.lb), n,
                                   eb._stream()))
         self.launches += 1
         self.rows_done += n
-        self._h_out[:, :n].copy_(self.s_out.view(self.NP, self.P)[:, :n], non_blocking=True)
-        self._h_fl[:n].copy_(self.flags[:n], non_blocking=True)
-        self._h_lb[:n].copy_(self.lb[:n], non_blocking=True)
+        self._h_out_all.copy_(self._d_out, non_blocking=True)  # one D2H
         torch.cuda.current_stream(eb.device).synchronize()
-        ho, hf, hl = self._h_out.numpy(), self._h_fl.numpy(), self._h_lb.numpy()
+        ho, hf, hl = self._ho, self._hf, self._hl
         res = []
         for r0, n in spans:
             nxt = ho[:, r0:r0 + n].T.copy()
@@ -281,7 +283,7 @@ class E2E_BRTDP:
         assert agents == sorted(agents), "subtask agent names are not in order"
         self._agents = agents
         level, A = env.level, len(names)
-        key = (level.width, tuple(level.tiles), A, str(self.device or env._device))
+        key = expander_key(env, self.device)
         if self._exp is None or self._exp_key != key:
             self._exp = self._make_expander(level, A, self.device or env._device)
             self._exp_key = key
@@ -676,6 +678,13 @@ class PlanEnv:
         return self._bytes.copy()
 
 
+def expander_key(env, device=None):
+    """What an expander is built for: the level's grid and tiles, the agent count, the device.
+    Planners may share an expander only when their keys are equal."""
+    level = env.level
+    return (level.width, tuple(level.tiles), len(env.get_agent_names()), str(device or env._device))
+
+
 def plan_batch(planners: Sequence[E2E_BRTDP], envs_, subtasks, agent_names, other_agent_planners=None) -> list:
     """get_next_action of many independent searches at once: planner i plans `subtasks[i]` for
     `agent_names[i]` in `envs_[i]`, at Level 0, or at Level 1 with `other_agent_planners[i]`
@@ -692,6 +701,10 @@ def plan_batch(planners: Sequence[E2E_BRTDP], envs_, subtasks, agent_names, othe
         return []
     others = other_agent_planners or [None] * len(planners)
     assert len(others) == len(planners)
+    keys = {expander_key(e, p.device) for p, e in zip(planners, envs_)}
+    if len(keys) != 1:
+        raise ValueError("plan_batch: the searches must share one level, agent count and device "
+                         "(they share one expander); got %d different ones" % len(keys))
     gens = [p._next_action(e, st, an, o) for p, e, st, an, o in zip(planners, envs_, subtasks, agent_names, others)]
     out = [None] * len(gens)
     pending = {}

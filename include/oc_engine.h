@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define OC_ABI_VERSION 1
+#define OC_ABI_VERSION 2
 
 #define OC_MAX_AGENTS 4
 #define OC_MAX_ITEMS 8
@@ -155,9 +155,13 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
  *   traj         : nullable; n x [num_planes][pitch]: the state after every step (traj[r] equals
  *                  the state_out of the r-th oc_step); must not alias state_in/state_out
  *   exec_actions : nullable; n x u8 [A][pitch];  coll_mask : nullable; n x u8 [pitch]
- *   stats        : accumulated over the n steps (same buffer as oc_step). */
+ *   stats        : accumulated over the n steps (same buffer as oc_step); nullable
+ *   totals       : nullable (needs stats); OC_NSTATS device uint64: the launch's last wave
+ *                  folds the stats buffer into it, i.e. oc_stats_reduce after the steps
+ *                  without a second launch (main.py's per-episode bookkeeping for the window). */
 int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions, void* traj,
-              uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, int64_t B, int32_t n, void* stream);
+              uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, uint64_t* totals, int64_t B, int32_t n,
+              void* stream);
 
 /* Synthetic i.i.d. uniform action codes 0..4 for B envs at step `step`:
  * code = splitmix64(seed ^ gid*0x9E3779B97F4A7C15 ^ step*0xC2B2AE3D27D4EB4F ^ agent) % 5,

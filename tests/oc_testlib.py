@@ -418,3 +418,15 @@ class BoundRows:
             if len(errs) > 20:
                 break
         return errs
+
+
+def window_totals(fl_in: np.ndarray, state_out: np.ndarray, coll: np.ndarray, A: int, K: int, pitch: int,
+                  B: int) -> np.ndarray:
+    """Host restatement of one step's contribution to the OC_STAT_* counters
+    (include/oc_engine.h): episodes whose DONE bit was newly set, their successes, their
+    lengths t, colliding pairs (popcount of the collision mask) and ERR ends."""
+    v = planes_view(state_out, A, K, pitch)
+    fl = v["fl"][:B]
+    ended = ((fl_in[:B] & 1) == 0) & ((fl & 1) == 1)
+    return np.array([ended.sum(), (ended & ((fl & 2) > 0)).sum(), v["t"][:B][ended].astype(np.int64).sum(),
+                     np.unpackbits(coll[:B]).sum(), (ended & ((fl & 4) > 0)).sum()], dtype=np.int64)

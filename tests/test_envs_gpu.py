@@ -45,7 +45,7 @@ def test_single_env_shim_replays_fixtures(fixture, limit):
             exp_fl = int(fx["flags"][off + step + 1])
             ncoll = len(env.collisions)
             if exp_fl & 0x04:
-                with pytest.raises(RuntimeError):
+                with pytest.raises(AttributeError):
                     env.step(ad)
                 n_err += 1
                 break
@@ -92,3 +92,26 @@ def test_vec_env_matches_batch():
     assert ends > 0
     tot = ve.episode_stats()
     assert int(tot[0]) == ends
+
+
+def test_vec_env_int64_actions_at_pitch():
+    """at B == pitch (2^k multiples of 4096) an int64 action tensor must be
+    converted, not read as raw bytes; results equal the uint8 path and the batch engine."""
+    from gym_cooking_amd.envs import OvercookedVecEnv
+    B, A = 8192, 2
+    v8 = OvercookedVecEnv("partial-divider_salad", A, B, max_num_timesteps=30)
+    v64 = OvercookedVecEnv("partial-divider_salad", A, B, max_num_timesteps=30)
+    assert v8.P == B
+    v8.reset()
+    v64.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(4)
+    for t in range(45):
+        a64 = torch.randint(0, 5, (A, B), device="cuda:0", generator=g)  # int64, torch's default
+        s8, r8, d8, _ = v8.step(a64.to(torch.uint8))
+        s64, r64, d64, _ = v64.step(a64)
+        assert torch.equal(s8, s64), t
+    from gym_cooking_amd.engine import OvercookedBatch
+    eb = OvercookedBatch("partial-divider_salad", A, B, max_T=30)
+    with pytest.raises(TypeError):
+        eb.step(eb.new_state(), eb.new_state(), torch.zeros(A * B, dtype=torch.int64, device="cuda:0"))

@@ -245,8 +245,10 @@ def _step_n_vs_steps(level, A, B, n, seed, max_T=100, with_traj=True, warm=0):
     ex_n = torch.zeros(n * A * P, dtype=torch.uint8, device="cuda:0")
     coll_n = torch.zeros(n * P, dtype=torch.uint8, device="cuda:0")
     stats_n = eb.new_stats()
-    eb.step_n(s0, out, acts, n, traj, ex_n, coll_n, stats_n)
+    totals = torch.full((5,), -1, dtype=torch.int64, device="cuda:0")
+    eb.step_n(s0, out, acts, n, traj, ex_n, coll_n, stats_n, totals)
     torch.cuda.synchronize()
+    assert torch.equal(totals, eb.reduce_stats(stats_ref)), "in-launch totals"
     assert torch.equal(out, ref_states[-1])
     for r in range(n):
         if with_traj:

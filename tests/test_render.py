@@ -1,17 +1,20 @@
 """Image observations (GameImage.get_image_obs, gym_cooking/misc/game/).
 
-Parity unpinned: pygame/SDL are absent, so no reference image exists.  The kernel
-(oc_render) is checked bit-exact against the independent numpy restatement
-oracle/render_oracle.py on fixture states recorded from the reference (streams.npz,
-greedy.npz: plates, merged and delivered dishes, held items, 2-4 agents).  The restatement's
-constants are checked against the values the reference's expressions evaluate to."""
+Pinned to the reference's own pixels (pygame/SDL are absent here, so the reference cannot
+draw new images, but its checkout holds some): the 9 screenshots images/{2,3,4}_{open,partial,
+full}.png of the initial Salad kitchens, exact RGB, and the 111 frames of the three recorded
+episodes images/{2_open_salad,2_full_salad,2_partial_tl}.gif (held, chopped, plated and
+delivered dishes), exact after the GIF's palette quantisation (tests/golden/gen_render_ref.py).
+The numpy restatement oracle/render_oracle.py reproduces all of them, and so does the kernel
+(oc_render).  The kernel is also checked bit-exact against the restatement on fixture states
+recorded from the reference (streams.npz, greedy.npz: 2-4 agents, every reachable dish)."""
 import numpy as np
 import pytest
 
 import oc_testlib as tl
 from gym_cooking_amd import capi, levels, render
 
-from oracle import render_oracle
+from oracle import oracle, render_oracle
 
 
 def test_geometry_is_the_references():
@@ -159,3 +162,132 @@ def test_shim_image_obs():
             assert info["image_obs"].shape == (lv.height * 80, lv.width * 80, 3)
             assert np.array_equal(info["image_obs"], exp), step
             assert np.array_equal(env.game.get_image_obs(), exp)
+
+
+# ----------------------------------------------------------------------------------------
+# Reference pixels (tests/golden/render_ref.npz, tests/golden/gen_render_ref.py): the
+# reference's own screenshots of the initial Salad kitchens (exact RGB) and the frames of its
+# three recorded episodes (palette-quantised GIFs; the joint actions recovered frame by frame).
+
+HOLD = 255
+REF_PNGS = ["%d_%s" % (A, k) for A in (2, 3, 4) for k in ("open", "partial", "full")]
+REF_GIFS = ["2_open_salad", "2_full_salad", "2_partial_tl"]
+
+
+def _ref():
+    import os
+    with np.load(os.path.join(tl.GOLDEN, "render_ref.npz")) as z:
+        return {k: z[k] for k in z.files}
+
+
+def _png(ref, name):
+    import hashlib
+    import zlib
+    lvname, A = (str(x) for x in ref["png_%s_meta" % name])
+    lv = levels.load_level(lvname)
+    rgb = np.frombuffer(zlib.decompress(ref["png_%s" % name].tobytes()), np.uint8).reshape(lv.height * 80,
+                                                                                           lv.width * 80, 3)
+    assert hashlib.sha256(rgb.tobytes()).hexdigest() == str(ref["png_%s_sha256" % name])
+    return lv, int(A), rgb
+
+
+def _gif(ref, name):
+    lvname, A = (str(x) for x in ref["gif_%s_meta" % name])
+    return levels.load_level(lvname), int(A)
+
+
+def gif_frame_ok(ref, name, f, render):
+    """Rebuild GIF frame f of `name` from a render (nearest frame colour per pixel, the recorded
+    GIF colour where two frame colours are equally near) and compare its SHA-256 with the
+    reference frame's."""
+    import hashlib
+    co = ref["gif_%s_colour_off" % name]
+    cols = ref["gif_%s_colours" % name][co[f]:co[f + 1]].astype(np.int64)
+    flat = render.reshape(-1, 3).astype(np.int64)
+    u, inv = np.unique(flat, axis=0, return_inverse=True)
+    near = ((u[:, None, :] - cols[None]) ** 2).sum(-1).argmin(1)[inv.reshape(-1)]
+    to = ref["gif_%s_tie_off" % name]
+    near[ref["gif_%s_tie_pos" % name][to[f]:to[f + 1]]] = ref["gif_%s_tie_idx" % name][to[f]:to[f + 1]]
+    rgb = cols[near].astype(np.uint8).reshape(render.shape)
+    return hashlib.sha256(rgb.tobytes()).hexdigest() == str(ref["gif_%s_sha256" % name][f])
+
+
+def _replay_gif(ref, name):
+    """The recovered episode replayed by the CPU oracle from reset: the per-frame state bytes
+    (a HOLD action repeats the final frame) -- equal to the recorded states."""
+    lv, A = _gif(ref, name)
+    ob = oracle.OracleBatch(lv, A, 0, 1)
+    s, s2 = ob.new_state(), ob.new_state()
+    ob.reset(s)
+    states = [tl.env_view(s, A, ob.K, ob.pitch, 1)[:, 0]]
+    for ja in ref["gif_%s_actions" % name]:
+        if ja[0] != HOLD:
+            act = ob.new_actions().reshape(A, ob.pitch)
+            act[:, 0] = ja
+            ob.step(s, s2, act.reshape(-1))
+            s, s2 = s2, s
+        states.append(tl.env_view(s, A, ob.K, ob.pitch, 1)[:, 0])
+    return lv, A, ob.K, np.stack(states)
+
+
+@pytest.mark.parametrize("name", REF_PNGS)
+def test_oracle_matches_reference_screenshot(name):
+    """render_oracle of the reset state == the reference's own 560x560 screenshot, every pixel."""
+    ref = _ref()
+    lv, A, rgb = _png(ref, name)
+    ob = oracle.OracleBatch(lv, A, 0, 1)
+    s = ob.new_state()
+    ob.reset(s)
+    img = render_oracle.render_env(lv, tl.env_view(s, A, ob.K, ob.pitch, 1)[:, 0], A, ob.K, channels="rgb")
+    assert np.array_equal(img, rgb), int((img != rgb).any(-1).sum())
+
+
+@pytest.mark.parametrize("name", REF_GIFS)
+def test_oracle_matches_reference_episode_frames(name):
+    """Every frame of the reference's recorded episode (held, chopped, plated and delivered
+    dishes): the oracle replays the recovered actions to the recorded states, and
+    render_oracle's image of each quantises to the reference frame exactly."""
+    ref = _ref()
+    lv, A, K, states = _replay_gif(ref, name)
+    assert np.array_equal(states, ref["gif_%s_states" % name])
+    masks = set(states[:, 3 * A + K:3 * A + 2 * K].ravel().tolist())
+    assert {0x11, 0x22} <= masks and masks & {0x19, 0x2A, 0x3B}  # chopped and plated dishes occur
+    assert (states[:, 2 * A:3 * A] != 0xFF).any()  # agents hold items
+    spr = render_oracle._sprites()
+    for f, st in enumerate(states):
+        assert gif_frame_ok(ref, name, f, render_oracle.render_env(lv, st, A, K, spr, channels="rgb")), (name, f)
+
+
+@pytest.mark.gpu
+def test_render_kernel_matches_reference_pixels():
+    """oc_render (channels rgb) on the screenshots' reset states and on every recorded episode
+    frame: the reference's own pixels (exact for the screenshots, exact after the GIF's
+    palette quantisation for the frames)."""
+    import torch
+    from gym_cooking_amd.engine import OvercookedBatch
+    ref = _ref()
+    spr = render.load_sprites()
+    for name in REF_PNGS:
+        lv, A, rgb = _png(ref, name)
+        eb = OvercookedBatch(lv, A, 1, max_T=0)
+        s = eb.new_state()
+        eb.reset(s)
+        img = render.Renderer(eb, spr).render(s, channels="rgb").cpu().numpy()[0]
+        assert np.array_equal(img, rgb), (name, int((img != rgb).any(-1).sum()))
+    for name in REF_GIFS:
+        lv, A = _gif(ref, name)
+        states = ref["gif_%s_states" % name]
+        B, K = len(states), capi.item_slots(lv)
+        pitch = capi.pitch_for(B)
+        host = np.zeros(capi.layout_planes(A, K)["num_planes"] * pitch, np.uint8)
+        P = capi.layout_planes(A, K)
+        v = host.reshape(-1, pitch)
+        for p in range(P["t"]):
+            v[p, :B] = states[:, p]
+        t = (states[:, P["t"]].astype(np.uint16) | (states[:, P["t"] + 1].astype(np.uint16) << 8))
+        host[P["t"] * pitch:(P["t"] + 2) * pitch].view(np.uint16)[:B] = t
+        v[P["flags"], :B] = states[:, P["flags"]]
+        eb = OvercookedBatch(lv, A, B, max_T=0)
+        imgs = render.Renderer(eb, spr).render(torch.from_numpy(host).to(eb.device), channels="rgb").cpu().numpy()
+        for f in range(B):
+            assert gif_frame_ok(ref, name, f, imgs[f]), (name, f)

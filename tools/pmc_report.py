@@ -20,7 +20,7 @@ import sys
 
 B, NP, A = 1 << 20, 17, 2  # tools/pmc_probe.py workload
 PITCH = B
-NFUSED = 100
+NFUSED = (20, 100)  # tools/pmc_probe.py: 3 oc_step_n dispatches of each, in this order
 
 
 def per_kernel(d, counter):
@@ -61,11 +61,15 @@ def main():
     res["oc_step_kernel"] = {"read_bytes": f_step, "write_bytes": w_step, "hbm_bytes_per_launch": f_step + w_step,
                              "algorithmic_bytes_per_launch": alg, "ratio": (f_step + w_step) / alg}
     if "oc_step_n_kernel" in fetch:
-        fn, wn = mean_tail(fetch["oc_step_n_kernel"]) * 1024 * rf, mean_tail(write["oc_step_n_kernel"]) * 1024 * wf
-        algn = (NP + NFUSED * (NP + 2 * A + 1)) * B
-        res["oc_step_n_kernel"] = {"steps_per_launch": NFUSED, "read_bytes": fn, "write_bytes": wn,
-                                   "hbm_bytes_per_launch": fn + wn, "algorithmic_bytes_per_launch": algn,
-                                   "ratio": (fn + wn) / algn}
+        shapes = {}
+        for i, n in enumerate(NFUSED):
+            fv, wv = fetch["oc_step_n_kernel"][3 * i:3 * i + 3], write["oc_step_n_kernel"][3 * i:3 * i + 3]
+            fn, wn = mean_tail(fv) * 1024 * rf, mean_tail(wv) * 1024 * wf
+            algn = (NP + n * (NP + 2 * A + 1)) * B
+            shapes[str(n)] = {"steps_per_launch": n, "read_bytes": fn, "write_bytes": wn,
+                              "hbm_bytes_per_launch": fn + wn, "algorithmic_bytes_per_launch": algn,
+                              "ratio": (fn + wn) / algn}
+        res["oc_step_n_kernel"] = {"by_steps_per_launch": shapes}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
