@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -463,6 +464,9 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--steps-per-launch", type=int, default=100, help="oc_step_n launch length (headline)")
     ap.add_argument("--min-warmup-ms", type=float, default=50.0, help="repeat the untimed warmup for at least this long")
+    ap.add_argument("--kernel-replay-ms", type=float, default=20.0,
+                    help="after the timed region, replay its launches back to back for about this long between "
+                         "two HIP events to measure the dominant kernel's mean launch duration")
     ap.add_argument("--no-graph", action="store_true", help="per-step line: eager launches instead of a hipGraph")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -549,25 +553,32 @@ def main() -> int:
     # ---------------- timed region ----------------
     ocdist.barrier()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record()
     for f in timed:
         f()
-    ev1.record()
     gathered = ocdist.gather_summaries(totals)
     torch.cuda.synchronize()
     ocdist.barrier()
     elapsed = time.perf_counter() - t0
     # ----------------------------------------------
     elapsed_max = ocdist.max_over_ranks(elapsed, dev)
-    steps_ms = ev0.elapsed_time(ev1)
     summary = ocdist.summarize(gathered)
 
-    # Dominant kernel: oc_step_n_kernel; HIP events on its launch stream bracket the timed
-    # launches (back to back, the last one's in-launch statistics fold included), so
-    # window / launches = its mean duration.
-    kern_ms = steps_ms / len(segs)
+    # Dominant kernel: oc_step_n_kernel.  Its mean launch duration is measured right after the
+    # timed region with HIP events on its launch stream around back-to-back replays of the timed
+    # launches (same shapes, buffers and in-launch statistics fold), so the GPU queue never
+    # drains between launches and the events bracket kernel time only.  Events inside the
+    # timed region itself would add their own record cost (~4 us, tools/window_probe.py) to a
+    # window of one ~90 us launch, and the first event would also time the host's launch call.
+    reps = max(1, int(math.ceil(args.kernel_replay_ms / max(1e-3, elapsed * 1e3))))
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(reps):
+        for f in timed:
+            f()
+    ev1.record()
+    torch.cuda.synchronize()
+    kern_ms = ocdist.max_over_ranks(ev0.elapsed_time(ev1) / (reps * len(segs)) * 1e-3, dev) * 1e3
     nS = eb.layout.num_planes  # state bytes per env (the u16 t counts 2)
     bytes_launch = (nS + n_per * (nS + 2 * A + 1)) * sh.batch
     bytes_env_step = bytes_launch / (n_per * sh.batch)
@@ -602,7 +613,8 @@ def main() -> int:
             "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
             "kernel": "oc_step_n_kernel<%d,%d>" % (A, eb.K), "steps_per_launch": n_per,
             "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_env_step": bytes_env_step,
-            "kernel_ms_mean": kern_ms, "traffic_source": traffic_src,
+            "kernel_ms_mean": kern_ms, "kernel_ms_source": "HIP events around %d back-to-back replays of the "
+            "timed launches on their stream (max over ranks)" % reps, "traffic_source": traffic_src,
         },
         "episodes": summary,
     }
