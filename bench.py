@@ -102,32 +102,45 @@ def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 20) -> dict:
     table = table[:capi.MAX_SUBTASKS]
     gen = torch.Generator(device=dev)
     gen.manual_seed(5)
-    alloc = torch.randint(0, len(table), (eb.pitch,), dtype=torch.uint8, device=dev, generator=gen)
+    # Rows are configuration-major (the ids sorted: each configuration's rows contiguous), the
+    # order in which the reference's delegator evaluates them (bayesian_delegator.py:1026-1072:
+    # for each subtask allocation, for each agent) and in which planner.py / delegation.py batch
+    # them.  The same ids in random row order are timed beside it ("random_order"): waves then
+    # mix configurations and diverge (profiles/r02/pmc_c5.json: 17 % active lanes per VALU op).
+    rnd = torch.randint(0, len(table), (eb.pitch,), dtype=torch.uint8, device=dev, generator=gen)
+    alloc = torch.sort(rnd)[0].contiguous()
     eb.gen_actions(a, 99, 12)
     out = eb.new_state()
     flags = torch.empty(eb.pitch, dtype=torch.uint8, device=dev)
     lb = torch.empty(eb.pitch, dtype=torch.float32, device=dev)
-    for _ in range(2):
-        eb.rollout(s, out, a, table, alloc, flags, lb)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        eb.rollout(s, out, a, table, alloc, flags, lb)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
+
+    def time_rollout(al):
+        for _ in range(2):
+            eb.rollout(s, out, a, table, al, flags, lb)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            eb.rollout(s, out, a, table, al, flags, lb)
+        e1.record()
+        torch.cuda.synchronize()
+        return ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
+
+    ms_rnd = time_rollout(rnd)
+    ms = time_rollout(alloc)
     nbytes = 55 * rows
     legal = int((flags[:rows] & capi.ROLL_LEGAL).ne(0).sum())
     lik = measure_likelihood(eb, s, a, table, alloc, dev, world)
+    lik["random_order"] = measure_likelihood(eb, s, a, table, rnd, dev, world)["ms_per_launch"]
     bnd = measure_bounds(eb, s, table, dev, world)
     return {"value": world * rows / (ms * 1e-3), "unit": "rollout rows/s", "rows_per_gpu": rows, "likelihood": lik,
             "subtask_bounds": bnd,
             "ms_per_launch": ms, "kernel": "oc_rollout_kernel<4,4>",
-            "workload": "C5: full-divider_salad 4 agents, %d Salad (subtask, agents) configs, random joint actions"
-                        % len(table),
+            "workload": "C5: full-divider_salad 4 agents, %d Salad (subtask, agents) configs, random joint actions, "
+                        "rows configuration-major" % len(table),
             "algorithmic_bytes_per_row": 55, "achieved_GBs": nbytes / (ms * 1e-3) / 1e9,
-            "frac_hbm": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "legal_rows": legal}
+            "frac_hbm": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "legal_rows": legal,
+            "random_order": {"ms_per_launch": ms_rnd, "value": world * rows / (ms_rnd * 1e-3)}}
 
 
 def measure_likelihood(eb, states, taken, table, alloc, dev, world, reps: int = 5) -> dict:
@@ -146,8 +159,8 @@ def measure_likelihood(eb, states, taken, table, alloc, dev, world, reps: int = 
     ms = ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
     ok = int((f[:eb.B] == capi.LIK_OK).sum())
     return {"value": world * eb.B / (ms * 1e-3), "unit": "likelihood rows/s", "ms_per_launch": ms,
-            "kernel": "oc_likelihood_kernel<4,4>", "rows_computed": ok, "bound": "compute (fp64 softmax over "
-            "up to 25 candidate rollouts per row)"}
+            "kernel": "oc_likelihood_kernel<4,4>", "rows_computed": ok, "bound": "issue (divergent row code: "
+            "up to 25 candidate rollouts per row, profiles/r02/pmc_c5.json)"}
 
 
 def measure_bounds(eb, states, table, dev, world, reps: int = 10) -> dict:

@@ -41,9 +41,8 @@ constexpr int kEnvsPerBlock = kBlock * kEPL;
 
 // Kernel argument block: everything static about the level, passed by value (SGPRs).
 struct LevelArgs {
-    uint64_t floor_mask;  // bit c: cell c is Floor (the only non-collidable tile)
-    uint64_t cut_mask;    // Cutboard cells
-    uint64_t deliv_mask;  // Delivery cells
+    uint32_t cls4[64];    // tile class byte of cell c (ocsw::tile_class) in byte c % 4 of word c / 4;
+                          // cells >= W*H (up to 255, 0xFF = dead) read 0
     uint64_t dcell_lut;   // per action code: signed cell delta + 128 (byte lanes 0..4)
     int32_t W, H;
     int32_t done_cell;    // first Delivery in scan order (done() reads only it, :349)
@@ -213,15 +212,20 @@ __global__ __launch_bounds__(kStepBlock) void oc_step_kernel(LevelArgs L, const 
     const uint32_t g = blockIdx.x * (uint32_t)kStepBlock + threadIdx.x;  // grid * kStepBlock == P / kEPL
     Chunk<A, K> c;
     load_chunk<A, K>(c, b, P, g);  // in flight while the block builds its table
-    // tile class per cell (bit7 Floor, bit6 Delivery, bit5 Cutboard); cells >= 64 read 0
-    __shared__ uint8_t tbl[256];
+    // tile class per cell (bit7 Floor, bit6 Delivery, bit5 Cutboard); cells past the grid read 0.
+    // Lane 0 writes the 64 table words from scalar kernel-argument loads (no vector memory
+    // access, so nothing waits behind the chunk loads) and the table is published with an
+    // LDS-only workgroup fence around the barrier (a plain __syncthreads would also wait for
+    // the chunk loads).
+    __shared__ uint32_t tbl4[64];
+    if (threadIdx.x == 0u) {
 #pragma unroll
-    for (int i = 0; i < 256 / kStepBlock; ++i) {
-        const uint32_t cell = threadIdx.x + i * kStepBlock;
-        tbl[cell] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, cell);
+        for (int i = 0; i < 64; ++i) tbl4[i] = L.cls4[i];
     }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: the LDS writes, not the chunk loads
+    const uint8_t* tbl = (const uint8_t*)tbl4;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     StepStats st;
     step_chunk<A, K, kCPsc1>(L, tbl, c, b, has_ex, has_coll, P, g, st);
     if (stats != nullptr) {  // wave sums, then fire-and-forget 64-bit atomics into this block's row
@@ -249,9 +253,10 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
                                                            uint8_t* __restrict__ coll_out,
                                                            uint64_t* __restrict__ stats, uint64_t* __restrict__ totals,
                                                            uint32_t stat_rows, int n) {
-    __shared__ uint8_t tbl[256];
-    tbl[threadIdx.x] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, threadIdx.x);
+    __shared__ uint32_t tbl4[64];
+    if (threadIdx.x < 64u) tbl4[threadIdx.x] = L.cls4[threadIdx.x];
     __syncthreads();
+    const uint8_t* tbl = (const uint8_t*)tbl4;
     const uint32_t P = (uint32_t)L.pitch, nlanes = P / kEPL, stride = gridDim.x * (uint32_t)kBlock;
     constexpr int NP = 3 * A + 2 * K + 3;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
@@ -381,25 +386,25 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
 }
 
 // Planner rollout (oc_rollout): one row per lane, scalar (oc_rollout.h).  Each block stages
-// the level's reachability distances, its tables and the subtask configurations in LDS, then
-// walks rows with a grid stride.  Rows are independent; byte-plane loads of 64 contiguous
-// bytes per wave instruction.
+// the level's table blob (tile classes, graph nodes, Cutboard / Delivery lists, reachability
+// distances: dynamic LDS sized for this level, oc_rollout.h blob_bytes) and the subtask
+// configurations in LDS, then walks rows with a grid stride.  Rows are independent;
+// byte-plane loads of 64 contiguous bytes per wave instruction.
 struct RollArgs {
     ocro::RollLevel L;
     ocro::Sub subs[OC_MAX_SUBTASKS];
     int32_t nsub;
+    int32_t blob_words;  // ocro::blob_bytes(nnodes) / 4
     int64_t pitch, B;
 };
 
-// Stage the reachability distances, the level tables and the subtask configurations in LDS.
-__device__ __forceinline__ void stage_roll_tables(const RollArgs& R, const uint8_t* dist_g, uint32_t* dist_w,
-                                                  ocro::RollLevel& Ls, ocro::Sub* subs) {
-    const int nwords = R.L.nnodes * ocro::kMaxNodes / 4;  // rows 0..nnodes-1 of the table
-    for (int i = threadIdx.x; i < nwords; i += kBlock) dist_w[i] = ((const uint32_t*)dist_g)[i];
-    if (threadIdx.x == 0) {
-        Ls = R.L;
-        for (int i = 0; i < R.nsub; ++i) subs[i] = R.subs[i];
-    }
+// Stage the level's table blob and the subtask configurations in LDS.
+__device__ __forceinline__ void stage_roll_tables(const RollArgs& R, const uint8_t* blob_g, uint32_t* blob_w,
+                                                  ocro::Sub* subs) {
+    for (int i = threadIdx.x; i < R.blob_words; i += kBlock) blob_w[i] = ((const uint32_t*)blob_g)[i];
+    constexpr int kSubWords = (int)(sizeof(ocro::Sub) / 4);
+    for (int i = threadIdx.x; i < R.nsub * kSubWords; i += kBlock)
+        ((uint32_t*)subs)[i] = ((const uint32_t*)R.subs)[i];
     __syncthreads();
 }
 
@@ -426,14 +431,13 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
                                                             uint8_t* __restrict__ sout,
                                                             const uint8_t* __restrict__ act,
                                                             const uint8_t* __restrict__ alloc,
-                                                            const uint8_t* __restrict__ dist_g,
+                                                            const uint8_t* __restrict__ blob_g,
                                                             uint8_t* __restrict__ out_flags,
                                                             float* __restrict__ lb) {
-    __shared__ uint32_t dist_w[ocro::kMaxNodes * ocro::kMaxNodes / 4];
-    __shared__ ocro::RollLevel Ls;
+    extern __shared__ uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
-    stage_roll_tables(R, dist_g, dist_w, Ls, subs);
-    const uint8_t* dist = (const uint8_t*)dist_w;
+    stage_roll_tables(R, blob_g, blob_w, subs);
+    const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
@@ -446,7 +450,7 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
         if (ai < R.nsub) {
             const ocro::Sub& s = subs[ai];
             const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
-            ocro::RowOps<A, K> ops(Ls, dist);
+            ocro::RowOps<A, K> ops(R.L, blob);
             f = ops.run(r, s, c0, c1, bound);
         }
 #pragma unroll
@@ -473,14 +477,13 @@ template <int A, int K>
 __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                                const uint8_t* __restrict__ taken_p,
                                                                const uint8_t* __restrict__ alloc,
-                                                               const uint8_t* __restrict__ dist_g, int self_agent,
+                                                               const uint8_t* __restrict__ blob_g, int self_agent,
                                                                double beta, double nap, double* __restrict__ out,
                                                                uint8_t* __restrict__ out_flags) {
-    __shared__ uint32_t dist_w[ocro::kMaxNodes * ocro::kMaxNodes / 4];
-    __shared__ ocro::RollLevel Ls;
+    extern __shared__ uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
-    stage_roll_tables(R, dist_g, dist_w, Ls, subs);
-    const uint8_t* dist = (const uint8_t*)dist_w;
+    stage_roll_tables(R, blob_g, blob_w, subs);
+    const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
         const int ai = alloc != nullptr ? alloc[e] : 0;
@@ -491,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
             uint32_t taken = 0;
 #pragma unroll
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
-            ocro::RowOps<A, K> ops(Ls, dist);
+            ocro::RowOps<A, K> ops(R.L, blob);
             f = ops.likelihood(r, subs[ai], taken, self_agent, beta, nap, v);
         }
         out[e] = f == OC_LIK_OK ? v : 0.0;
@@ -504,17 +507,16 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
 // store instruction of a wave covers 64 consecutive envs of one configuration.
 template <int A, int K>
 __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uint8_t* __restrict__ sin,
-                                                           const uint8_t* __restrict__ dist_g,
+                                                           const uint8_t* __restrict__ blob_g,
                                                            float* __restrict__ lb, uint8_t* __restrict__ doable) {
-    __shared__ uint32_t dist_w[ocro::kMaxNodes * ocro::kMaxNodes / 4];
-    __shared__ ocro::RollLevel Ls;
+    extern __shared__ uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
-    stage_roll_tables(R, dist_g, dist_w, Ls, subs);
-    const uint8_t* dist = (const uint8_t*)dist_w;
+    stage_roll_tables(R, blob_g, blob_w, subs);
+    const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
         const ocro::Row r = load_row<A, K>(sin, P, e);
-        ocro::RowOps<A, K> ops(Ls, dist);
+        ocro::RowOps<A, K> ops(R.L, blob);
         for (int i = 0; i < R.nsub; ++i) {
             float v;
             const bool ok = ops.full_bound(r, subs[i], v);
@@ -815,8 +817,9 @@ struct oc_handle {
     int32_t cus;                // compute units of the device (persistent grids: <= 5 blocks per CU)
     LevelArgs args;
     ocro::RollLevel roll;       // planner rollout tables (nnodes < 0: graph too large)
-    uint8_t* roll_dist = nullptr;  // device: reachability distances [kMaxNodes][kMaxNodes]
-    uint8_t roll_dist_host[ocro::kMaxNodes * ocro::kMaxNodes];  // the same table on the host
+    uint8_t* roll_blob = nullptr;  // device: the level's rollout table blob (oc_rollout.h)
+    int32_t roll_blob_bytes = 0;
+    uint8_t roll_blob_host[ocro::kBlobMax];  // the same blob on the host
 };
 
 // Statistics rows, shared by the blocks of every kernel modulo the row count; one more
@@ -835,7 +838,8 @@ const char* oc_last_error(void) { return g_last_error.c_str(); }
 int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_t device, oc_handle** out) {
     if (lv == nullptr || out == nullptr) return fail(OC_EINVAL, "null argument");
     const int W = lv->width, H = lv->height;
-    if (W < 3 || H < 3 || W * H > OC_MAX_CELLS) return fail(OC_ELEVEL, "grid %dx%d outside 3..64 cells", W, H);
+    if (W < 3 || H < 3 || W * H > OC_MAX_CELLS)
+        return fail(OC_ELEVEL, "grid %dx%d: width and height >= 3 and at most %d cells", W, H, OC_MAX_CELLS);
     if (num_agents < 1 || num_agents > OC_MAX_AGENTS) return fail(OC_EINVAL, "num_agents %d", num_agents);
     if (lv->num_spawns < num_agents || lv->num_spawns > OC_MAX_AGENTS) return fail(OC_ELEVEL, "num_spawns %d", lv->num_spawns);
     if (lv->num_items < 0 || lv->num_items > OC_MAX_ITEMS) return fail(OC_ELEVEL, "num_items %d", lv->num_items);
@@ -851,12 +855,8 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
         const int x = c % W, y = c / W;
         if (t == OC_TILE_FLOOR && (x == 0 || y == 0 || x == W - 1 || y == H - 1))
             return fail(OC_ELEVEL, "Floor on the border at (%d,%d)", x, y);
-        if (t == OC_TILE_FLOOR) L.floor_mask |= 1ull << c;
-        if (t == OC_TILE_CUTBOARD) L.cut_mask |= 1ull << c;
-        if (t == OC_TILE_DELIVERY) {
-            L.deliv_mask |= 1ull << c;
-            if (L.done_cell < 0) L.done_cell = c;
-        }
+        L.cls4[c >> 2] |= (uint32_t)ocsw::tile_class(t) << (8 * (c & 3));
+        if (t == OC_TILE_DELIVERY && L.done_cell < 0) L.done_cell = c;
     }
     if (L.done_cell < 0) return fail(OC_ELEVEL, "no Delivery tile");
     uint32_t seen_food = 0;
@@ -908,17 +908,19 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
         else
             (void)hipGetLastError();
     }
-    // planner rollout: the static reachability graph's BFS table (world.py:67-108)
+    // planner rollout: the static reachability graph's BFS table (world.py:67-108) and the
+    // level's other static tables, one blob per level (oc_rollout.h)
     {
-        uint8_t* dist = h->roll_dist_host;
-        const int n = ocro::build_roll_level(h->roll, dist, W, H, lv->tiles);
+        const int n = ocro::build_roll_level(h->roll, h->roll_blob_host, W, H, lv->tiles);
         if (n < 0) {
             h->roll.nnodes = -1;
         } else {
+            h->roll_blob_bytes = ocro::blob_bytes(n);
             if (hipSetDevice(device) != hipSuccess ||
-                hipMalloc(&h->roll_dist, sizeof(h->roll_dist_host)) != hipSuccess ||
-                hipMemcpy(h->roll_dist, dist, sizeof(h->roll_dist_host), hipMemcpyHostToDevice) != hipSuccess) {
-                h->roll_dist = nullptr;  // no device (e.g. a CPU-only build check): rollout unavailable
+                hipMalloc(&h->roll_blob, (size_t)h->roll_blob_bytes) != hipSuccess ||
+                hipMemcpy(h->roll_blob, h->roll_blob_host, (size_t)h->roll_blob_bytes, hipMemcpyHostToDevice) !=
+                    hipSuccess) {
+                h->roll_blob = nullptr;  // no device (e.g. a CPU-only build check): rollout unavailable
                 (void)hipGetLastError();
             }
         }
@@ -935,18 +937,17 @@ int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint8_t* node_of, in
     *num_nodes = n;
     if (node_of != nullptr) {
         if (node_of_len < (int64_t)cells * 5) return fail(OC_EINVAL, "node_of needs %d bytes", cells * 5);
-        for (int i = 0; i < cells * 5; ++i) node_of[i] = h->roll.node[i];
+        for (int i = 0; i < cells * 5; ++i) node_of[i] = h->roll_blob_host[ocro::kNodeOff + i];
     }
     if (dist != nullptr) {
         if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %d bytes", n * n);
-        for (int u = 0; u < n; ++u)
-            for (int v = 0; v < n; ++v) dist[u * n + v] = h->roll_dist_host[u * ocro::kMaxNodes + v];
+        for (int i = 0; i < n * n; ++i) dist[i] = h->roll_blob_host[ocro::kDistOff + i];
     }
     return OC_OK;
 }
 
 int oc_destroy(oc_handle* h) {
-    if (h != nullptr && h->roll_dist != nullptr) (void)hipFree(h->roll_dist);
+    if (h != nullptr && h->roll_blob != nullptr) (void)hipFree(h->roll_blob);
     delete h;
     return OC_OK;
 }
@@ -1069,9 +1070,10 @@ static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num
             return fail(OC_EINVAL, "subtask %d: only oc_rollout takes OC_LEVEL1", i);
     if (num_subtasks < 1 || num_subtasks > OC_MAX_SUBTASKS) return fail(OC_EINVAL, "num_subtasks %d", num_subtasks);
     if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes", ocro::kMaxNodes);
-    if (h->roll_dist == nullptr) return fail(OC_EHIP, "rollout tables not on the device");
+    if (h->roll_blob == nullptr) return fail(OC_EHIP, "rollout tables not on the device");
     R.L = h->roll;
     R.nsub = num_subtasks;
+    R.blob_words = h->roll_blob_bytes / 4;
     R.pitch = pitch_for(B);
     R.B = B;
     for (int i = 0; i < num_subtasks; ++i) {
@@ -1113,8 +1115,9 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_ROLL(A, K)                                                                                 \
-    hipLaunchKernelGGL((oc_rollout_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state_in,  \
-                       (uint8_t*)state_out, actions, alloc, h->roll_dist, out_flags, lower_bound)
+    hipLaunchKernelGGL((oc_rollout_kernel<A, K>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,                \
+                       (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags,    \
+                       lower_bound)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_ROLL)
     return hip_check("oc_rollout launch");
 }
@@ -1134,8 +1137,9 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_LIK(A, K)                                                                                     \
-    hipLaunchKernelGGL((oc_likelihood_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state, taken, \
-                       alloc, h->roll_dist, self_agent, beta, none_action_prob, likelihood, out_flags)
+    hipLaunchKernelGGL((oc_likelihood_kernel<A, K>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,              \
+                       (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,       \
+                       likelihood, out_flags)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_LIK)
     return hip_check("oc_nav_likelihood launch");
 }
@@ -1153,8 +1157,8 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_BOUNDS(A, K)                                                                             \
-    hipLaunchKernelGGL((oc_bounds_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state,     \
-                       h->roll_dist, lower_bound, doable)
+    hipLaunchKernelGGL((oc_bounds_kernel<A, K>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,            \
+                       (const uint8_t*)state, h->roll_blob, lower_bound, doable)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_BOUNDS)
     return hip_check("oc_subtask_bounds launch");
 }

@@ -9,8 +9,11 @@
 //   lower_bound()   get_lower_bound_for_subtask_given_objs  overcooked_environment.py:480-664,
 //                   World.get_lower_bound_between(_helper), check_bound  world.py:115-283
 // The reachability graph of the static level (world.py:67-108) is precomputed by
-// build_roll_level() as a compact all-pairs distance table (u8, 0xFF = no path); the kernel
-// stages it in LDS.  Distances and bounds are exact in fp32 (integers and halves < 2^8).
+// build_roll_level() as a compact all-pairs distance table (u8, 0xFF = no path).  The static
+// tables of a level (tile classes, graph node ids, Cutboard / Delivery lists, distances) form
+// one byte blob that the kernels stage in LDS, sized per level (kBlob*Off + nnodes^2 bytes):
+// a 7x7 kitchen's blob is ~6 KB, the largest (248 nodes) ~63 KB.  Distances and
+// bounds are exact in fp32 (integers and halves < 2^9).
 //
 // The includer defines __host__ / __device__ (HIP, or empty for the host test harness).
 #pragma once
@@ -24,17 +27,28 @@
 
 namespace ocro {
 
-constexpr int kMaxNodes = 160;  // compact reachability-graph nodes (LDS table kMaxNodes^2 bytes)
+constexpr int kMaxCells = 255;  // cell ids are bytes, 0xFF = dead / none
+// compact reachability-graph node ids are bytes (0xFF = none); at most 248 nodes keep a block's
+// LDS (blob + 64 configurations) within the 64 KB a launch gets without a function attribute
+constexpr int kMaxNodes = 248;
 constexpr uint8_t kNone = 0xFF;
 constexpr int kFloor = 0, kCounter = 1, kCutboard = 2, kDelivery = 3;  // OC_TILE_*
 constexpr int kNoop = 4;
 constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NAV_ACTIONS + (0, 0)
 
-struct RollLevel {
+// Static level tables, one byte blob: tile class per cell, node id per (cell, approach),
+// Cutboard and Delivery cells in scan order, then the nnodes x nnodes distance table.
+constexpr int kTileOff = 0;                        // [256] tile class (cells >= W*H: Counter)
+constexpr int kNodeOff = 256;                      // [256 * 5] cell * 5 + approach (4 = (0, 0))
+constexpr int kCutOff = kNodeOff + 256 * 5;        // [256] Cutboard cells, L.ncut of them
+constexpr int kDelivOff = kCutOff + 256;           // [256] Delivery cells, L.ndeliv of them
+constexpr int kDistOff = kDelivOff + 256;          // [nnodes][nnodes] BFS distances
+constexpr int kBlobMax = kDistOff + kMaxNodes * kMaxNodes;
+OC_RH int blob_bytes(int nnodes) { return (kDistOff + nnodes * nnodes + 3) & ~3; }
+
+struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t W, H, perimeter, nnodes;
-    uint64_t cut_cells, deliv_cells;  // static Cutboard / Delivery squares
-    uint8_t tile[64];                 // static tile class per cell
-    uint8_t node[64 * 5];             // cell * 5 + approach direction (4 = (0, 0)) -> compact node or kNone
+    int32_t ncut, ndeliv;
 };
 
 struct Sub {  // oc_subtask, device copy
@@ -60,20 +74,30 @@ struct Row {
     OC_RH int im(int j) const { return (int)b64(mask, j); }
 };
 
+// byte v occurs in one of the four bytes of w
+OC_RH bool has_byte(uint32_t w, uint32_t v) {
+    const uint32_t x = w ^ (v * 0x01010101u);
+    return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u;
+}
+
 // ---- host: level tables --------------------------------------------------------------------
 // Builds the reachability graph of make_reachability_graph (world.py:67-108) and its BFS
-// distances.  Returns the node count, or -1 when it exceeds kMaxNodes.
-inline int build_roll_level(RollLevel& L, uint8_t* dist /* kMaxNodes^2 */, int W, int H, const uint8_t* tiles) {
+// distances into `blob` (kBlobMax bytes).  Returns the node count, or -1 when the level has
+// more than kMaxCells cells or the graph more than kMaxNodes nodes.
+inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uint8_t* tiles) {
     L.W = W;
     L.H = H;
     L.perimeter = 2 * (W + H);
-    L.cut_cells = L.deliv_cells = 0;
-    for (int c = 0; c < 64; ++c) {
-        L.tile[c] = c < W * H ? tiles[c] : (uint8_t)kCounter;
-        if (c < W * H && tiles[c] == kCutboard) L.cut_cells |= 1ull << c;
-        if (c < W * H && tiles[c] == kDelivery) L.deliv_cells |= 1ull << c;
+    L.ncut = L.ndeliv = 0;
+    if (W * H > kMaxCells) return -1;
+    uint8_t* tile = blob + kTileOff;
+    uint8_t* node = blob + kNodeOff;
+    for (int c = 0; c < 256; ++c) {
+        tile[c] = c < W * H ? tiles[c] : (uint8_t)kCounter;
+        if (c < W * H && tiles[c] == kCutboard) blob[kCutOff + L.ncut++] = (uint8_t)c;
+        if (c < W * H && tiles[c] == kDelivery) blob[kDelivOff + L.ndeliv++] = (uint8_t)c;
     }
-    for (int i = 0; i < 64 * 5; ++i) L.node[i] = kNone;
+    for (int i = 0; i < 256 * 5; ++i) node[i] = kNone;
     int n = 0;
     auto clampx = [&](int v) { return v < 0 ? 0 : (v > W - 1 ? W - 1 : v); };
     auto clampy = [&](int v) { return v < 0 ? 0 : (v > H - 1 ? H - 1 : v); };
@@ -82,13 +106,13 @@ inline int build_roll_level(RollLevel& L, uint8_t* dist /* kMaxNodes^2 */, int W
         const bool coll = tiles[c] != kFloor;
         if (!coll) {
             if (n >= kMaxNodes) return -1;
-            L.node[c * 5 + 4] = (uint8_t)n++;
+            node[c * 5 + 4] = (uint8_t)n++;
         }
         for (int d = 0; d < 4; ++d) {
             const int nc = clampy(y + kDY[d]) * W + clampx(x + kDX[d]);
             if (coll && tiles[nc] == kFloor) {
                 if (n >= kMaxNodes) return -1;
-                L.node[c * 5 + d] = (uint8_t)n++;
+                node[c * 5 + d] = (uint8_t)n++;
             }
         }
     }
@@ -96,7 +120,7 @@ inline int build_roll_level(RollLevel& L, uint8_t* dist /* kMaxNodes^2 */, int W
     // adjacency (undirected): floor-floor, and a collidable square's approach node with the
     // floor it is approached from
     static const int opp[4] = {1, 0, 3, 2};
-    uint8_t adj[kMaxNodes][8];
+    static uint8_t adj[kMaxNodes][8];
     int deg[kMaxNodes] = {0};
     auto link = [&](int u, int v) {
         if (u == kNone || v == kNone || u == v) return;
@@ -111,14 +135,15 @@ inline int build_roll_level(RollLevel& L, uint8_t* dist /* kMaxNodes^2 */, int W
         for (int d = 0; d < 4; ++d) {
             const int nc = clampy(y + kDY[d]) * W + clampx(x + kDX[d]);
             const bool ncoll = tiles[nc] != kFloor;
-            if (coll && !ncoll) link(L.node[c * 5 + d], L.node[nc * 5 + 4]);
-            else if (!coll && ncoll) link(L.node[c * 5 + 4], L.node[nc * 5 + opp[d]]);
-            else if (!coll && !ncoll) link(L.node[c * 5 + 4], L.node[nc * 5 + 4]);
+            if (coll && !ncoll) link(node[c * 5 + d], node[nc * 5 + 4]);
+            else if (!coll && ncoll) link(node[c * 5 + 4], node[nc * 5 + opp[d]]);
+            else if (!coll && !ncoll) link(node[c * 5 + 4], node[nc * 5 + 4]);
         }
     }
+    uint8_t* dist = blob + kDistOff;
     for (int s = 0; s < n; ++s) {
-        uint8_t* row = dist + s * kMaxNodes;
-        for (int t = 0; t < kMaxNodes; ++t) row[t] = kNone;
+        uint8_t* row = dist + s * n;
+        for (int t = 0; t < n; ++t) row[t] = kNone;
         int q[kMaxNodes], qh = 0, qt = 0;
         row[s] = 0;
         q[qt++] = s;
@@ -140,14 +165,15 @@ inline int build_roll_level(RollLevel& L, uint8_t* dist /* kMaxNodes^2 */, int W
 template <int A, int K>
 struct RowOps {
     const RollLevel& L;
-    const uint8_t* dist;  // LDS on the device
-    uint64_t ac = 0;        // AgentCounter cells of this row's Level-0 view
+    const uint8_t* T;       // the level's table blob (LDS on the device)
+    uint32_t ac = 0xFFFFFFFFu;  // AgentCounter cells of this row's Level-0 view, one per byte (0xFF none)
     uint32_t active = 0;    // bit a: agent a is a subtask agent
     uint32_t blockers = 0;  // bit a: agent a's cell may not be moved into (get_single_actions)
 
-    OC_RH RowOps(const RollLevel& l, const uint8_t* d) : L(l), dist(d) {}
+    OC_RH RowOps(const RollLevel& l, const uint8_t* blob) : L(l), T(blob) {}
 
-    OC_RH int tile(int cell) const { return (ac >> cell) & 1u ? kCounter : L.tile[cell]; }
+    OC_RH int static_tile(int cell) const { return T[kTileOff + cell]; }
+    OC_RH int tile(int cell) const { return has_byte(ac, (uint32_t)cell) ? kCounter : T[kTileOff + cell]; }
     OC_RH int cell(int x, int y) const { return y * L.W + x; }
     OC_RH int agent_cell(const Row& r, int a) const { return cell(r.ax(a), r.ay(a)); }
 
@@ -172,9 +198,9 @@ struct RowOps {
                 Row::s64(r.mask, hh, 0);
                 Row::s32(r.h, a, kNone);
             }
-            const uint64_t bit = 1ull << agent_cell(r, a);
-            raised |= (ac & bit) != 0;
-            ac |= bit;
+            const uint32_t c = (uint32_t)agent_cell(r, a);
+            raised |= has_byte(ac, c);
+            Row::s32(ac, a, c);
         }
         return raised;
     }
@@ -275,25 +301,26 @@ struct RowOps {
     OC_RH bool is_goal(const Row& r, const Sub& s) const {
         if (s.kind == 0) return true;
         int count = 0;
-        uint64_t seen = 0;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const int c = r.il(j);
             if (c == kNone || r.im(j) != s.goal) continue;
             if (s.kind == 3) {  // un-held goal items on a Delivery square
-                count += (L.deliv_cells >> c) & 1u ? 1 : 0;
-            } else {  // distinct locations of goal items, held or not
-                count += (seen >> c) & 1u ? 0 : 1;
-                seen |= 1ull << c;
+                count += static_tile(c) == kDelivery ? 1 : 0;
+            } else {  // distinct locations of goal items, held or not: count a slot's cell once
+                bool dup = false;
+#pragma unroll
+                for (int i = 0; i < j; ++i) dup |= r.il(i) == c && r.im(i) == s.goal;
+                count += dup ? 0 : 1;
             }
         }
         return count > s.count;
     }
 
     OC_RH int rg(int c1, int d1, int c2, int d2) const {  // nx.shortest_path_length or -1
-        const int u = L.node[c1 * 5 + d1], v = L.node[c2 * 5 + d2];
+        const int u = T[kNodeOff + c1 * 5 + d1], v = T[kNodeOff + c2 * 5 + d2];
         if (u == kNone || v == kNone) return -1;
-        const int d = dist[u * kMaxNodes + v];
+        const int d = T[kDistOff + u * L.nnodes + v];
         return d == kNone ? -1 : d;
     }
 
@@ -355,7 +382,7 @@ struct RowOps {
                 if (!((active >> a) & 1u) || h == kNone || r.im(h) != m) continue;
                 c = agent_cell(r, a);
             }
-            if (skip_deliv && ((L.deliv_cells >> c) & 1u)) continue;
+            if (skip_deliv && static_tile(c) == kDelivery) continue;
             f(c);
         }
     }
@@ -382,10 +409,11 @@ struct RowOps {
         }
         float lower = (float)L.perimeter + 1.0f;
         if (s.kind == 1 || s.kind == 3) {
-            const uint64_t bset = s.kind == 1 ? L.cut_cells : L.deliv_cells;
+            const uint8_t* bl = T + (s.kind == 1 ? kCutOff : kDelivOff);
+            const int nb = s.kind == 1 ? L.ncut : L.ndeliv;
             visit_objs(r, s.start[0], s.kind == 3, [&](int Ac) OC_RL {
-                for (uint64_t m = bset; m; m &= m - 1) {
-                    const float b = helper(s, ag0, ag1, Ac, __builtin_ctzll(m));
+                for (int i = 0; i < nb; ++i) {
+                    const float b = helper(s, ag0, ag1, Ac, bl[i]);
                     if (b < lower) lower = b;
                 }
             });
@@ -404,7 +432,7 @@ struct RowOps {
     // given_objs; returns BayesianDelegator.subtask_alloc_is_doable (bayesian_delegator.py:98-156):
     // None -> true, else the distance < world.perimeter.
     OC_RH bool full_bound(const Row& r, const Sub& s, float& lb) {
-        ac = 0;
+        ac = 0xFFFFFFFFu;
         active = 1u << s.agent[0];
         if (s.n == 2) active |= 1u << s.agent[1];
         blockers = active;
@@ -462,7 +490,7 @@ struct RowOps {
         if (s.kind == 0) {  // None: one agent, the self agent's movable actions in the full state
             if (s.n != 1) return 4;
             active = blockers = (1u << A) - 1u;
-            ac = 0;
+            ac = 0xFFFFFFFFu;
             int n = 0;
             for (int c = 0; c < 4; ++c) n += single_legal(r, self_agent, c) ? 1 : 0;
             if (n == 0) return 8;

@@ -4,7 +4,7 @@
 // env q of that lane (q = 0..3).  The step runs on those words directly: all per-env
 // predicates are byte masks, computed with carry-free byte arithmetic and v_bitop3 logic,
 // selects are v_bitop3 (m ? a : b), per-env table lookups are v_perm byte selects, and the
-// tile class of a cell comes from a 64-entry LDS table.  Measured on MI355X (tools/
+// tile class of a cell comes from a 256-entry LDS table.  Measured on MI355X (tools/
 // valubench.hip): v_add / v_xor / shifts / v_bitop3 issue at ~2.9 cycles per wave-instruction,
 // v_perm / v_bfi / v_bfe / v_cndmask / v_cmp at ~5, so the formulation leans on the former.
 //
@@ -60,6 +60,8 @@ OC_SW uint32_t nz80(uint32_t x) { return (x + k7F) & k80; }
 OC_SW uint32_t z80(uint32_t x) { return andn(k80, x + k7F); }
 // bytes may have bit 7 set (0xFF sentinels): h80 of (a == b) on the low 7 bits
 OC_SW uint32_t eq80(uint32_t a, uint32_t b) { return z80(bop3<OC_LUT((a ^ b) & c)>(a, b, k7F)); }
+// any bytes: h80 of (byte == 0) over all 8 bits
+OC_SW uint32_t zf80(uint32_t x) { return andn(k80, ((x & k7F) + k7F) | x); }
 
 // Per-level constants the SWAR step reads (all wave-uniform, kernel-argument resident).
 struct SwarLevel {
@@ -72,6 +74,10 @@ struct SwarLevel {
     uint32_t maxT_rep;       // max_T replicated to both u16 halves (0 = no limit)
     uint32_t tmpl_x[4], tmpl_y[4], tmpl_l[8], tmpl_m[8];  // reset template, replicated
     int32_t tall;            // H > 8: y*W by multiply instead of the 8-entry LUT
+    int32_t big;             // W*H > 128: cell ids reach bit 7, so cell compares use all 8 bits
+                             // and the move delta is added as (positive part) - (negative part)
+                             // (each byte stays in 0..254, no carry between envs)
+    uint32_t dp_lo, dp_hi, dn_lo, dn_hi;  // big: v_perm LUTs action code -> max(delta, 0), max(-delta, 0)
 };
 
 // Host-side construction of the SwarLevel constants (called by oc_create after validation).
@@ -82,7 +88,19 @@ __host__ __device__ inline void build_swar_level(SwarLevel& S, int W, int H, int
     S = SwarLevel{};
     S.W = (uint32_t)W;
     S.tall = H > 8;
+    S.big = W * H > 128;
     const int dcell[5] = {W, -W, -1, 1, 0};
+    for (int c = 0; c < 8; ++c) {
+        const int d = c < 5 ? dcell[c] : 0;
+        const uint32_t pv = (uint32_t)(d > 0 ? d : 0), nv = (uint32_t)(d < 0 ? -d : 0);
+        if (c < 4) {
+            S.dp_lo |= pv << (8 * c);
+            S.dn_lo |= nv << (8 * c);
+        } else {
+            S.dp_hi |= pv << (8 * (c - 4));
+            S.dn_hi |= nv << (8 * (c - 4));
+        }
+    }
     for (int y = 0; y < 8; ++y) {
         const uint32_t v = (uint32_t)(y * W) & 0xFFu;
         if (y < 4) S.yw_lo |= v << (8 * y); else S.yw_hi |= v << (8 * (y - 4));
@@ -105,10 +123,10 @@ __host__ __device__ inline void build_swar_level(SwarLevel& S, int W, int H, int
     }
 }
 
-// Tile class byte of a cell (the LDS table): 0x80 Floor, 0x40 Delivery, 0x20 Cutboard.
-__host__ __device__ inline uint8_t tile_class(uint64_t floor_mask, uint64_t deliv_mask, uint64_t cut_mask, uint32_t c) {
-    if (c >= 64u) return 0;
-    return (uint8_t)((((floor_mask >> c) & 1u) << 7) | (((deliv_mask >> c) & 1u) << 6) | (((cut_mask >> c) & 1u) << 5));
+// Tile class byte of a cell (the LDS table) from its OC_TILE_* code: 0x80 Floor, 0x40 Delivery,
+// 0x20 Cutboard, 0 Counter (and every cell id past the grid).
+__host__ __device__ inline uint8_t tile_class(int tile) {
+    return (uint8_t)(tile == 0 ? 0x80 : tile == 3 ? 0x40 : tile == 2 ? 0x20 : 0);
 }
 
 // dx + 1 / dy + 1 per action code (World.NAV_ACTIONS order, world.py:16, + no-op)
@@ -153,7 +171,10 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         else
             yw = perm(L.yw_hi, L.yw_lo, Y[a]);
         loc[a] = yw + X[a];
-        nraw[a] = (loc[a] + perm(L.dc_hi, L.dc_lo, c)) ^ k80;  // loc + delta (bias removed)
+        if (L.big)  // wave-uniform: cells up to 254, loc + delta in two carry-free halves
+            nraw[a] = loc[a] + perm(L.dp_hi, L.dp_lo, c) - perm(L.dn_hi, L.dn_lo, c);
+        else  // cells < 128: loc + (delta + 0x80) stays in its byte, bias removed
+            nraw[a] = (loc[a] + perm(L.dc_hi, L.dc_lo, c)) ^ k80;
         cls[a] = cls_of(nraw[a]);
         const uint32_t onF80 = cls[a] & k80;
         nxt[a] = sel(full80(onF80), nraw[a], loc[a]);
@@ -168,8 +189,14 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
     for (int i = 0; i < A; ++i) {
 #pragma unroll
         for (int j = i + 1; j < A; ++j, ++p) {
-            const uint32_t eq = z80(nxt[i] ^ nxt[j]);
-            const uint32_t sw = bop3<OC_LUT((!a) & (!b) & c)>((loc[i] ^ nxt[j]) + k7F, (loc[j] ^ nxt[i]) + k7F, k80);
+            uint32_t eq, sw;
+            if (L.big) {  // cell bytes reach bit 7: full-byte zero tests (no carry between envs)
+                eq = zf80(nxt[i] ^ nxt[j]);
+                sw = zf80(loc[i] ^ nxt[j]) & zf80(loc[j] ^ nxt[i]);
+            } else {
+                eq = z80(nxt[i] ^ nxt[j]);
+                sw = bop3<OC_LUT((!a) & (!b) & c)>((loc[i] ^ nxt[j]) + k7F, (loc[j] ^ nxt[i]) + k7F, k80);
+            }
             const uint32_t bi = bop3<OC_LUT(a ? !b : c)>(eq, bump80[i], sw);
             const uint32_t u = bop3<OC_LUT((a | !b) & c)>(bump80[i], bump80[j], k80);
             const uint32_t bj = sel(eq, u, sw);
@@ -194,7 +221,7 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         uint32_t at80[K], seen = 0u, ob0 = 0u, ob1 = 0u, ob2 = 0u;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            at80[j] = eq80(Lc[j], tc);
+            at80[j] = L.big ? zf80(Lc[j] ^ tc) : eq80(Lc[j], tc);
             seen |= at80[j];
             if (j & 1) ob0 |= at80[j];
             if (j & 2) ob1 |= at80[j];
@@ -286,9 +313,14 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
     uint32_t ok = k80;
     for (int g = 0; g < L.ngoals; ++g) {  // every Deliver goal: an item == goal at the delivery cell
         uint32_t hit = 0u;
+        if (L.big) {  // masks are < 0x80, so bit 7 of the OR comes from the cell compare only
 #pragma unroll
-        for (int j = 0; j < K; ++j)
-            hit |= z80(bop3<OC_LUT((a | b) & c)>(Lc[j] ^ L.done_rep, M[j] ^ L.goals_rep[g], k7F));
+            for (int j = 0; j < K; ++j) hit |= zf80((Lc[j] ^ L.done_rep) | (M[j] ^ L.goals_rep[g]));
+        } else {
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                hit |= z80(bop3<OC_LUT((a | b) & c)>(Lc[j] ^ L.done_rep, M[j] ^ L.goals_rep[g], k7F));
+        }
         ok &= hit;
     }
     const uint32_t done80 = or3(err, tout, ok);

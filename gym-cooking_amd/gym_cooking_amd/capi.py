@@ -16,11 +16,12 @@ LIB_PATH = os.path.join(PKG_DIR, "liboc_engine.so")
 
 OC_MAX_AGENTS = 4
 OC_MAX_ITEMS = 8
-OC_MAX_CELLS = 64
+OC_MAX_CELLS = 255
 OC_MAX_GOALS = 4
 OC_PITCH_ALIGN = 4096
 OC_NSTATS = 5
-OC_ABI_VERSION = 2  # include/oc_engine.h
+OC_ABI_VERSION = 3  # include/oc_engine.h
+OC_EINVAL, OC_EHIP, OC_ELEVEL = -1, -2, -3
 
 OC_FLAG_DONE = 0x01
 OC_FLAG_SUCCESS = 0x02
@@ -197,7 +198,13 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     return lib
 
 
+class LevelError(RuntimeError):
+    """OC_ELEVEL: the level is outside an entry point's envelope (e.g. a reachability graph of
+    more than 248 nodes for the planner entry points)."""
+
+
 def check(rc: int) -> None:
     if rc != 0:
         msg = _lib.oc_last_error().decode() if _lib is not None else "?"
-        raise RuntimeError("oc_engine error %d: %s" % (rc, msg))
+        cls = LevelError if rc == OC_ELEVEL else RuntimeError
+        raise cls("oc_engine error %d: %s" % (rc, msg))

@@ -440,6 +440,7 @@ class OvercookedEnvironment:
         self._engine = None
         self._host = None
         self._group_names = frozenset()
+        self._step_raises = False
         self.game = None
 
     # -- reference bookkeeping ------------------------------------------------------------
@@ -456,7 +457,12 @@ class OvercookedEnvironment:
             from .engine import OvercookedBatch  # raises without liboc_engine.so / a GPU
             level = self.arglist.level
             self.level = _levels.load_level(level) if isinstance(level, str) else level
-            self._engine = _Single(OvercookedBatch(self.level, self.arglist.num_agents, 1,
+            if self.level.missing:  # reset raises KeyError in make_reachability_graph (world.py:79-86)
+                raise KeyError(self.level.reset_key_error())
+            # squares past the world width: reset works and every step raises after executing
+            # (display -> World.add_object, overcooked_environment.py:283 -> world.py:302)
+            self._step_raises = bool(self.level.overflow)
+            self._engine = _Single(OvercookedBatch(self.level.within_width(), self.arglist.num_agents, 1,
                                                    max_T=self.arglist.max_num_timesteps, device=self._device))
         return self._engine
 
@@ -514,6 +520,8 @@ class OvercookedEnvironment:
         self._host = new
         self._refresh(executed)
         self.agent_actions = {n: act for n, act in zip(names, executed)}
+        if self._step_raises:
+            raise IndexError("list assignment index out of range")  # world.py:302
         if self._flags & FLAG_ERR:
             raise CopyCrash("two co-located agents both hold items: the reference crashes in copy.copy "
                             "(overcooked_environment.py:289 -> world.py:417)")
@@ -672,8 +680,11 @@ class _Single:
         self.s_in, self.s_out = batch.new_state(), batch.new_state()
         self.act, self.ex, self.coll = batch.new_actions(), batch.new_exec(), batch.new_coll()
         self._t = batch.layout.plane_t
-        node_of, dist = batch.reachability()
-        self.reach = ReachabilityGraph(batch.level.width, node_of, dist)
+        try:
+            node_of, dist = batch.reachability()
+            self.reach = ReachabilityGraph(batch.level.width, node_of, dist)
+        except capi.LevelError:  # graph past the planner tables' 248 nodes: stepping still works
+            self.reach = None
 
     def _download(self, buf) -> np.ndarray:
         host = buf.view(self.NP, self.P)[:, :2].cpu().numpy()  # env 0 of every plane (+ t's high byte)

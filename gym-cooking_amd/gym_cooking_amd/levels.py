@@ -11,7 +11,14 @@ goal masks.  It restates the parsing rules of the reference loader
   any other character becomes Floor (overcooked_environment.py:170-173);
 * only Floor is non-collidable (core.py:34, 64);
 * width is the last map row's length, height the number of map rows
-  (overcooked_environment.py:196-197);
+  (overcooked_environment.py:196-197).  Ragged maps follow from that: a row longer than
+  the last one puts squares past the world width: ``reset`` works, but every ``step``
+  raises ``IndexError`` after executing the actions, when ``display`` writes those squares
+  into a width-wide character grid (overcooked_environment.py:283 -> world.py:50, :302);
+  a row shorter than the last one leaves squares of the grid without a GridSquare, and
+  ``reset`` raises ``KeyError`` in ``make_reachability_graph`` (overcooked_environment.py:235
+  -> world.py:79-86).  The batched engine refuses both (IndexError / KeyError at creation);
+  the single-env shim mirrors the reference call by call;
 * agents ``agent-1..A`` take the first A spawn lines (overcooked_environment.py:186-193);
 * recipe lines name recipe classes (recipe_planner/recipe.py:199-228); each recipe
   contributes one ``Deliver(full_plate_name)`` subtask (recipe.py:39-47) whose goal
@@ -19,7 +26,9 @@ goal masks.  It restates the parsing rules of the reference loader
 
 Item contents are encoded as a 7-bit mask: bit0 Tomato,
 bit1 Lettuce, bit2 Onion, bit3 Plate, bit4/5/6 Tomato/Lettuce/Onion chopped.  The
-mask is exact because a level may hold at most one of each food type (validated).
+mask is exact because a level may hold at most one of each food type (validated: a
+second Tomato, Lettuce or Onion is rejected, since a merged dish of two of one food has
+no mask).  Grids of up to 255 cells are supported (cell ids are bytes, 0xFF = dead).
 """
 from __future__ import annotations
 
@@ -44,7 +53,7 @@ M_FOODS = M_TOMATO | M_LETTUCE | M_ONION
 # Engine limits (include/oc_engine.h).
 MAX_AGENTS = 4
 MAX_ITEMS = 8
-MAX_CELLS = 64
+MAX_CELLS = 255
 MAX_GOALS = 4
 LOC_DEAD = 0xFF
 HOLD_NONE = 0xFF
@@ -117,6 +126,10 @@ class Level:
     items: List[Tuple[int, int]]          # (cell, mask) in map scan order
     spawns: List[Tuple[int, int]]         # (x, y) spawn lines
     recipes: List[str]
+    # ragged maps: grid squares with no map character (a row shorter than the last one) and
+    # map characters past the world width (a row longer than the last one), as (x, y, char)
+    missing: List[Tuple[int, int]] = dataclasses.field(default_factory=list)
+    overflow: List[Tuple[int, int, str]] = dataclasses.field(default_factory=list)
 
     @property
     def ncells(self) -> int:
@@ -150,10 +163,37 @@ class Level:
     def xy(self, cell: int) -> Tuple[int, int]:
         return cell % self.width, cell // self.width
 
+    def within_width(self) -> "Level":
+        """The same level without the squares past the world width (what a step sees before
+        the reference's display raises)."""
+        return dataclasses.replace(self, overflow=[])
+
+    def reset_key_error(self) -> Tuple[int, int]:
+        """The location whose lookup raises KeyError when the reference's reset builds the
+        reachability graph of a map with missing squares: make_reachability_graph visits x
+        then y and reads each square, then its four inbounds neighbours (world.py:79-86)."""
+        miss = set(self.missing)
+        W, H = self.width, self.height
+        for x in range(W):
+            for y in range(H):
+                if (x, y) in miss:
+                    return (x, y)
+                for dx, dy in ACTIONS[:4]:
+                    n = (min(max(x + dx, 0), W - 1), min(max(y + dy, 0), H - 1))
+                    if n in miss:
+                        return n
+        raise AssertionError("no missing square")
+
     def validate(self, num_agents: int) -> None:
         """Reject levels outside the engine's exact-semantics envelope (raises ValueError)."""
         if not 1 <= num_agents <= MAX_AGENTS:
             raise ValueError("num_agents must be in 1..%d" % MAX_AGENTS)
+        if self.missing:  # the reference cannot reset this level
+            raise KeyError(self.reset_key_error())
+        if self.overflow:  # the reference raises in every step
+            x, y, _ = self.overflow[0]
+            raise IndexError("level %s: square (%d,%d) lies past the world width %d; the reference's step "
+                             "raises IndexError in World.add_object (world.py:302)" % (self.name, x, y, self.width))
         if len(self.spawns) < num_agents:
             raise ValueError("level %s has %d spawns < %d agents" % (self.name, len(self.spawns), num_agents))
         if self.ncells > MAX_CELLS:
@@ -207,20 +247,26 @@ def parse_level_text(text: str, name: str = "custom") -> Level:
             spawns.append((int(xs[0]), int(xs[1])))
     if not rows:
         raise ValueError("empty map")
-    width = len(rows[-1])
-    if any(len(r) != width for r in rows):
-        raise ValueError("ragged map rows are not supported")
+    width = len(rows[-1])  # world.width = x + 1 of the last map row (:196)
     tiles: List[int] = []
     items: List[Tuple[int, int]] = []
+    missing: List[Tuple[int, int]] = []
+    overflow: List[Tuple[int, int, str]] = []
     for y, row in enumerate(rows):
-        for x, ch in enumerate(row):
+        for x in range(width):
+            if x >= len(row):  # no GridSquare here: the reference's reset raises KeyError
+                missing.append((x, y))
+                tiles.append(TILE_COUNTER)
+                continue
+            ch = row[x]
             if ch in _CHAR_ITEM:
                 tiles.append(TILE_COUNTER)
                 items.append((y * width + x, _CHAR_ITEM[ch]))
             else:
                 tiles.append(_CHAR_TILE.get(ch, TILE_FLOOR))
+        overflow.extend((x, y, row[x]) for x in range(width, len(row)))
     return Level(name=name, width=width, height=len(rows), tiles=tiles, items=items,
-                 spawns=spawns, recipes=recipes)
+                 spawns=spawns, recipes=recipes, missing=missing, overflow=overflow)
 
 
 def _builtin(divider: str, recipes: Sequence[str], name: str) -> Level:

@@ -35,11 +35,11 @@
 extern "C" {
 #endif
 
-#define OC_ABI_VERSION 2
+#define OC_ABI_VERSION 3
 
 #define OC_MAX_AGENTS 4
 #define OC_MAX_ITEMS 8
-#define OC_MAX_CELLS 64
+#define OC_MAX_CELLS 255  /* cell ids are bytes; 0xFF is OC_LOC_DEAD */
 #define OC_MAX_GOALS 4
 #define OC_PITCH_ALIGN 4096
 
@@ -89,7 +89,7 @@ extern "C" {
 #define OC_NSTATS 5
 
 typedef struct oc_level_desc {
-    int32_t width, height;           /* width*height <= OC_MAX_CELLS; non-Floor border */
+    int32_t width, height;           /* 3..; width*height <= OC_MAX_CELLS; non-Floor border */
     int32_t num_items;               /* <= OC_MAX_ITEMS, at most one of each food type */
     int32_t num_spawns;              /* >= num_agents */
     int32_t num_goals;               /* 1..OC_MAX_GOALS Deliver goal masks */

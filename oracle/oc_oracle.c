@@ -52,7 +52,7 @@ typedef struct {
     Agent agents[OC_MAX_AGENTS];
     /* planner Level-0 view (e2e_brtdp.py:389-406): agents outside the subtask are removed
      * from sim_agents and their Floor becomes an AgentCounter; 0 / all-active on the env step */
-    uint64_t agent_counter;
+    int ac_cell[OC_MAX_AGENTS]; /* AgentCounter cells (-1 none), one per removed agent */
     int active[OC_MAX_AGENTS];
 } Env;
 
@@ -72,7 +72,8 @@ static int action_code(Loc a) {
 static int gridsquare_at(const Env* e, Loc l) {
     if (l.x < 0 || l.y < 0 || l.x >= e->L->width || l.y >= e->L->height) abort();
     const int c = l.y * e->L->width + l.x;
-    if ((e->agent_counter >> c) & 1u) return OC_TILE_COUNTER; /* AgentCounter (core.py:79-93) */
+    for (int a = 0; a < OC_MAX_AGENTS; ++a)
+        if (e->ac_cell[a] == c) return OC_TILE_COUNTER; /* AgentCounter (core.py:79-93) */
     return e->L->tiles[c];
 }
 
@@ -347,8 +348,10 @@ static void unpack(const Cfg* c, const uint8_t* s, int64_t e, Env* env, int* fla
     }
     for (int a = 0; a < A; ++a)
         if (env->agents[a].holding >= 0) env->objs[env->agents[a].holding].is_held = 1;
-    env->agent_counter = 0;
-    for (int a = 0; a < OC_MAX_AGENTS; ++a) env->active[a] = 1;
+    for (int a = 0; a < OC_MAX_AGENTS; ++a) {
+        env->ac_cell[a] = -1;
+        env->active[a] = 1;
+    }
 }
 
 static void pack(const Cfg* c, const Env* env, int flags, uint8_t* s, int64_t e) {
@@ -552,9 +555,10 @@ static int level0_view(Env* e, const oc_subtask* s) {
         }
         /* env.world.remove(Floor(location)) asserts when a second removed agent stands on an
          * already replaced Floor (world.py:307-315) */
-        const uint64_t bit = 1ull << cell_of(e, ag->location);
-        if (e->agent_counter & bit) raised = 1;
-        e->agent_counter |= bit; /* Floor -> AgentCounter */
+        const int c = cell_of(e, ag->location);
+        for (int b = 0; b < OC_MAX_AGENTS; ++b)
+            if (e->ac_cell[b] == c) raised = 1;
+        e->ac_cell[a] = c; /* Floor -> AgentCounter */
     }
     return raised;
 }

@@ -78,6 +78,14 @@ def canonical(state: np.ndarray, A: int, K: int, pitch: int, width: int, B: int)
     return dict(t=v["t"][:B].copy(), flags=v["fl"][:B].copy(), agents=agents, items=items[:, :4])
 
 
+def load_level(name: str) -> levels.Level:
+    """A builtin level by name, or a committed level file (tests/golden/levels/*.txt, stored
+    in fixtures as a path relative to tests/golden)."""
+    if name.endswith(".txt") and not os.path.isabs(name):
+        name = os.path.join(GOLDEN, name)
+    return levels.load_level(name)
+
+
 def load_fixture(name: str) -> Dict[str, np.ndarray]:
     """All arrays of a golden .npz, materialised (NpzFile re-reads an array on every index)."""
     with np.load(os.path.join(GOLDEN, name)) as z:
@@ -91,7 +99,7 @@ class EpisodeGroup:
         self.fx = fx
         self.idx = idx
         e0 = idx[0]
-        self.level = levels.load_level(str(fx["level_names"][fx["ep_level"][e0]]))
+        self.level = load_level(str(fx["level_names"][fx["ep_level"][e0]]))
         self.A = int(fx["ep_A"][e0])
         self.max_T = int(fx["ep_maxT"][e0])
         self.B = len(idx)
@@ -234,7 +242,7 @@ class RolloutRows:
         if limit is not None and len(sel) > limit:
             sel = sel[np.linspace(0, len(sel) - 1, limit).astype(int)]
         self.idx = sel
-        self.level = levels.load_level(str(fx["cfg_level"][cfg]))
+        self.level = load_level(str(fx["cfg_level"][cfg]))
         self.A = int(fx["cfg_A"][cfg])
         self.K = capi.item_slots(self.level)
         st = fx["state"][sel]
@@ -323,7 +331,7 @@ class LikelihoodRows:
         sel = np.nonzero((st_cfg == cfg) & (fx["self_agent"] == self_agent))[0]
         self.idx = sel
         self.self_agent = self_agent
-        self.level = levels.load_level(str(fx["cfg_level"][cfg]))
+        self.level = load_level(str(fx["cfg_level"][cfg]))
         self.A = int(fx["cfg_A"][cfg])
         self.K = capi.item_slots(self.level)
         st = fx["state"][sel]
@@ -376,7 +384,7 @@ class BoundRows:
 
     def __init__(self, fx, cfg: int):
         st_sel = np.nonzero(fx["st_cfg"] == cfg)[0]
-        self.level = levels.load_level(str(fx["cfg_level"][cfg]))
+        self.level = load_level(str(fx["cfg_level"][cfg]))
         self.A = int(fx["cfg_A"][cfg])
         self.K = capi.item_slots(self.level)
         self.agents, self.items, self.t = fx["st_agents"][st_sel], fx["st_items"][st_sel], fx["st_t"][st_sel]

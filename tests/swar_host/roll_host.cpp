@@ -14,9 +14,9 @@
 template <int A, int K>
 static void run(const oc_level_desc* lv, const uint8_t* sin, uint8_t* sout, const uint8_t* act, const uint8_t* alloc,
                 const oc_subtask* subs, int nsub, uint8_t* flags, float* lb, int64_t B, int64_t P) {
-    static uint8_t dist[ocro::kMaxNodes * ocro::kMaxNodes];
+    static uint8_t blob[ocro::kBlobMax];
     ocro::RollLevel L;
-    ocro::build_roll_level(L, dist, lv->width, lv->height, lv->tiles);
+    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles) < 0) return;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
     for (int64_t e = 0; e < B; ++e) {
         ocro::Row r;
@@ -37,7 +37,7 @@ static void run(const oc_level_desc* lv, const uint8_t* sin, uint8_t* sout, cons
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
                         {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
             const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
-            ocro::RowOps<A, K> ops(L, dist);
+            ocro::RowOps<A, K> ops(L, blob);
             f = ops.run(r, s, c0, c1, bound);
         }
         for (int a = 0; a < A; ++a) {
@@ -61,9 +61,9 @@ template <int A, int K>
 static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* taken_p, const uint8_t* alloc,
                 const oc_subtask* subs, int nsub, int self_agent, double beta, double nap, double* out, uint8_t* flags,
                 int64_t B, int64_t P) {
-    static uint8_t dist[ocro::kMaxNodes * ocro::kMaxNodes];
+    static uint8_t blob[ocro::kBlobMax];
     ocro::RollLevel L;
-    ocro::build_roll_level(L, dist, lv->width, lv->height, lv->tiles);
+    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles) < 0) return;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
     for (int64_t e = 0; e < B; ++e) {
         const int ai = alloc ? alloc[e] : 0;
@@ -85,7 +85,7 @@ static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* take
             const oc_subtask& o = subs[ai];
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
                         {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
-            ocro::RowOps<A, K> ops(L, dist);
+            ocro::RowOps<A, K> ops(L, blob);
             f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
         }
         out[e] = f == OC_LIK_OK ? v : 0.0;
@@ -117,9 +117,9 @@ extern "C" int roll_host(const oc_level_desc* lv, int A, int K, const uint8_t* s
 template <int A, int K>
 static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask* subs, int nsub, float* lb,
                    uint8_t* doable, int64_t B, int64_t P) {
-    static uint8_t dist[ocro::kMaxNodes * ocro::kMaxNodes];
+    static uint8_t blob[ocro::kBlobMax];
     ocro::RollLevel L;
-    ocro::build_roll_level(L, dist, lv->width, lv->height, lv->tiles);
+    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles) < 0) return;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
     for (int64_t e = 0; e < B; ++e) {
         ocro::Row r;
@@ -132,7 +132,7 @@ static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask
             r.loc |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
             r.mask |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
         }
-        ocro::RowOps<A, K> ops(L, dist);
+        ocro::RowOps<A, K> ops(L, blob);
         for (int i = 0; i < nsub; ++i) {
             const oc_subtask& o = subs[i];
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},

@@ -38,19 +38,16 @@ template <int A, int K>
 static void run(const oc_level_desc* lv, int max_T, const uint8_t* sin, uint8_t* sout, const uint8_t* act,
                 uint8_t* exo, uint8_t* coll, int64_t B, int64_t P) {
     const int W = lv->width, H = lv->height;
-    uint64_t fm = 0, dm = 0, cmk = 0;
     int done_cell = -1;
+    uint8_t tbl[256] = {0};
     for (int c = 0; c < W * H; ++c) {
-        if (lv->tiles[c] == OC_TILE_FLOOR) fm |= 1ull << c;
-        if (lv->tiles[c] == OC_TILE_CUTBOARD) cmk |= 1ull << c;
-        if (lv->tiles[c] == OC_TILE_DELIVERY) { dm |= 1ull << c; if (done_cell < 0) done_cell = c; }
+        tbl[c] = ocsw::tile_class(lv->tiles[c]);
+        if (lv->tiles[c] == OC_TILE_DELIVERY && done_cell < 0) done_cell = c;
     }
     uint8_t cell[8], mask[8];
     for (int j = 0; j < 8; ++j) { cell[j] = j < lv->num_items ? lv->item_cell[j] : 0xFF; mask[j] = j < lv->num_items ? lv->item_mask[j] : 0; }
     ocsw::SwarLevel S;
     ocsw::build_swar_level(S, W, H, done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y, A, cell, mask);
-    uint8_t tbl[256];
-    for (int c = 0; c < 256; ++c) tbl[c] = ocsw::tile_class(fm, dm, cmk, (uint32_t)c);
     auto cls_of = [&](uint32_t cells) -> uint32_t {
         return (uint32_t)tbl[cells & 0xFF] | ((uint32_t)tbl[(cells >> 8) & 0xFF] << 8) |
                ((uint32_t)tbl[(cells >> 16) & 0xFF] << 16) | ((uint32_t)tbl[cells >> 24] << 24);

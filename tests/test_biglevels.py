@@ -1,0 +1,160 @@
+"""User levels outside the nine shipped 7x7 kitchens (CPU): grids of 120, 169 and 255 cells,
+ragged maps and a repeated food type.  Pinned to what the reference itself does with the same
+level files (tests/golden/gen_biglevels.py: load_level/reset tables, 54 recorded episodes,
+3,865 subtask-bound rows, the exceptions ragged maps raise):
+  * levels.parse_level_text builds the reference's tables (overcooked_environment.py:144-198);
+  * the CPU oracle and the host build of the device SWAR step replay every recorded episode
+    bit for bit (cell ids >= 128 take the SWAR step's full-byte compare path);
+  * the host build of the planner-table row (oc_rollout.h) reproduces the reference's lower
+    bounds and allocation feasibility on the 120- and 169-cell kitchens;
+  * ragged maps raise what the reference raises (KeyError at reset, IndexError at step);
+  * a second Tomato / Lettuce / Onion is refused by the level check and by oc_create."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oc_testlib as tl
+import test_bounds_host as tb
+import test_swar_host as ts
+from gym_cooking_amd import capi, levels
+
+from oracle import oracle
+
+BIG = ["big-10x12_salad", "big-13x13_tl", "big-15x17_salad"]
+
+
+def _info():
+    with open(os.path.join(tl.GOLDEN, "biglevels.json")) as f:
+        return json.load(f)
+
+
+def _path(name):
+    return os.path.join(tl.GOLDEN, "levels", name + ".txt")
+
+
+@pytest.mark.parametrize("name", BIG + ["ragged-long_salad"])
+def test_level_files_match_reference_loader(name):
+    ref = _info()[name]
+    lv = levels.load_level(_path(name))
+    assert (lv.width, lv.height) == (ref["width"], ref["height"])
+    assert lv.tiles == ref["tiles"]
+    assert sorted(lv.items) == sorted(tuple(x) for x in ref["items"])
+    assert [list(s) for s in lv.spawns] == ref["spawns"]
+    assert sorted(lv.goals) == ref["goals"]
+    assert 2 * (lv.width + lv.height) == ref["perimeter"]
+
+
+def test_big_levels_reach_cell_ids_past_127():
+    lv = levels.load_level(_path("big-15x17_salad"))
+    assert lv.ncells == 255 == levels.MAX_CELLS
+    lv.validate(4)
+    assert max(c for c, _ in lv.items) > 127
+
+
+@pytest.mark.parametrize("impl", ["oracle", "swar_host"])
+def test_big_level_episodes_match_reference(impl):
+    fx = tl.load_fixture("biglevels.npz")
+    groups = tl.episode_groups(fx)
+    assert len(groups) == 9 and sum(g.B for g in groups) == 54
+    for g in groups:
+        if impl == "oracle":
+            ob = oracle.OracleBatch(g.level, g.A, g.max_T, g.B)
+            from test_oracle_golden import _oracle_step_fn as mk
+        else:
+            ts._load()
+            ob = ts.SwarHostBatch(g.level, g.A, g.max_T, g.B)
+            mk = ts._step_fn
+        s = ob.new_state()
+        ob.reset(s)
+        g.relocate(s, ob.pitch)
+        errs = tl.compare_group(g, mk(ob), s, ob.pitch, g.level.width)
+        assert not errs, "%s A=%d: %s" % (g.level.name, g.A, "\n".join(errs[:10]))
+
+
+@pytest.mark.parametrize("name", BIG)
+@pytest.mark.parametrize("A", [2, 4])
+def test_big_level_swar_matches_oracle_random(name, A):
+    """Uniform random streams over many envs (collisions, pick-ups, resets at max_T)."""
+    ts._load()
+    B, steps, max_T = 1001, 90, 40
+    lv = levels.load_level(_path(name))
+    ob = oracle.OracleBatch(lv, A, max_T, B)
+    sb = ts.SwarHostBatch(lv, A, max_T, B)
+    s, s2 = ob.new_state(), ob.new_state()
+    ob.reset(s)
+    h = s.copy()
+    h2 = h.copy()
+    act = ob.new_actions()
+    for t in range(steps):
+        ob.gen_actions(act, 0, t, 77)
+        ob.step(s, s2, act)
+        sb.step(h, h2, act)
+        s, s2, h, h2 = s2, s, h2, h
+        assert np.array_equal(tl.env_view(s, A, ob.K, ob.pitch, B), tl.env_view(h, A, ob.K, ob.pitch, B)), t
+
+
+@pytest.mark.parametrize("cfg", range(3))
+def test_big_level_bounds_match_reference_rows(cfg):
+    rows = tl.BoundRows(tl.load_fixture("bounds_big.npz"), cfg)
+    assert rows.level.ncells > 64
+    ob = oracle.OracleBatch(rows.level, rows.A, 100, rows.B)
+    st = rows.state(ob.pitch)
+    lb, doable = tb.host_bounds(ob, st, rows.subtasks)
+    errs = rows.compare(lb, doable)
+    assert not errs, "\n".join(errs[:20])
+    o_lb, o_ok = ob.subtask_bounds(st, rows.subtasks)
+    errs = rows.compare(o_lb, o_ok)
+    assert not errs, "oracle: " + "\n".join(errs[:20])
+
+
+def test_ragged_short_map_raises_keyerror_like_reset():
+    ref = _info()["ragged-short_salad"]
+    assert ref["raises"] == "KeyError"
+    lv = levels.load_level(_path("ragged-short_salad"))
+    assert lv.missing and lv.width == 7
+    with pytest.raises(KeyError) as ei:
+        lv.validate(2)
+    assert list(ei.value.args[0]) == ref["arg"]
+
+
+def test_ragged_long_map_loads_and_step_raises_indexerror():
+    ref = _info()["ragged-long_salad"]
+    assert ref["step_raises"] == "IndexError"
+    lv = levels.load_level(_path("ragged-long_salad"))
+    assert lv.overflow and lv.width == 7 and not lv.missing
+    with pytest.raises(IndexError):  # the batched engine refuses a level the reference cannot step
+        lv.validate(2)
+    lv.within_width().validate(2)
+
+
+def test_repeated_food_type_is_refused():
+    text = "\n".join(["-----t-", "/     l", "/     t", "*     -", "-     -", "-     p", "-----p-"]) + \
+        "\n\nSalad\n\n2 1\n4 1\n"
+    lv = levels.parse_level_text(text, "two-tomatoes")
+    with pytest.raises(ValueError, match="food type twice"):
+        lv.validate(2)
+    # the C-ABI refuses it too (oc_create's own check; no device needed)
+    lib = capi.load_library()
+    d = capi.OcLevelDesc()
+    d.width, d.height, d.num_items, d.num_spawns, d.num_goals = lv.width, lv.height, len(lv.items), 2, 1
+    for c, t in enumerate(lv.tiles):
+        d.tiles[c] = t
+    for j, (c, m) in enumerate(lv.items):
+        d.item_cell[j], d.item_mask[j] = c, m
+    for a, (x, y) in enumerate(lv.spawns[:2]):
+        d.spawn_x[a], d.spawn_y[a] = x, y
+    d.goal_mask[0] = lv.goals[0]
+    h = ctypes.c_void_p()
+    assert lib.oc_create(ctypes.byref(d), 2, 100, 0, ctypes.byref(h)) == capi.OC_ELEVEL
+    assert b"twice" in lib.oc_last_error()
+
+
+def test_grid_past_255_cells_is_refused():
+    rows = ["-" * 16] + ["/" + " " * 14 + "-"] * 14 + ["--*-----tl---pp-"]
+    lv = levels.parse_level_text("\n".join(rows) + "\n\nSalad\n\n2 1\n4 1\n", "too-big")
+    assert lv.ncells == 256
+    with pytest.raises(ValueError, match="cells"):
+        lv.validate(2)
