@@ -510,32 +510,34 @@ struct RowOps {
         if (!q_value(r, s, t0, t1, old_q)) return 4;
         if (!action_legal(r, s, t0, t1)) return 4;  // assert action in valid_nav_actions
         const int other = s.n == 2 ? (s.agent[0] == self_agent ? 1 : (s.agent[1] == self_agent ? 0 : -1)) : -1;
-        // pass 1: max of beta * (old_q - Q) over the valid actions; pass 2: softmax sum
-        double m = -1.0e300, S = 0.0, xt = 0.0;
+        // one rollout per valid candidate: x = beta * (old_q - Q) kept per candidate, then the
+        // max and the softmax sum over them in candidate order (the reference's two passes
+        // over the same values, bayesian_delegator.py:676-689)
+        double xs[25];
+        uint32_t valid = 0u;
+        double m = -1.0e300, xt = 0.0;
         bool found = false;
         // kept rolled: each candidate is a whole rollout (interact + goal + bound walk)
 #pragma unroll 1
-        for (int pass = 0; pass < 2; ++pass) {
+        for (int a0 = 0; a0 < 5; ++a0)
 #pragma unroll 1
-            for (int a0 = 0; a0 < 5; ++a0)
-#pragma unroll 1
-                for (int a1 = 0; a1 < (s.n == 2 ? 5 : 1); ++a1) {
-                    const int c1 = s.n == 2 ? a1 : kNoop;
-                    if (!action_legal(r, s, a0, c1)) continue;
-                    if (other == 0 && a0 != t0) continue;
-                    if (other == 1 && c1 != t1) continue;
-                    double q;
-                    if (!q_value(r, s, a0, c1, q)) return 4;
-                    const double x = beta * (old_q - q);
-                    if (pass == 0) {
-                        m = x > m ? x : m;
-                        if (a0 == t0 && c1 == t1) { found = true; xt = x; }
-                    } else {
-                        S += exp(x - m);
-                    }
-                }
-        }
+            for (int a1 = 0; a1 < (s.n == 2 ? 5 : 1); ++a1) {
+                const int c1 = s.n == 2 ? a1 : kNoop;
+                if (!action_legal(r, s, a0, c1)) continue;
+                if (other == 0 && a0 != t0) continue;
+                if (other == 1 && c1 != t1) continue;
+                double q;
+                if (!q_value(r, s, a0, c1, q)) return 4;
+                const double x = beta * (old_q - q);
+                const int k = a0 * 5 + a1;
+                xs[k] = x;
+                valid |= 1u << k;
+                m = x > m ? x : m;
+                if (a0 == t0 && c1 == t1) { found = true; xt = x; }
+            }
         if (!found) return 4;
+        double S = 0.0;
+        for (uint32_t v = valid; v; v &= v - 1u) S += exp(xs[__builtin_ctz(v)] - m);
         out = exp(xt - m) / S;
         return 1;
     }

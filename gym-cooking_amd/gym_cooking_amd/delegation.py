@@ -16,13 +16,21 @@ is restated so that an update gives the reference's posterior bit for bit
 
 Allocation enumeration and the spatial priors (``set_priors``) stay with the reference; a
 distribution is built here from its allocations (``SubtaskAllocDistribution``).
+
+``bayes_update_batch`` runs many delegators' updates at once (the agents of many envs): their
+doability queries go to the GPU as one oc_subtask_bounds launch per 64 configurations, and
+their inverse-planning requests -- each update's own sequence, as ``bayes_update`` issues it
+-- in lockstep through shared oc_rollout launches, so the launch count is about that of the
+longest single update.  Each update gives exactly its sequential result when its delegator
+and planner have their own generators (``rng=random.Random(seed)``,
+``E2E_BRTDP(..., rng=np.random.RandomState(seed))``).
 """
 from __future__ import annotations
 
 import copy
 import random
 from collections import namedtuple
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import scipy.special
@@ -55,11 +63,11 @@ class SubtaskAllocDistribution:
     def get(self, subtask_alloc) -> float:
         return self.probs[tuple(subtask_alloc)]
 
-    def get_max(self):
+    def get_max(self, rng=random):
         if len(self.probs) > 0:
             max_prob = max(self.probs.values())
             max_subtask_allocs = [subtask_alloc for subtask_alloc, p in self.probs.items() if p == max_prob]
-            return random.choice(max_subtask_allocs)
+            return rng.choice(max_subtask_allocs)
         return None
 
     def update(self, subtask_alloc, factor) -> None:
@@ -84,9 +92,11 @@ _CODE = {a: i for i, a in enumerate(_levels.ACTIONS)}
 class BayesianDelegator:
     """The belief update of the reference's ``BayesianDelegator`` (constructor and the methods
     ``bayes_update`` calls), over an engine-backed ``planner`` (gym_cooking_amd.planner.E2E_BRTDP).
-    ``probs`` is a :class:`SubtaskAllocDistribution` of tuples of :data:`SubtaskAllocation`."""
+    ``probs`` is a :class:`SubtaskAllocDistribution` of tuples of :data:`SubtaskAllocation`.
+    `rng`: the generator of ``get_max``'s tie-break (default Python's global one, as the
+    reference)."""
 
-    def __init__(self, agent_name, all_agent_names, model_type, planner, none_action_prob):
+    def __init__(self, agent_name, all_agent_names, model_type, planner, none_action_prob, rng=None):
         self.name = "Bayesian Delegator"
         self.agent_name = agent_name
         self.all_agent_names = all_agent_names
@@ -95,10 +105,11 @@ class BayesianDelegator:
         self.priors = "uniform" if model_type == "up" else "spatial"
         self.planner = planner
         self.none_action_prob = none_action_prob
+        self._rng = rng if rng is not None else random
 
     # ---- beliefs ------------------------------------------------------------------------
     def select_subtask(self, agent_name):  # :1009-1017
-        max_subtask_alloc = self.probs.get_max()
+        max_subtask_alloc = self.probs.get_max(self._rng)
         if max_subtask_alloc is not None:
             for t in max_subtask_alloc:
                 if agent_name in t.subtask_agent_names:
@@ -114,11 +125,25 @@ class BayesianDelegator:
     def subtask_alloc_is_doable(self, env, subtask, subtask_agent_names) -> bool:  # :98-156
         if subtask is None:
             return True
+        return self._doability(env, [(subtask, tuple(subtask_agent_names))])[(subtask, tuple(subtask_agent_names))]
+
+    @staticmethod
+    def _config(env, subtask, subtask_agent_names):
         names = env.get_agent_names()
-        agents = [names.index(n) for n in subtask_agent_names]
         kind, starts, goal = _recipes.subtask_masks(subtask)
-        _, ok = self._expander(env).bounds(env.state_bytes(), [capi.subtask(kind, agents, list(starts), goal, 0)])
-        return bool(ok[0])
+        return capi.subtask(kind, [names.index(n) for n in subtask_agent_names], list(starts), goal, 0)
+
+    def _doability(self, env, pairs) -> Dict[tuple, bool]:
+        """subtask_alloc_is_doable of every (subtask, agent names) pair on env's state: one
+        oc_subtask_bounds launch per 64 of them (the query is a pure function of the state)."""
+        pairs = [q for q in dict.fromkeys(pairs) if q[0] is not None]
+        out = {}
+        exp = self._expander(env)
+        for c0 in range(0, len(pairs), capi.MAX_SUBTASKS):
+            chunk = pairs[c0:c0 + capi.MAX_SUBTASKS]
+            _, ok = exp.bounds(env.state_bytes(), [self._config(env, st, an) for st, an in chunk])
+            out.update({q: bool(v) for q, v in zip(chunk, ok)})
+        return out
 
     def _expander(self, env):
         p = self.planner
@@ -129,7 +154,7 @@ class BayesianDelegator:
         return p._exp
 
     # ---- inverse planning ---------------------------------------------------------------
-    def get_other_agent_planners(self, obs, backup_subtask):  # :375-433
+    def _other_agent_planners_gen(self, obs, backup_subtask):  # get_other_agent_planners :375-433
         planners = {}
         for other_agent_name in self.all_agent_names:
             if other_agent_name != self.agent_name:
@@ -138,19 +163,31 @@ class BayesianDelegator:
                     subtask = backup_subtask
                     subtask_agent_names = tuple(sorted([other_agent_name, self.agent_name]))
                 planner = copy.copy(self.planner)
-                planner.set_settings(obs, subtask, subtask_agent_names)
+                yield from planner._set_settings_gen(obs, subtask, subtask_agent_names)
                 planners[other_agent_name] = planner
         return planners
 
-    def get_appropriate_state_and_other_agent_planners(self, obs_tm1, backup_subtask, no_level_1):  # :435-459
+    def get_other_agent_planners(self, obs, backup_subtask):  # :375-433
+        return self.planner._drive(self._other_agent_planners_gen(obs, backup_subtask))
+
+    def _state_and_other_planners_gen(self, obs_tm1, backup_subtask, no_level_1):  # :435-459
         if no_level_1:
             return obs_tm1, {}
-        self.planner.modified_state(obs_tm1)
-        return obs_tm1, self.get_other_agent_planners(obs=obs_tm1, backup_subtask=backup_subtask)
+        yield from self.planner._modified_state_env(obs_tm1)
+        planners = yield from self._other_agent_planners_gen(obs=obs_tm1, backup_subtask=backup_subtask)
+        return obs_tm1, planners
+
+    def get_appropriate_state_and_other_agent_planners(self, obs_tm1, backup_subtask, no_level_1):  # :435-459
+        return self.planner._drive(self._state_and_other_planners_gen(obs_tm1, backup_subtask, no_level_1))
 
     def prob_nav_actions(self, obs_tm1, actions_tm1, subtask, subtask_agent_names, beta, no_level_1) -> float:
         """:461-689.  Q values, legal actions and the None branch's action count come from
         engine rollout rows; the softmax is scipy's, as the reference's."""
+        self._expander(obs_tm1)
+        return self.planner._drive(self._prob_nav_actions_gen(obs_tm1, actions_tm1, subtask, subtask_agent_names,
+                                                              beta, no_level_1))
+
+    def _prob_nav_actions_gen(self, obs_tm1, actions_tm1, subtask, subtask_agent_names, beta, no_level_1):
         assert len(subtask_agent_names) == 1 or len(subtask_agent_names) == 2
         names = obs_tm1.get_agent_names()
         if subtask is None:
@@ -158,7 +195,7 @@ class BayesianDelegator:
             me = names.index(self.agent_name)
             # get_single_actions(obs_tm1, self agent) - 1: its legal moves with every agent in place
             probe = capi.subtask(1, [me], [0, 0], 0, 0, 1)
-            _, fl, _ = self._expander(obs_tm1).rows(obs_tm1.state_bytes(), [(c,) for c in range(4)], probe)
+            _, fl, _ = yield (obs_tm1.state_bytes(), [(c,) for c in range(4)], probe)
             num_actions = int(sum(1 for f in fl if f & capi.ROLL_LEGAL))
             action_prob = (1.0 - self.none_action_prob) / (num_actions)
             diffs = [self.none_action_prob] + [action_prob] * num_actions
@@ -167,30 +204,38 @@ class BayesianDelegator:
                 return softmax_diffs[0]
             return softmax_diffs[1]
         action = tuple(_CODE[tuple(actions_tm1[a_name])] for a_name in subtask_agent_names)
-        state, other_planners = self.get_appropriate_state_and_other_agent_planners(
+        state, other_planners = yield from self._state_and_other_planners_gen(
             obs_tm1=obs_tm1, backup_subtask=subtask, no_level_1=no_level_1)
         if not other_planners:
             raise NotImplementedError("prob_nav_actions without other agents (a 1-agent env or no_level_1)")
         p = self.planner
-        p.set_settings(obs_tm1, subtask, subtask_agent_names, other_planners)
-        err = p.taken_action_error(p.start, action)  # Q(state, taken) and the assert below raise
+        yield from p._set_settings_gen(obs_tm1, subtask, subtask_agent_names, other_planners)
+        err = yield from p._taken_action_error_gen(p.start, action)  # Q(state, taken) and the assert below raise
         if err is not None:
             raise err("valid_nav_actions do not hold the taken action {}".format(action))
-        old_q = p.Q(p.start, action, p.v_l)
-        valid_nav_actions = p.get_actions(p.start)
+        old_q = yield from p._Q_gen(p.start, action, p.v_l)
+        yield from p._need(p.start)
+        valid_nav_actions = p._succ[(p.start, p._sub_key)][0]  # get_actions(state)
         assert action in valid_nav_actions, "valid_nav_actions: {}\naction: {}".format(valid_nav_actions, action)
         if len(subtask_agent_names) == 2 and self.agent_name in subtask_agent_names:
             other_index = 1 - subtask_agent_names.index(self.agent_name)
             valid_nav_actions = list(filter(lambda x: x[other_index] == action[other_index], valid_nav_actions))
-        qdiffs = [old_q - p.Q(p.start, nav_action, p.v_l) for nav_action in valid_nav_actions]
+        qdiffs = []
+        for nav_action in valid_nav_actions:
+            q = yield from p._Q_gen(p.start, nav_action, p.v_l)
+            qdiffs.append(old_q - q)
         softmax_diffs = scipy.special.softmax(beta * np.asarray(qdiffs))
         return softmax_diffs[valid_nav_actions.index(action)]
 
-    def bayes_update(self, obs_tm1, actions_tm1, beta) -> None:  # :1026-1072
+    def _doability_pairs(self) -> list:
+        return [(t.subtask, tuple(t.subtask_agent_names)) for a in self.probs.enumerate_subtask_allocs() for t in a]
+
+    def _bayes_update_gen(self, obs_tm1, actions_tm1, beta, doable):
+        """bayes_update with the doability answers given (`doable`: (subtask, agent names) ->
+        bool, from :meth:`_doability`) and every rollout request yielded."""
         for subtask_alloc in self.probs.enumerate_subtask_allocs():
             for t in subtask_alloc:
-                if not self.subtask_alloc_is_doable(env=obs_tm1, subtask=t.subtask,
-                                                    subtask_agent_names=t.subtask_agent_names):
+                if t.subtask is not None and not doable[(t.subtask, tuple(t.subtask_agent_names))]:
                     self.probs.delete(subtask_alloc)
                     break
         self.ensure_at_least_one_subtask()
@@ -201,12 +246,82 @@ class BayesianDelegator:
             for t in subtask_alloc:
                 if self.model_type == "greedy":
                     if self.agent_name in t.subtask_agent_names:
-                        update += self.prob_nav_actions(obs_tm1=obs_tm1, actions_tm1=actions_tm1, subtask=t.subtask,
-                                                        subtask_agent_names=t.subtask_agent_names, beta=beta,
-                                                        no_level_1=False)
+                        update += yield from self._prob_nav_actions_gen(
+                            obs_tm1=obs_tm1, actions_tm1=actions_tm1, subtask=t.subtask,
+                            subtask_agent_names=t.subtask_agent_names, beta=beta, no_level_1=False)
                 else:
-                    p = self.prob_nav_actions(obs_tm1=obs_tm1, actions_tm1=actions_tm1, subtask=t.subtask,
-                                              subtask_agent_names=t.subtask_agent_names, beta=beta, no_level_1=False)
+                    p = yield from self._prob_nav_actions_gen(
+                        obs_tm1=obs_tm1, actions_tm1=actions_tm1, subtask=t.subtask,
+                        subtask_agent_names=t.subtask_agent_names, beta=beta, no_level_1=False)
                     update += len(t.subtask_agent_names) * p
             self.probs.update(subtask_alloc=subtask_alloc, factor=update)
         self.probs.normalize()
+
+    def bayes_update(self, obs_tm1, actions_tm1, beta) -> None:  # :1026-1072
+        doable = self._doability(obs_tm1, self._doability_pairs())
+        self.planner._drive(self._bayes_update_gen(obs_tm1, actions_tm1, beta, doable))
+
+
+def bayes_update_batch(delegators: Sequence[BayesianDelegator], obs_list, actions_list, beta) -> list:
+    """``bayes_update`` of many delegators at once (e.g. every Bayesian-delegation agent of
+    many envs): delegator i updates on (obs_list[i], actions_list[i]).  Updates on one level
+    and agent count share one expander (the first such planner's).  Doability queries: one
+    oc_subtask_bounds launch per 64 distinct configurations over all the states of a level;
+    inverse planning: the updates run in lockstep, each round's rollout requests of a level in
+    shared oc_rollout launches.  Returns, per delegator, None or the exception its update
+    raised (the reference's bayes_update raises AssertionError / AttributeError on some
+    states; the others still complete)."""
+    n = len(delegators)
+    assert len(obs_list) == len(actions_list) == n
+    groups: Dict[tuple, List[int]] = {}
+    for i, (d, o) in enumerate(zip(delegators, obs_list)):
+        groups.setdefault(_planner.expander_key(o, d.planner.device), []).append(i)
+    exp_of = [None] * n
+    doable: List[dict] = [{} for _ in range(n)]
+    for idx in groups.values():
+        d0 = delegators[idx[0]]
+        exp = d0._expander(obs_list[idx[0]])
+        for i in idx:
+            delegators[i].planner._exp, delegators[i].planner._exp_key = exp, d0.planner._exp_key
+            exp_of[i] = exp
+        # doability of every (state, configuration) pair: configurations x states per launch
+        pairs = {i: [q for q in dict.fromkeys(delegators[i]._doability_pairs()) if q[0] is not None] for i in idx}
+        cols: Dict[bytes, object] = {}
+        for i in idx:
+            for st, an in pairs[i]:
+                cfg = delegators[i]._config(obs_list[i], st, an)
+                cols.setdefault(bytes(cfg), cfg)
+        col_of = {k: c for c, k in enumerate(cols)}
+        table = list(cols.values())
+        states = np.stack([obs_list[i].state_bytes() for i in idx])
+        ok_all = np.zeros((len(table), len(idx)), bool)
+        for c0 in range(0, len(table), capi.MAX_SUBTASKS):
+            for r0 in range(0, len(idx), exp.ROWS):
+                _, ok = exp.bounds_many(states[r0:r0 + exp.ROWS], table[c0:c0 + capi.MAX_SUBTASKS])
+                ok_all[c0:c0 + ok.shape[0], r0:r0 + ok.shape[1]] = ok
+        for r, i in enumerate(idx):
+            doable[i] = {q: bool(ok_all[col_of[bytes(delegators[i]._config(obs_list[i], *q))], r]) for q in pairs[i]}
+    gens = [d._bayes_update_gen(o, a, beta, dq) for d, o, a, dq in zip(delegators, obs_list, actions_list, doable)]
+    out = [None] * n
+    pending = {}
+
+    def advance(i, value=None, first=False):
+        try:
+            pending[i] = next(gens[i]) if first else gens[i].send(value)
+        except StopIteration:
+            pending.pop(i, None)
+        except (AssertionError, AttributeError) as ex:
+            pending.pop(i, None)
+            out[i] = ex
+
+    for i in range(n):
+        advance(i, first=True)
+    while pending:
+        for idx in groups.values():
+            live = [i for i in idx if i in pending]
+            if not live:
+                continue
+            results = exp_of[live[0]].run([pending[i] for i in live])
+            for i, res in zip(live, results):
+                advance(i, res)
+    return out

@@ -158,6 +158,20 @@ class _Expander:
                                                  _ptr(okt), 1, self.eb._stream()))
         return lbt[:, 0].cpu().numpy(), okt[:, 0].cpu().numpy()
 
+    def bounds_many(self, states: np.ndarray, subs):
+        """oc_subtask_bounds of up to ROWS states (env_view bytes, [B, NP]) under each of up to
+        64 configurations in one launch: (lower bounds [S][B], doable [S][B])."""
+        B, S = len(states), len(subs)
+        hi = self._hi
+        hi[:, :B] = np.asarray(states).T
+        hi[self.t_plane:, :B] = 0
+        self._d_in.copy_(self._h_in_all, non_blocking=True)
+        lbt = torch.empty((S, self.P), dtype=torch.float32, device=self.eb.device)
+        okt = torch.empty((S, self.P), dtype=torch.uint8, device=self.eb.device)
+        capi.check(self.eb.lib.oc_subtask_bounds(self.eb._h, _ptr(self.s_in), capi.subtask_array(subs), S, _ptr(lbt),
+                                                 _ptr(okt), B, self.eb._stream()))
+        return lbt[:, :B].cpu().numpy(), okt[:, :B].cpu().numpy()
+
     def run(self, requests):
         out, chunk, nrows, subs = [], [], 0, {}
         for req in requests:
@@ -311,7 +325,10 @@ class E2E_BRTDP:
         self._value_init(self.start, self._start_goal, float(lb[0]))
 
     def set_settings(self, env, subtask, subtask_agent_names, other_agent_planners=None):
-        self._configured(self._exp_run(self._configure(env, subtask, subtask_agent_names, other_agent_planners)))
+        self._drive(self._set_settings_gen(env, subtask, subtask_agent_names, other_agent_planners))
+
+    def _set_settings_gen(self, env, subtask, subtask_agent_names, other_agent_planners=None):
+        self._configured((yield self._configure(env, subtask, subtask_agent_names, other_agent_planners)))
 
     def _exp_run(self, req):
         return self._exp.run([req])[0]
@@ -469,6 +486,10 @@ class E2E_BRTDP:
         its first configuration computed.  This T keeps that memo (per object, as the
         reference's); such a successor is value-initialised under the current configuration
         (Q's value_init, e2e_brtdp.py:768-770) from one no-op row of it."""
+        return self._drive(self._T_gen(key, action))
+
+    def _T_gen(self, key, action):
+        """T as a generator (yields the rollout request it may need)."""
         memo = (self._repr(key), action)
         hit = self._tmemo.get(memo)
         if hit is not None:
@@ -477,10 +498,11 @@ class E2E_BRTDP:
             nk = (hit[0], hit[1], tuple(self._agents), self._level)
             vk = (self._repr(nk), self._sub_key)
             if vk not in self.v_l or vk not in self.v_u:
-                _, fl, lb = self._exp_run((np.frombuffer(hit[0], np.uint8), [(_NOOP,) * len(self._agents)], self._sub))
+                _, fl, lb = yield (np.frombuffer(hit[0], np.uint8), [(_NOOP,) * len(self._agents)], self._sub)
                 self._value_init(nk, bool(fl[0] & capi.ROLL_GOAL), float(lb[0]))
             return nk
-        got = self._expand(key)
+        yield from self._need(key)
+        got = self._succ[(key, self._sub_key)]
         i = got[0].index(action)
         if got[7] and i in got[7]:
             _raise_copy_crash(action)
@@ -499,8 +521,11 @@ class E2E_BRTDP:
         return cost
 
     def Q(self, key, action, value_f) -> float:  # e2e_brtdp.py:736-760
+        return self._drive(self._Q_gen(key, action, value_f))
+
+    def _Q_gen(self, key, action, value_f):
         cost = self.cost(action)
-        nk = self.T(key, action)
+        nk = yield from self._T_gen(key, action)
         expected_value = 1.0 * value_f[(self._repr(nk), self._sub_key)]
         return float(cost + expected_value)
 
@@ -604,7 +629,10 @@ class E2E_BRTDP:
         (bayesian_delegator.py:657-673) -- AttributeError when T's copy of the next state
         meets two co-located agents that both hold (world.py:417), else AssertionError (T's
         joint co-location assert, or the membership assert).  None for a legal action."""
-        self._expand(key)
+        return self._drive(self._taken_action_error_gen(key, action))
+
+    def _taken_action_error_gen(self, key, action):
+        yield from self._need(key)
         got = self._illegal.get((key, self._sub_key), {})
         if action not in got:
             return None
@@ -621,6 +649,9 @@ class E2E_BRTDP:
         """_get_modified_state_with_other_agent_actions(state=env) under the planner's current
         configuration (what BayesianDelegator.prob_nav_actions calls first, :435-459): at Level
         1 the other agents' planners are set up on env's state and pick their actions."""
+        self._drive(self._modified_state_env(env))
+
+    def _modified_state_env(self, env):
         if not getattr(self, "_level", 0):
             return
         exp = self._exp
@@ -628,7 +659,7 @@ class E2E_BRTDP:
         full[exp.t_plane:] = 0
         groups = frozenset(env._group_names) | frozenset(it.name for it in env.world.items)
         key = (_canon(full.tobytes(), exp.A, exp.K), groups, tuple(self._agents), self._level)
-        self._drive(self._modified_state(key))
+        yield from self._modified_state(key)
 
     def _modified_state(self, key):
         """_get_modified_state_with_other_agent_actions (e2e_brtdp.py:842-878) as a generator.

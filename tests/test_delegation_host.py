@@ -50,6 +50,47 @@ def run_update(fx, c, make_env, **planner_kw):
     return got, c["after"] if c["raised"] is None else c["raised"]
 
 
+def run_batch(fx, calls, make_env, **planner_kw):
+    """The recorded updates `calls` in ONE bayes_update_batch call, each delegator and planner
+    with its own generators seeded as the recording was; returns [(got, want)] per call."""
+    from gym_cooking_amd.delegation import BayesianDelegator, SubtaskAllocDistribution, bayes_update_batch
+    from gym_cooking_amd.planner import E2E_BRTDP
+    ds, obs, acts = [], [], []
+    for c in calls:
+        cfg = fx["configs"][c["cfg"]]
+        o = make_env(cfg["level"], cfg["A"], c)
+        planner = E2E_BRTDP(**fx["params"], rng=np.random.RandomState(c["np_seed"]), **planner_kw)
+        d = BayesianDelegator(c["self"], o.get_agent_names(), "bd", planner, fx["none_action_prob"],
+                              rng=random.Random(c["random_seed"]))
+        allocs = [_alloc(a) for a, _ in c["before"]]
+        d.probs = SubtaskAllocDistribution(allocs)
+        for k, (_, p) in zip(allocs, c["before"]):
+            d.probs.probs[k] = p
+        ds.append(d)
+        obs.append(o)
+        acts.append({n: tuple(a) for n, a in c["actions"].items()})
+    errs = bayes_update_batch(ds, obs, acts, fx["beta"])
+    out = []
+    for d, e, c in zip(ds, errs, calls):
+        if e is not None:
+            out.append((type(e).__name__, c["raised"]))
+            continue
+        got = [[[[None if t.subtask is None else str(t.subtask), list(t.subtask_agent_names)] for t in k], p]
+               for k, p in d.probs.get_list()]
+        out.append((got, c["after"] if c["raised"] is None else c["raised"]))
+    return out
+
+
+def test_host_bayes_update_batch_matches_reference():
+    """Every recorded update (all configurations) in one bayes_update_batch call."""
+    import test_planner_host as th
+    fx = load()
+    calls = fx["calls"]
+    res = run_batch(fx, calls, th._env, expander=th.OracleExpander)
+    bad = [i for i, (g, w) in enumerate(res) if g != w]
+    assert not bad, "%d of %d batched updates differ: %s" % (len(bad), len(res), bad[:10])
+
+
 def test_host_bayes_update_matches_reference():
     import test_planner_host as th
     fx = load()

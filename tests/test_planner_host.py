@@ -38,6 +38,14 @@ class OracleExpander:
         lb, ok = self.ob.subtask_bounds(sin.reshape(-1), subs, nthreads=1)
         return lb[:, 0], ok[:, 0]
 
+    def bounds_many(self, states, subs):
+        out_lb, out_ok = [], []
+        for st in states:
+            lb, ok = self.bounds(st, subs)
+            out_lb.append(lb)
+            out_ok.append(ok)
+        return np.stack(out_lb, 1), np.stack(out_ok, 1)
+
     def rows(self, state, codes, sub):
         n = len(codes)
         sin = np.zeros((self.NP, self.P), np.uint8)
