@@ -3,7 +3,8 @@
 group per pass; tools/pmc_c5_report.py reads them).
 
 Dispatches, on bench.py's C5 rows (full-divider_salad, 4 agents, 2^18 mid-episode states,
-64 Salad (subtask, agents) configurations, random allocation and joint action per row):
+64 Salad (subtask, agents) configurations, random allocation and joint action per row; rows in
+random order, or configuration-major with OC_C5_ORDER=grouped as bench.py times them):
   oc_rollout_kernel     x4
   oc_bounds_kernel      x4
   oc_likelihood_kernel  x3
@@ -39,6 +40,9 @@ table = [capi.subtask(k, ags, st, g, 0) for (k, st, g) in SALAD_SUBTASKS for ags
 gen = torch.Generator(device=dev)
 gen.manual_seed(5)
 alloc = torch.randint(0, len(table), (eb.pitch,), dtype=torch.uint8, device=dev, generator=gen)
+ORDER = os.environ.get("OC_C5_ORDER", "random")  # "grouped": configuration-major rows, as bench.py
+if ORDER == "grouped":
+    alloc = torch.sort(alloc)[0].contiguous()
 eb.gen_actions(a, 99, 12)
 out = eb.new_state()
 flags = torch.empty(eb.pitch, dtype=torch.uint8, device=dev)
@@ -70,5 +74,5 @@ stats, totals = e2.new_stats(), torch.zeros(5, dtype=torch.int64, device=dev)
 for _ in range(3):
     e2.step_n(x, y, acts.reshape(-1), n, traj, exn, colln, stats, totals)
 torch.cuda.synchronize()
-print("pmc c5 probe done: rollout rows %d, configurations %d, state planes %d"
-      % (rows, len(table), eb.layout.num_planes))
+print("pmc c5 probe done (%s rows): rollout rows %d, configurations %d, state planes %d"
+      % (ORDER, rows, len(table), eb.layout.num_planes))

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Counter passes for the C5 kernels (oc_rollout / oc_bounds / oc_likelihood) and the headline
 # step kernel, run on the GPU box from the repo root:
-#   tools/profile_c5.sh OUT_TAG
+#   [OC_C5_ORDER=grouped] tools/profile_c5.sh OUT_TAG
 # One rocprofv3 --pmc pass per counter group (SQ <= 8, TCC FETCH_SIZE or WRITE_SIZE alone,
 # GRBM <= 2), no trace domains, each under its own time limit; then tools/pmc_c5_report.py.
 set -euo pipefail
