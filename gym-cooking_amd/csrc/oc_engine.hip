@@ -471,9 +471,24 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
     }
 }
 
-// Bayesian-delegation likelihood (oc_nav_likelihood): one row per lane; every candidate action
-// of the row is a rollout (interact + goal + lower bound) evaluated in registers.
-template <int A, int K>
+// Bayesian-delegation likelihood (oc_nav_likelihood): a group of G lanes per row; candidate
+// action k (k = a0 for one subtask agent, a0*5 + a1 for two: the reference's loop order,
+// bayesian_delegator.py:676-689) belongs to lane k % G, slot k / G (32 / G slots per lane).  Every
+// lane of a group builds the row's Level-0 view, tests its candidates' legality and evaluates
+// Q(s, k) with one rollout (interact + goal + lower bound) for each legal candidate and for
+// the taken action.  The group then takes Q(s, taken) from the taken action's lane, the max of
+// x = beta * (Q(s, taken) - Q(s, k)) over the legal candidates (a butterfly max: order-free),
+// exp(x - max) per candidate, and the softmax sum over k in ascending order (every lane adds
+// the group's terms in that order, so the sum is the sequential one bit for bit).  A lane
+// walking all candidates of its row kept 22 % of the lanes active per VALU instruction
+// (profiles/r02/c5_grouped); spreading them over the group leaves the candidates' own path
+// differences.  G = 32 (one candidate per lane) when the call's table has a two-agent
+// configuration; G = 8 when every configuration has one agent (5 candidates: a 32-lane group
+// would idle 27 lanes).  Measured on the C5 rows (profiles/r02/c5_order_probe.json): G = 32
+// 0.35 ms configuration-major, 0.55 ms random order, against 0.44 / 1.29 ms with G = 8; a
+// one-agent table 0.19 ms with G = 8, 0.41 with G = 32.  The None subtask's closed form runs
+// on the group's first lane.
+template <int A, int K, int G>
 __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                                const uint8_t* __restrict__ taken_p,
                                                                const uint8_t* __restrict__ alloc,
@@ -485,20 +500,110 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
     stage_roll_tables(R, blob_g, blob_w, subs);
     const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
-    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-        const int ai = alloc != nullptr ? alloc[e] : 0;
+    constexpr int kLikGroup = G, kLikSlots = 32 / G;  // G x slots >= 25 candidates
+    const int lane = (int)(threadIdx.x & (kLikGroup - 1));
+    const int64_t ngroups = (int64_t)gridDim.x * (kBlock / kLikGroup);
+    for (int64_t e = (int64_t)blockIdx.x * (kBlock / kLikGroup) + threadIdx.x / kLikGroup; e < R.B; e += ngroups) {
+        const int ai = alloc != nullptr ? alloc[e] : 0;  // group-uniform from here on
         double v = 0.0;
         int f = OC_LIK_BADALLOC;
         if (ai < R.nsub) {
-            const ocro::Row r = load_row<A, K>(sin, P, e);
+            const ocro::Sub& s = subs[ai];
+            ocro::Row r = load_row<A, K>(sin, P, e);
             uint32_t taken = 0;
 #pragma unroll
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
             ocro::RowOps<A, K> ops(R.L, blob);
-            f = ops.likelihood(r, subs[ai], taken, self_agent, beta, nap, v);
+            if (s.kind == 0) {
+                f = 0;
+                if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
+            } else if (ops.level0(r, s)) {
+                f = OC_LIK_RAISES;  // two removed agents on one square
+            } else {
+                const bool joint = s.n == 2;
+                int t0 = (int)((taken >> (8 * s.agent[0])) & 0xFFu), t1 = ocro::kNoop;
+                if (joint) t1 = (int)((taken >> (8 * s.agent[1])) & 0xFFu);
+                t0 = t0 > ocro::kNoop ? ocro::kNoop : t0;
+                t1 = t1 > ocro::kNoop ? ocro::kNoop : t1;
+                const int ncand = joint ? 25 : 5, kt = joint ? t0 * 5 + t1 : t0;
+                const int other = joint ? (s.agent[0] == self_agent ? 1 : (s.agent[1] == self_agent ? 0 : -1)) : -1;
+                double q[kLikSlots], ex[kLikSlots];
+                bool legal[kLikSlots];
+                int bad = 0, taken_ok = 0;
+                double qt = 0.0;
+                // candidate k's legality and Q (one rollout when legal or taken)
+                auto eval = [&](int k, double& qj, bool& lg) OC_RL {
+                    const int a0 = joint ? k / 5 : k, c1 = joint ? k % 5 : ocro::kNoop;
+                    lg = k < ncand && ops.action_legal(r, s, a0, c1);
+                    if (other == 0 && a0 != t0) lg = false;
+                    if (other == 1 && c1 != t1) lg = false;
+                    qj = 0.0;
+                    bool ok = true;
+                    if (lg || k == kt) ok = ops.q_value(r, s, a0, c1, qj);
+                    bad |= (int)(lg && !ok);
+                    if (k == kt) {
+                        qt = qj;
+                        taken_ok = (int)(ok && lg);
+                    }
+                };
+                if constexpr (kLikSlots == 1) {
+                    eval(lane, q[0], legal[0]);
+                } else {
+                    // one rolled loop, one rollout call site (the row code is large); its results
+                    // go to the slot registers by static selects (no scratch)
+#pragma unroll 1
+                    for (int j = 0; j < kLikSlots; ++j) {
+                        double qj;
+                        bool lg;
+                        eval(lane + kLikGroup * j, qj, lg);
+#pragma unroll
+                        for (int i = 0; i < kLikSlots; ++i)
+                            if (i == j) {
+                                q[i] = qj;
+                                legal[i] = lg;
+                            }
+                    }
+                }
+                // Q(s, taken) and its legality from the taken action's lane; the row raises when
+                // that rollout or any legal candidate's rollout hits the co-location assert, or
+                // when the taken action is not among get_actions
+                const double old_q = __shfl(qt, kt % kLikGroup, kLikGroup);
+                taken_ok = __shfl(taken_ok, kt % kLikGroup, kLikGroup);
+#pragma unroll
+                for (int off = 1; off < kLikGroup; off <<= 1) bad |= __shfl_xor(bad, off, kLikGroup);
+                if (!taken_ok || bad) {
+                    f = OC_LIK_RAISES;
+                } else {
+                    double m = -1.0e300;
+#pragma unroll
+                    for (int j = 0; j < kLikSlots; ++j) {
+                        q[j] = legal[j] ? beta * (old_q - q[j]) : -1.0e300;  // q now holds x
+                        m = q[j] > m ? q[j] : m;
+                    }
+#pragma unroll
+                    for (int off = 1; off < kLikGroup; off <<= 1) {
+                        const double o = __shfl_xor(m, off, kLikGroup);
+                        m = o > m ? o : m;
+                    }
+                    double et = 0.0;
+#pragma unroll
+                    for (int j = 0; j < kLikSlots; ++j) {
+                        ex[j] = legal[j] ? exp(q[j] - m) : 0.0;
+                        if (lane + kLikGroup * j == kt) et = ex[j];
+                    }
+                    double S = 0.0;  // ascending k = 8 j + c: the reference's summation order
+#pragma unroll
+                    for (int j = 0; j < kLikSlots; ++j)
+                        for (int c = 0; c < kLikGroup && kLikGroup * j + c < ncand; ++c) S += __shfl(ex[j], c, kLikGroup);
+                    v = __shfl(et, kt % kLikGroup, kLikGroup) / S;
+                    f = OC_LIK_OK;
+                }
+            }
         }
-        out[e] = f == OC_LIK_OK ? v : 0.0;
-        out_flags[e] = (uint8_t)f;
+        if (lane == 0) {
+            out[e] = f == OC_LIK_OK ? v : 0.0;
+            out_flags[e] = (uint8_t)f;
+        }
     }
 }
 
@@ -1133,13 +1238,23 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     RollArgs R;
     if (const int rc = roll_args(h, subtasks, num_subtasks, B, R)) return rc;
     if (B == 0) return OC_OK;
-    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
+    bool any_joint = false;  // lanes per row: one per candidate with a two-agent configuration
+    for (int i = 0; i < num_subtasks; ++i) any_joint |= subtasks[i].num_agents == 2;
+    const int64_t G = any_joint ? 32 : 8;
+    // grid: up to 16 blocks per CU with 32-lane groups (5 resident per CU: measured 0.35 vs
+    // 0.39 ms per 2^18 C5 rows against 8 per CU), 8 per CU with 8-lane groups (3-4 resident)
+    const int64_t need = (B * G + kBlock - 1) / kBlock, cap = (int64_t)h->cus * (any_joint ? 16 : 8);
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
-#define OC_LAUNCH_LIK(A, K)                                                                                     \
-    hipLaunchKernelGGL((oc_likelihood_kernel<A, K>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,              \
-                       (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,       \
-                       likelihood, out_flags)
+#define OC_LAUNCH_LIK(A, K)                                                                                          \
+    if (any_joint)                                                                                                   \
+        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 32>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,          \
+                           (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,   \
+                           likelihood, out_flags);                                                                   \
+    else                                                                                                             \
+        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 8>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,           \
+                           (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,   \
+                           likelihood, out_flags)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_LIK)
     return hip_check("oc_nav_likelihood launch");
 }

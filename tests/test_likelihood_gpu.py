@@ -47,3 +47,19 @@ def test_likelihood_matches_oracle_random(level, A, B):
         assert ok.sum() > 100
         np.testing.assert_allclose(g_v[ok], o_v[ok], rtol=1e-12)
         assert np.all(g_v[~ok] == 0)
+
+
+@pytest.mark.parametrize("level,A,B", [("partial-divider_salad", 2, 4000), ("full-divider_salad", 4, 20000)])
+def test_likelihood_one_agent_tables_match_oracle(level, A, B):
+    """Tables of one-agent configurations only take the kernel's 8-lane groups (two-agent
+    tables its 32-lane groups, the tests above)."""
+    import test_rollout_host as th
+    ob, s, acts, subs, alloc = th.random_rollout_case(level, A, B, seed=B % 89 + 3)
+    subs = [capi.subtask(x.kind, [x.agent[0]], list(x.start_mask), x.goal_mask, x.goal_count) for x in subs]
+    for self_agent in range(2):
+        o_v, o_f = ob.nav_likelihood(s, acts, subs, alloc, self_agent, 1.3, 0.5, nthreads=16)
+        g_v, g_f = _gpu_lik(level, A, B, s, acts, subs, alloc, self_agent, 1.3, 0.5)
+        assert np.array_equal(o_f, g_f), np.argwhere(o_f != g_f)[:5]
+        ok = o_f == capi.LIK_OK
+        assert ok.sum() > 100
+        np.testing.assert_allclose(g_v[ok], o_v[ok], rtol=1e-12)

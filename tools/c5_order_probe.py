@@ -7,6 +7,8 @@ allocation ids in three orders:
   grouped   the same ids sorted, so the rows of one configuration are contiguous (how the
             reference's delegator iterates: for each allocation, for each agent)
   single    every row configuration 0
+and a table of the one-agent configurations only, configuration-major (the likelihood
+kernel's 8-lane groups; tables with a two-agent configuration take 32-lane groups).
 Usage: python tools/c5_order_probe.py
 """
 import itertools
@@ -66,6 +68,11 @@ def main():
         r_ms = timed(lambda: eb.rollout(s, out, a, table, al, flags, lb), 20)
         l_ms = timed(lambda: eb.nav_likelihood(s, a, table, 0, 1.3, 0.5, al), 5)
         res[name] = {"rollout_ms": r_ms, "likelihood_ms": l_ms}
+    # a table of one-agent configurations only (the likelihood kernel's 8-lane groups)
+    singles = [i for i, t in enumerate(table) if t.num_agents == 1]
+    t1 = [table[i] for i in singles]
+    al1 = torch.sort(torch.randint(0, len(t1), (eb.pitch,), dtype=torch.uint8, device=dev, generator=gen))[0]
+    res["one_agent_table_grouped"] = {"likelihood_ms": timed(lambda: eb.nav_likelihood(s, a, t1, 0, 1.3, 0.5, al1), 5)}
     bl = torch.empty((len(table), eb.pitch), dtype=torch.float32, device=dev)
     bo = torch.empty((len(table), eb.pitch), dtype=torch.uint8, device=dev)
     res["bounds_ms"] = timed(lambda: eb.subtask_bounds(s, table, bl, bo), 10)
