@@ -159,8 +159,8 @@ def measure_likelihood(eb, states, taken, table, alloc, dev, world, reps: int = 
     ms = ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
     ok = int((f[:eb.B] == capi.LIK_OK).sum())
     return {"value": world * eb.B / (ms * 1e-3), "unit": "likelihood rows/s", "ms_per_launch": ms,
-            "kernel": "oc_likelihood_kernel<4,4>", "rows_computed": ok, "bound": "issue (divergent row code: "
-            "up to 25 candidate rollouts per row, profiles/r02/pmc_c5.json)"}
+            "kernel": "oc_likelihood_kernel<4,4>", "rows_computed": ok, "bound": "divergence + latency (a lane "
+            "per candidate rollout, up to 25 per row; profiles/r02/c5_grouped/pmc_c5.json)"}
 
 
 def measure_bounds(eb, states, table, dev, world, reps: int = 10) -> dict:
@@ -245,6 +245,89 @@ def load_traffic(path: str, kernel: str = "oc_step_n_kernel", steps_per_launch=N
     n0 = min(shapes, key=lambda n: abs(n - steps_per_launch))
     return (shapes[n0]["ratio"] * algorithmic,
             "%s [%s, ratio of the %d-step record x this launch's algorithmic bytes]" % (src, kernel, n0))
+
+
+def measure_bayes(dev, world, n_updates: int = 256, n_seq: int = 8) -> dict:
+    """Secondary line, C5's consumer: Bayesian-delegation belief updates (delegation.bayes_update,
+    Level-1 inverse planning over oc_rollout, doability over oc_subtask_bounds) on the C5 layout
+    (full-divider_salad, 4 agents).  The workload is the reference's own: the 4-agent updates
+    recorded from it (tests/golden/bayes.json: states, executed actions, the 18 allocations of
+    set_priors and their probabilities), replicated to `n_updates` delegators with their own
+    planners, all updated in ONE bayes_update_batch call; `n_seq` of them are also updated one
+    at a time (bayes_update) for comparison."""
+    import random as _random
+    import re
+    import numpy as np
+    from gym_cooking_amd import capi, levels as _lv, recipes
+    from gym_cooking_amd.delegation import (BayesianDelegator, SubtaskAllocation, SubtaskAllocDistribution,
+                                            bayes_update_batch)
+    from gym_cooking_amd.planner import E2E_BRTDP, PlanEnv
+    with open(os.path.join(ROOT, "tests", "golden", "bayes.json")) as f:
+        fx = json.load(f)
+    cfg4 = [i for i, c in enumerate(fx["configs"]) if c["A"] == 4]
+    calls = [c for c in fx["calls"] if c["cfg"] in cfg4 and c["raised"] is None]
+    static = {"Counter", "Floor", "Delivery", "Cutboard"}
+
+    def subtask(text):
+        m = re.fullmatch(r"(\w+)\((.*)\)", text)
+        cls = {"Chop": recipes.Chop, "Merge": recipes.Merge, "Deliver": recipes.Deliver}[m.group(1)]
+        return cls(*[a.strip() for a in m.group(2).split(",")])
+
+    def make(c):
+        cfg = fx["configs"][c["cfg"]]
+        lv = _lv.load_level(cfg["level"])
+        A, K, P = cfg["A"], capi.item_slots(lv), capi.pitch_for(1)
+        s = np.zeros(capi.layout_planes(A, K)["num_planes"], np.uint8)
+        L = capi.layout_planes(A, K)
+        ag, it = np.array(c["agents"], np.uint8), np.array(c["items"], np.uint8)
+        s[:] = 0
+        s[L["agent_x"]:L["agent_x"] + A], s[L["agent_y"]:L["agent_y"] + A] = ag[:A, 0], ag[:A, 1]
+        s[L["agent_hold"]:L["agent_hold"] + A] = 0xFF
+        s[L["item_loc"]:L["item_loc"] + K] = 0xFF
+        held = []  # canonical rows -> slots; each holder takes the held item at its cell with its mask
+        for j in range(len(it)):
+            m, x, y, h = (int(v) for v in it[j])
+            if m == 255:
+                continue
+            s[L["item_loc"] + j], s[L["item_mask"] + j] = y * lv.width + x, m
+            if h:
+                held.append((j, x, y, m))
+        for q in range(A):
+            x, y, hm = (int(v) for v in ag[q])
+            if hm not in (0, 255):
+                i = next(i for i, (_, ix, iy, m) in enumerate(held) if (ix, iy, m) == (x, y, hm))
+                s[L["agent_hold"] + q] = held.pop(i)[0]
+        env = PlanEnv(lv, A, s, [g for g in c["groups"] if g not in static], device=dev)
+        planner = E2E_BRTDP(**fx["params"], rng=np.random.RandomState(c["np_seed"]))
+        d = BayesianDelegator(c["self"], env.get_agent_names(), "bd", planner, fx["none_action_prob"],
+                              rng=_random.Random(c["random_seed"]))
+        allocs = [tuple(SubtaskAllocation(None if st is None else subtask(st), tuple(a)) for st, a in rec)
+                  for rec, _ in c["before"]]
+        d.probs = SubtaskAllocDistribution(allocs)
+        for k, (_, p) in zip(allocs, c["before"]):
+            d.probs.probs[k] = p
+        return d, env, {n: tuple(a) for n, a in c["actions"].items()}
+
+    warm = [make(c) for c in calls]  # first use of the level: expander, library, caches
+    bayes_update_batch([w[0] for w in warm], [w[1] for w in warm], [w[2] for w in warm], fx["beta"])
+    jobs = [make(calls[i % len(calls)]) for i in range(n_updates)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    errs = bayes_update_batch([j[0] for j in jobs], [j[1] for j in jobs], [j[2] for j in jobs], fx["beta"])
+    torch.cuda.synchronize()
+    dt = ocdist.max_over_ranks(time.perf_counter() - t0, dev)
+    seq = [make(calls[i % len(calls)]) for i in range(n_seq)]
+    t1 = time.perf_counter()
+    for d, env, acts in seq:
+        d.bayes_update(obs_tm1=env, actions_tm1=acts, beta=fx["beta"])
+    dts = time.perf_counter() - t1
+    exp = jobs[0][0].planner._exp
+    return {"value": world * n_updates / dt, "unit": "belief updates/s", "updates_per_gpu": n_updates,
+            "seconds": dt, "raised": sum(e is not None for e in errs),
+            "sequential": {"updates": n_seq, "value": n_seq / dts, "unit": "belief updates/s"},
+            "rollout_launches_per_batch": None if exp is None else exp.launches,
+            "workload": "C5 layout: full-divider_salad 4 agents, the reference's recorded 4-agent bayes_update "
+                        "calls (18 allocations each, Level-1 inverse planning) replicated, one batched call"}
 
 
 def measure_planner(dev, world) -> dict:
@@ -643,6 +726,7 @@ def main() -> int:
         line["c3"] = measure_c3(dev, world)
     if not args.no_planner:
         line["planner"] = measure_planner(dev, world)
+        line["bayes"] = measure_bayes(dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         hc = host_cores()
         line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget,
