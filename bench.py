@@ -728,10 +728,16 @@ def main() -> int:
         line["planner"] = measure_planner(dev, world)
         line["bayes"] = measure_bayes(dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the C restatement over all host cores (nproc).  The GPU pool gives each
+        # GPU's job a CPU share (cgroup quota, OMP_NUM_THREADS); the same sample threaded to that
+        # share is reported beside it ("job_share").
         hc = host_cores()
-        line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget,
-                                            hc["threads"])
+        nproc = hc["limits"]["nproc"]
+        line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget, nproc)
         line["cpu_baseline"]["host_cpu_limits"] = hc["limits"]
+        if hc["threads"] != nproc:
+            share = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget / 2, hc["threads"])
+            line["cpu_baseline"]["job_share"] = {k: share[k] for k in ("value", "cores", "sample")}
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:
