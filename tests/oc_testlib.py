@@ -75,7 +75,8 @@ def canonical(state: np.ndarray, A: int, K: int, pitch: int, width: int, B: int)
     items = np.where((key == 0xFFFFFFFF)[..., None], PAD, items).astype(np.uint8)
     if K < 4:
         items = np.concatenate([items, np.full((B, 4 - K, 4), PAD, np.uint8)], 1)
-    return dict(t=v["t"][:B].copy(), flags=v["fl"][:B].copy(), agents=agents, items=items[:, :4])
+    # 4 item rows (the 7x7 fixtures' width), 8 for levels with 8 item slots
+    return dict(t=v["t"][:B].copy(), flags=v["fl"][:B].copy(), agents=agents, items=items[:, :max(4, K)])
 
 
 def load_level(name: str) -> levels.Level:
@@ -211,7 +212,7 @@ def state_from_canonical(level, A: int, K: int, pitch: int, agents: np.ndarray, 
     W = level.width
     for b in range(B):
         held_slots = []
-        for j in range(4):
+        for j in range(items.shape[1]):
             m, x, y, h = (int(c) for c in items[b, j])
             if m == PAD:
                 continue

@@ -1,7 +1,8 @@
-"""User levels outside the nine shipped 7x7 kitchens (CPU): grids of 120, 169 and 255 cells,
+"""User levels outside the nine shipped 7x7 kitchens (CPU): grids of 120, 169 and 255 cells, a
+9x9 OnionSalad kitchen of 6 items (the engine's 8-slot layout, which no shipped level uses),
 ragged maps and a repeated food type.  Pinned to what the reference itself does with the same
-level files (tests/golden/gen_biglevels.py: load_level/reset tables, 54 recorded episodes,
-3,865 subtask-bound rows, the exceptions ragged maps raise):
+level files (tests/golden/gen_biglevels.py: load_level/reset tables, 54 + 21 recorded episodes,
+3,865 + 5,400 subtask-bound rows, the exceptions ragged maps raise):
   * levels.parse_level_text builds the reference's tables (overcooked_environment.py:144-198);
   * the CPU oracle and the host build of the device SWAR step replay every recorded episode
     bit for bit (cell ids >= 128 take the SWAR step's full-byte compare path);
@@ -24,6 +25,7 @@ from gym_cooking_amd import capi, levels
 from oracle import oracle
 
 BIG = ["big-10x12_salad", "big-13x13_tl", "big-15x17_salad"]
+K8 = "onion-9x9_onionsalad"  # Tomato, Lettuce, Onion and 3 Plates: the engine's 8 item slots
 
 
 def _info():
@@ -35,7 +37,7 @@ def _path(name):
     return os.path.join(tl.GOLDEN, "levels", name + ".txt")
 
 
-@pytest.mark.parametrize("name", BIG + ["ragged-long_salad"])
+@pytest.mark.parametrize("name", BIG + ["ragged-long_salad", K8])
 def test_level_files_match_reference_loader(name):
     ref = _info()[name]
     lv = levels.load_level(_path(name))
@@ -54,11 +56,14 @@ def test_big_levels_reach_cell_ids_past_127():
     assert max(c for c, _ in lv.items) > 127
 
 
+@pytest.mark.parametrize("fixture,n_eps", [("biglevels.npz", 54), ("biglevels_k8.npz", 21)])
 @pytest.mark.parametrize("impl", ["oracle", "swar_host"])
-def test_big_level_episodes_match_reference(impl):
-    fx = tl.load_fixture("biglevels.npz")
+def test_big_level_episodes_match_reference(impl, fixture, n_eps):
+    fx = tl.load_fixture(fixture)
     groups = tl.episode_groups(fx)
-    assert len(groups) == 9 and sum(g.B for g in groups) == 54
+    assert sum(g.B for g in groups) == n_eps
+    if fixture == "biglevels_k8.npz":
+        assert all(g.K == 8 for g in groups)
     for g in groups:
         if impl == "oracle":
             ob = oracle.OracleBatch(g.level, g.A, g.max_T, g.B)
@@ -74,7 +79,7 @@ def test_big_level_episodes_match_reference(impl):
         assert not errs, "%s A=%d: %s" % (g.level.name, g.A, "\n".join(errs[:10]))
 
 
-@pytest.mark.parametrize("name", BIG)
+@pytest.mark.parametrize("name", BIG + [K8])
 @pytest.mark.parametrize("A", [2, 4])
 def test_big_level_swar_matches_oracle_random(name, A):
     """Uniform random streams over many envs (collisions, pick-ups, resets at max_T)."""
@@ -96,10 +101,11 @@ def test_big_level_swar_matches_oracle_random(name, A):
         assert np.array_equal(tl.env_view(s, A, ob.K, ob.pitch, B), tl.env_view(h, A, ob.K, ob.pitch, B)), t
 
 
-@pytest.mark.parametrize("cfg", range(3))
-def test_big_level_bounds_match_reference_rows(cfg):
-    rows = tl.BoundRows(tl.load_fixture("bounds_big.npz"), cfg)
-    assert rows.level.ncells > 64
+@pytest.mark.parametrize("fixture,cfg", [("bounds_big.npz", 0), ("bounds_big.npz", 1), ("bounds_big.npz", 2),
+                                         ("bounds_k8.npz", 0)])
+def test_big_level_bounds_match_reference_rows(fixture, cfg):
+    rows = tl.BoundRows(tl.load_fixture(fixture), cfg)
+    assert rows.level.ncells > 64 or rows.K == 8
     ob = oracle.OracleBatch(rows.level, rows.A, 100, rows.B)
     st = rows.state(ob.pitch)
     lb, doable = tb.host_bounds(ob, st, rows.subtasks)

@@ -1,7 +1,8 @@
 """User levels outside the shipped 7x7 kitchens on the GPU, through the C-ABI (120-, 169- and
 255-cell grids from tests/golden/levels/, ragged maps):
-  * the engine replays the 54 episodes recorded from the reference on those levels bit for bit
-    (tests/golden/biglevels.npz), one oc_step launch per step;
+  * the engine replays the 54 episodes recorded from the reference on those levels, and the 21
+    on a 9x9 kitchen of 6 items (the 8-slot layout), bit for bit (tests/golden/biglevels*.npz),
+    one oc_step launch per step;
   * oc_step_n (multi-step launches) against the CPU oracle on every step's full state;
   * oc_subtask_bounds against the reference's bound rows (bounds_big.npz), oc_rollout and
     oc_nav_likelihood against the oracle on random rows;
@@ -25,6 +26,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 BIG = ["big-10x12_salad", "big-13x13_tl", "big-15x17_salad"]
+K8 = "onion-9x9_onionsalad"  # 6 items: the engine's 8 item slots
 
 
 def _path(name):
@@ -36,9 +38,10 @@ def _batch(level, A, B, max_T=100):
     return OvercookedBatch(level, A, B, max_T=max_T, device="cuda:0")
 
 
-def test_engine_replays_big_level_episodes():
+@pytest.mark.parametrize("fixture,n_eps", [("biglevels.npz", 54), ("biglevels_k8.npz", 21)])
+def test_engine_replays_big_level_episodes(fixture, n_eps):
     import test_gpu_parity as tg
-    fx = tl.load_fixture("biglevels.npz")
+    fx = tl.load_fixture(fixture)
     n = 0
     for g in tl.episode_groups(fx):
         eb = _batch(g.level, g.A, g.B, g.max_T)
@@ -49,10 +52,10 @@ def test_engine_replays_big_level_episodes():
         errs = tl.compare_group(g, tg._gpu_step_fn(eb), host, eb.pitch, g.level.width)
         assert not errs, "%s A=%d: %s" % (g.level.name, g.A, "\n".join(errs[:10]))
         n += g.B
-    assert n == 54
+    assert n == n_eps
 
 
-@pytest.mark.parametrize("name", BIG)
+@pytest.mark.parametrize("name", BIG + [K8])
 @pytest.mark.parametrize("A", [2, 4])
 def test_big_level_step_n_matches_oracle(name, A):
     """Two 30-step oc_step_n launches over 20,000 envs (max_T 25: auto-resets inside launches),
@@ -92,9 +95,10 @@ def test_big_level_step_n_matches_oracle(name, A):
         s_in, s_out = s_out, s_in
 
 
-@pytest.mark.parametrize("cfg", range(3))
-def test_big_level_bounds_match_reference_rows(cfg):
-    rows = tl.BoundRows(tl.load_fixture("bounds_big.npz"), cfg)
+@pytest.mark.parametrize("fixture,cfg", [("bounds_big.npz", 0), ("bounds_big.npz", 1), ("bounds_big.npz", 2),
+                                         ("bounds_k8.npz", 0)])
+def test_big_level_bounds_match_reference_rows(fixture, cfg):
+    rows = tl.BoundRows(tl.load_fixture(fixture), cfg)
     P = capi.pitch_for(rows.B)
     s = rows.state(P)
     eb = _batch(rows.level, rows.A, rows.B)
@@ -105,7 +109,7 @@ def test_big_level_bounds_match_reference_rows(cfg):
         assert not errs, "\n".join(errs[:20])
 
 
-@pytest.mark.parametrize("name", ["big-10x12_salad", "big-13x13_tl"])
+@pytest.mark.parametrize("name", ["big-10x12_salad", "big-13x13_tl", K8])
 @pytest.mark.parametrize("A", [2, 4])
 def test_big_level_rollout_and_likelihood_match_oracle(name, A):
     B = 6000
