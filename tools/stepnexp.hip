@@ -248,7 +248,29 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(ref_co.data(), co[0], ref_co.size(), hipMemcpyDeviceToHost));
     CK(hipMemcpy(ref_f.data(), fin[0], S, hipMemcpyDeviceToHost));
     const int cus = h->cus;
-    for (int bpc : {2, 3, 4, 5, 8}) {
+    // the product kernel under other store / action-load cache policies (CPol bits of the buffer
+    // intrinsics: 0 plain, 2 nt, 16 sc1, 1 sc0), same grid as oc_step_n
+    {
+        const int64_t need = P / kEnvsPerBlock, cap = (int64_t)cus * 5;
+        const dim3 grid((unsigned)(need < cap ? need : cap));
+#define PV(CP, LCP, NAME)                                                                                            \
+        {                                                                                                            \
+            auto f = [&](int v) {                                                                                    \
+                hipLaunchKernelGGL((oc_step_n_kernel<2, 4, CP, LCP>), grid, dim3(kBlock), 0, nullptr, L, s0, fin[v], \
+                                   acts, tr[v], ex[v], co[v], stats, (uint64_t*)nullptr, srows, n);                  \
+            };                                                                                                       \
+            time(NAME, f);                                                                                           \
+        }
+        PV(2, 0, "product kernel, stores nt, loads plain")
+        PV(2, 2, "product kernel, stores nt, action loads nt")
+        PV(0, 0, "product kernel, stores plain")
+        PV(16, 0, "product kernel, stores sc1")
+        PV(3, 0, "product kernel, stores nt sc0")
+        PV(18, 0, "product kernel, stores nt sc1")
+        PV(2, 16, "product kernel, stores nt, action loads sc1")
+#undef PV
+    }
+    for (int bpc : {2, 5}) {
         const uint32_t need = (uint32_t)(P / 8 / kBlock), cap = (uint32_t)(cus * bpc);
         const dim3 grid(need < cap ? need : cap);
         char name[64];
