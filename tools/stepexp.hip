@@ -39,7 +39,7 @@ __global__ __launch_bounds__(BS) void step_flat(LevelArgs L, const uint8_t* __re
 #pragma unroll
     for (int i = 0; i < CH; ++i) load_chunk<A, K>(c[i], b, P, g0 + i * span);
     __shared__ uint8_t tbl[256];
-    for (int i = threadIdx.x; i < 256; i += BS) tbl[i] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, i);
+    for (int i = threadIdx.x; i < 256; i += BS) tbl[i] = (uint8_t)(L.cls4[i >> 2] >> (8 * (i & 3)));
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     StepStats st;
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(BS) void step_timeline(LevelArgs L, const uint8_t* 
     Chunk<A, K> c;
     load_chunk<A, K>(c, b, P, g);
     __shared__ uint8_t tbl[256];
-    for (int i = threadIdx.x; i < 256; i += BS) tbl[i] = ocsw::tile_class(L.floor_mask, L.deliv_mask, L.cut_mask, i);
+    for (int i = threadIdx.x; i < 256; i += BS) tbl[i] = (uint8_t)(L.cls4[i >> 2] >> (8 * (i & 3)));
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every load landed
@@ -246,39 +246,6 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((step_flat<2, 4, CH, BS, __VA_ARGS__>), dim3(nl / CH / BS), dim3(BS), 0, s, L, i, o, a, ex, coll, stats); \
     })
     ref.clear();
-    // oc_step_n cache policies: 2 launches x 100 steps, trajectory written (the bench headline)
-    {
-        uint8_t* traj;
-        uint8_t *exn, *colln;
-        CK(hipMalloc(&traj, (int64_t)R * NP * P));
-        CK(hipMalloc(&exn, (int64_t)R * A * P));
-        CK(hipMalloc(&colln, (int64_t)R * P));
-        const int64_t need = P / kEnvsPerBlock, cap = (int64_t)kCUs * 5;
-        const dim3 grid((unsigned)(need < cap ? need : cap));
-        auto stepn = [&](auto kern, const char* name) {
-            float best = 1e30f;
-            for (int rep = 0; rep < 6; ++rep) {
-                oc_reset(h, sa, B, s);
-                CK(hipEventRecord(e0, s));
-                hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, sa, sb, act, traj, exn, colln, stats, R);
-                hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, L, sb, sa, act, traj, exn, colln, stats, R);
-                CK(hipEventRecord(e1, s));
-                CK(hipEventSynchronize(e1));
-                float ms;
-                CK(hipEventElapsedTime(&ms, e0, e1));
-                if (rep > 0 && ms < best) best = ms;
-            }
-            const double us = best * 1000.0 / (2 * R);
-            printf("%-40s %7.2f us/step  %6.2f TB/s alg (22.17 B/env-step)\n", name, us, 22.17 * B / us / 1e6);
-        };
-        stepn(oc_step_n_kernel<2, 4, 2, 0>, "step_n nt stores (product)");
-        stepn(oc_step_n_kernel<2, 4, 2, 2>, "step_n nt stores, nt action loads");
-        stepn(oc_step_n_kernel<2, 4, 2, 16>, "step_n nt stores, sc1 action loads");
-        stepn(oc_step_n_kernel<2, 4, 2, 17>, "step_n nt stores, sc0 sc1 action loads");
-        stepn(oc_step_n_kernel<2, 4, 2, 0>, "step_n nt stores (product)");
-        stepn(oc_step_n_kernel<2, 4, 2, 2>, "step_n nt stores, nt action loads");
-        stepn(oc_step_n_kernel<2, 4, 3, 0>, "step_n nt+sc0 stores");
-        stepn(oc_step_n_kernel<2, 4, 18, 0>, "step_n nt+sc1 stores");
-    }
+    // (oc_step_n launch-shape and cache-policy experiments: tools/stepnexp.hip)
     return 0;
 }

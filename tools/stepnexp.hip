@@ -1,15 +1,23 @@
-// tools/stepnexp.hip -- oc_step_n store-width experiment (includes the engine TU).
-// Build: hipcc -O3 -std=c++20 --offload-arch=gfx950 -o tools/stepnexp tools/stepnexp.hip
-// Workload: the bench's headline launch -- partial-divider_salad, 2 agents, B = 2^20, n = 20
-// steps per launch, every step's state / executed actions / collision mask written, stats on.
-// Variants:
+// tools/stepnexp.hip -- oc_step_n launch-shape experiment (includes the engine TU).
+// Build: hipcc -O3 -std=c++20 --offload-arch=gfx950 -o stepnexp tools/stepnexp.hip
+// Run:   stepnexp N_STEPS [A]   (A = 2 or 3; partial-divider_salad, B = 2^20, every step's state /
+//        executed actions / collision mask written, stats on)
+// Variants, timed interleaved (7 rounds x 20 launches each, min and median per variant):
 //   product  oc_step_n_kernel: 4 envs per lane, one dword per plane per instruction (256 B per
-//            wave store instruction)
+//            wave store instruction); alone, with its in-launch totals fold, or followed by an
+//            oc_stats_reduce launch
 //   x2       8 envs per lane as two SWAR words, b64 loads and stores (512 B per wave store
-//            instruction, half the store instructions), persistent grid capped at BPC blocks/CU
+//            instruction, half the store instructions), persistent grid of <= 5 blocks per CU
 // Every variant's trajectory, exec, coll and final state are compared with the product's.
+// Results (profiles/r02/stepnexp_*.log): on different boxes x2 ran 4-6 % faster than the
+// product at A = 2 without the statistics fold, ~4 % slower with it, slower at A = 3 (156 VGPRs,
+// 2 waves per SIMD), and at 100 steps per launch 6 % faster on one box and 8 % slower on
+// another; the product stayed.
 #include "../gym-cooking_amd/csrc/oc_engine.hip"
 
+#include <algorithm>
+#include <functional>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                                      \
@@ -170,7 +178,8 @@ __global__ __launch_bounds__(kBlock) void step_n_x2(LevelArgs L, const uint8_t* 
 
 int main(int argc, char** argv) {
     const int64_t B = 1 << 20;
-    const int n = argc > 1 ? atoi(argv[1]) : 20, reps = 60;
+    const int n = argc > 1 ? atoi(argv[1]) : 20;
+    const int A = argc > 2 ? atoi(argv[2]) : 2;  // 2 or 3 agents
     // partial-divider_salad (levels.py builtin): 7x7
     const char* rows[7] = {"-----t-", "/     l", "/  -  -", "*  -  -", "-  -  -", "-     p", "-----p-"};
     oc_level_desc lv{};
@@ -191,7 +200,7 @@ int main(int argc, char** argv) {
     for (int a = 0; a < 4; ++a) { lv.spawn_x[a] = sx[a]; lv.spawn_y[a] = sy[a]; }
     lv.goal_mask[0] = 0x3B;
     oc_handle* h;
-    if (oc_create(&lv, 2, 100, 0, &h) != 0) { printf("create: %s\n", oc_last_error()); return 1; }
+    if (oc_create(&lv, A, 100, 0, &h) != 0) { printf("create: %s\n", oc_last_error()); return 1; }
     oc_layout lay;
     oc_get_layout(h, B, &lay);
     const int64_t S = lay.state_bytes, P = lay.pitch;
@@ -199,19 +208,19 @@ int main(int argc, char** argv) {
     uint64_t *stats, *totals;
     int64_t sb = 0;
     oc_stats_size(h, B, &sb);
-    CK(hipMalloc(&s0, S)); CK(hipMalloc(&s1, S)); CK(hipMalloc(&acts, (int64_t)n * 2 * P));
+    CK(hipMalloc(&s0, S)); CK(hipMalloc(&s1, S)); CK(hipMalloc(&acts, (int64_t)n * A * P));
     CK(hipMalloc(&stats, sb + 64)); CK(hipMalloc(&totals, 64));
     for (int v = 0; v < 2; ++v) {
-        CK(hipMalloc(&tr[v], n * S)); CK(hipMalloc(&ex[v], (int64_t)n * 2 * P)); CK(hipMalloc(&co[v], (int64_t)n * P));
+        CK(hipMalloc(&tr[v], n * S)); CK(hipMalloc(&ex[v], (int64_t)n * A * P)); CK(hipMalloc(&co[v], (int64_t)n * P));
         CK(hipMalloc(&fin[v], S));
     }
     CK(hipMemset(stats, 0, sb + 64));
     oc_reset(h, s0, B, nullptr);
-    for (int r = 0; r < n; ++r) oc_gen_actions(h, acts + (int64_t)r * 2 * P, B, 0, r, 7, nullptr);
+    for (int r = 0; r < n; ++r) oc_gen_actions(h, acts + (int64_t)r * A * P, B, 0, r, 7, nullptr);
     // a mid-episode start state: 37 product steps
     {
         uint8_t* a1;
-        CK(hipMalloc(&a1, 2 * P));
+        CK(hipMalloc(&a1, A * P));
         for (int r = 0; r < 37; ++r) {
             oc_gen_actions(h, a1, B, 0, 1000 + r, 3, nullptr);
             oc_step(h, r & 1 ? s1 : s0, r & 1 ? s0 : s1, a1, nullptr, nullptr, nullptr, B, nullptr);
@@ -225,69 +234,77 @@ int main(int argc, char** argv) {
     const uint32_t srows = (uint32_t)stats_rows(h, B);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    auto product = [&](int v) {
+    // variants are timed interleaved: 7 rounds over all of them, 20 launches each, so that clock
+    // and box drift hit every variant alike; min and median per variant are printed
+    std::vector<std::pair<std::string, std::function<void(int)>>> vs;
+    uint64_t* tot;
+    CK(hipMalloc(&tot, 64));
+    vs.push_back({"product oc_step_n (4 envs/lane, dword)", [&](int v) {
         oc_step_n(h, s0, fin[v], acts, tr[v], ex[v], co[v], stats, nullptr, B, n, nullptr);
-    };
-    auto time = [&](const char* name, auto&& fn) {
-        for (int i = 0; i < 5; ++i) fn(i & 1);
-        CK(hipEventRecord(e0));
-        for (int i = 0; i < reps; ++i) fn(i & 1);
-        CK(hipEventRecord(e1));
-        CK(hipEventSynchronize(e1));
-        float ms;
-        CK(hipEventElapsedTime(&ms, e0, e1));
-        const double us = ms * 1e3 / reps, bytes = (double)(17 + n * 22) * B;
-        printf("%-34s %8.2f us/launch  %5.2f us/step  %5.2f TB/s\n", name, us, us / n, bytes / (us * 1e-6) / 1e12);
-    };
-    time("product oc_step_n (dword, nt)", product);
-    std::vector<uint8_t> ref_tr(n * S), ref_ex((size_t)n * 2 * P), ref_co((size_t)n * P), ref_f(S);
-    product(0);
+    }});
+    vs.push_back({"product, in-launch totals fold", [&](int v) {
+        oc_step_n(h, s0, fin[v], acts, tr[v], ex[v], co[v], stats, tot, B, n, nullptr);
+    }});
+    vs.push_back({"product + oc_stats_reduce launch", [&](int v) {
+        oc_step_n(h, s0, fin[v], acts, tr[v], ex[v], co[v], stats, nullptr, B, n, nullptr);
+        oc_stats_reduce(h, stats, B, tot, nullptr);
+    }});
+    const int cus = h->cus;
+    {
+        const uint32_t need = (uint32_t)(P / 8 / kBlock), cap = (uint32_t)(cus * 5);
+        const dim3 grid(need < cap ? need : cap);
+        for (int red = 0; red < 2; ++red)
+            vs.push_back({red ? "x2 (8 envs/lane, b64) + oc_stats_reduce launch" : "x2 (8 envs/lane, b64)",
+                          [&, grid, red](int v) {
+                              if (A == 2)
+                                  hipLaunchKernelGGL((step_n_x2<2, 4, kCPnt>), grid, dim3(kBlock), 0, nullptr, L, s0, fin[v],
+                                                     acts, tr[v], ex[v], co[v], stats, srows, n);
+                              else
+                                  hipLaunchKernelGGL((step_n_x2<3, 4, kCPnt>), grid, dim3(kBlock), 0, nullptr, L, s0, fin[v],
+                                                     acts, tr[v], ex[v], co[v], stats, srows, n);
+                              if (red) oc_stats_reduce(h, stats, B, tot, nullptr);
+                          }});
+    }
+    std::vector<std::vector<double>> us(vs.size());
+    for (auto& v : vs)
+        for (int i = 0; i < 5; ++i) v.second(i & 1);
+    for (int round = 0; round < 7; ++round)
+        for (size_t k = 0; k < vs.size(); ++k) {
+            CK(hipEventRecord(e0));
+            for (int i = 0; i < 20; ++i) vs[k].second(i & 1);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            us[k].push_back(ms * 1e3 / 20);
+        }
+    const double bytes = (double)((3 * A + 11) + n * (3 * A + 11 + 2 * A + 1)) * B;
+    for (size_t k = 0; k < vs.size(); ++k) {
+        std::sort(us[k].begin(), us[k].end());
+        printf("%-40s min %7.2f  median %7.2f us/launch  (%5.2f us/step, %4.2f TB/s at the median)\n", vs[k].first.c_str(),
+               us[k][0], us[k][3], us[k][3] / n, bytes / (us[k][3] * 1e-6) / 1e12);
+    }
+    // outputs of every variant against the product's
+    vs[0].second(0);  // the product: the reference outputs
     CK(hipDeviceSynchronize());
+    std::vector<uint8_t> ref_tr(n * S), ref_ex((size_t)n * A * P), ref_co((size_t)n * P), ref_f(S);
     CK(hipMemcpy(ref_tr.data(), tr[0], n * S, hipMemcpyDeviceToHost));
     CK(hipMemcpy(ref_ex.data(), ex[0], ref_ex.size(), hipMemcpyDeviceToHost));
     CK(hipMemcpy(ref_co.data(), co[0], ref_co.size(), hipMemcpyDeviceToHost));
     CK(hipMemcpy(ref_f.data(), fin[0], S, hipMemcpyDeviceToHost));
-    const int cus = h->cus;
-    // the product kernel under other store / action-load cache policies (CPol bits of the buffer
-    // intrinsics: 0 plain, 2 nt, 16 sc1, 1 sc0), same grid as oc_step_n
-    {
-        const int64_t need = P / kEnvsPerBlock, cap = (int64_t)cus * 5;
-        const dim3 grid((unsigned)(need < cap ? need : cap));
-#define PV(CP, LCP, NAME)                                                                                            \
-        {                                                                                                            \
-            auto f = [&](int v) {                                                                                    \
-                hipLaunchKernelGGL((oc_step_n_kernel<2, 4, CP, LCP>), grid, dim3(kBlock), 0, nullptr, L, s0, fin[v], \
-                                   acts, tr[v], ex[v], co[v], stats, (uint64_t*)nullptr, srows, n);                  \
-            };                                                                                                       \
-            time(NAME, f);                                                                                           \
-        }
-        PV(2, 0, "product kernel, stores nt, loads plain")
-        PV(2, 2, "product kernel, stores nt, action loads nt")
-        PV(0, 0, "product kernel, stores plain")
-        PV(16, 0, "product kernel, stores sc1")
-        PV(3, 0, "product kernel, stores nt sc0")
-        PV(18, 0, "product kernel, stores nt sc1")
-        PV(2, 16, "product kernel, stores nt, action loads sc1")
-#undef PV
-    }
-    for (int bpc : {2, 5}) {
-        const uint32_t need = (uint32_t)(P / 8 / kBlock), cap = (uint32_t)(cus * bpc);
-        const dim3 grid(need < cap ? need : cap);
-        char name[64];
-        snprintf(name, sizeof name, "x2 b64 nt, <= %d blocks/CU", bpc);
-        auto x2 = [&](int v) {
-            hipLaunchKernelGGL((step_n_x2<2, 4, kCPnt>), grid, dim3(kBlock), 0, nullptr, L, s0, fin[v], acts, tr[v], ex[v],
-                               co[v], stats, srows, n);
-        };
-        time(name, x2);
-        x2(1);
+    bool all_same = true;
+    for (size_t k = 1; k < vs.size(); ++k) {
+        vs[k].second(1);
         CK(hipDeviceSynchronize());
         std::vector<uint8_t> t2(n * S), e2(ref_ex.size()), c2(ref_co.size()), f2(S);
         CK(hipMemcpy(t2.data(), tr[1], n * S, hipMemcpyDeviceToHost));
         CK(hipMemcpy(e2.data(), ex[1], e2.size(), hipMemcpyDeviceToHost));
         CK(hipMemcpy(c2.data(), co[1], c2.size(), hipMemcpyDeviceToHost));
         CK(hipMemcpy(f2.data(), fin[1], S, hipMemcpyDeviceToHost));
-        printf("    outputs %s\n", (t2 == ref_tr && e2 == ref_ex && c2 == ref_co && f2 == ref_f) ? "identical" : "DIFFER");
+        const bool same = t2 == ref_tr && e2 == ref_ex && c2 == ref_co && f2 == ref_f;
+        all_same &= same;
+        if (!same) printf("    %s: outputs DIFFER\n", vs[k].first.c_str());
     }
+    printf("outputs %s\n", all_same ? "identical for every variant" : "differ");
     return 0;
 }
