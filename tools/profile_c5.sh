@@ -2,6 +2,7 @@
 # Counter passes for the C5 kernels (oc_rollout / oc_bounds / oc_likelihood) and the headline
 # step kernel, run on the GPU box from the repo root:
 #   [OC_C5_ORDER=grouped] tools/profile_c5.sh OUT_TAG
+#   PROBE="python3 tools/pmc_render_probe.py" tools/profile_c5.sh OUT_TAG   (the render kernel)
 # One rocprofv3 --pmc pass per counter group (SQ <= 8, TCC FETCH_SIZE or WRITE_SIZE alone,
 # GRBM <= 2), no trace domains, each under its own time limit; then tools/pmc_c5_report.py.
 set -euo pipefail
@@ -9,7 +10,7 @@ TAG=${1:?tag}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-PROBE="python3 tools/pmc_c5_probe.py"
+PROBE=${PROBE:-python3 tools/pmc_c5_probe.py}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o c5 -- $PROBE > "$OUT/trace.log" 2>&1
 pass() {
   local name=$1; shift
