@@ -634,10 +634,15 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
 // Image observation (oc_render, GameImage.get_image_obs: gym_cooking/misc/game/gameimage.py:31-51,
 // Game.on_render / draw_*: game.py:56-186).  One block per (env, cell row): the first W lanes
 // build each cell's ordered draw list in LDS (items not held in slot order, then every agent
-// in order followed by its held item), then the block writes the row's tile*W*tile*3 output
-// bytes, 16 pixels (48 bytes, three 16-byte non-temporal stores) per lane and iteration,
-// consecutive lanes on consecutive pixels.  A pixel starts from the static level image and blends every sprite of
-// its cell's list that covers it.  Everything is tile-local: every sprite lies inside its cell.
+// in order followed by its held item).  The block then writes the row's tile*W*tile*3 output
+// bytes in iterations of 16 pixels per lane (48 output bytes), consecutive lanes on consecutive
+// pixels, so a wave's 64 lanes cover 1,024 pixels that span every cell of one to three image
+// rows.  A pixel starts from the static level image and blends every sprite of its cell's list
+// that covers it; everything is tile-local (every sprite lies inside its cell).  Only the lanes
+// over a cell with sprites have blending to do, so the wave does it together: those lanes put
+// their 16 pixels in the wave's LDS slice and list themselves, and the wave then blends the
+// listed pixels one per lane (16 c / 64 passes for c listed lanes) instead of the listed lanes
+// looping over 16 pixels each while the others idle.
 struct RenderArgs {
     int32_t W, H, tile;
     int32_t size[OC_RENDER_SIZES], offset[OC_RENDER_SIZES], food_base[OC_RENDER_SIZES];
@@ -650,17 +655,24 @@ constexpr int kRenderMaxW = 32, kRenderMaxDraw = 2 * OC_MAX_ITEMS + 3 * OC_MAX_A
 constexpr int kRenderPx = 16;  // pixels per lane and iteration: 48 output bytes, three 16-byte stores
 
 // SDL 1.2 per-pixel alpha blit of an RGBA source pixel onto an RGB destination pixel
-// (BlitNtoNPixelAlpha / ALPHA_BLEND: d = (((s - d) * a + 255) >> 8) + d per channel, a = 0 skipped).
+// (BlitNtoNPixelAlpha / ALPHA_BLEND: d = (((s - d) * a + 255) >> 8) + d per channel, a = 0
+// skipped).  ((s - d) a + 255 >> 8) + d = (s a + d (256 - a) + 255) >> 8 exactly, and that
+// numerator is at most 65,535, so R and B share one 24-bit multiply-add pair in 16-bit fields
+// without carries; a = 0 gives (256 d + 255) >> 8 = d, the skipped blit, with no branch.
 __device__ __forceinline__ uint32_t sdl_blend(uint32_t d, uint32_t s) {
-    const int a = (int)(s >> 24);
-    if (a == 0) return d;
-    uint32_t out = 0u;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const int sc = (int)((s >> (8 * c)) & 0xFFu), dc = (int)((d >> (8 * c)) & 0xFFu);
-        out |= (uint32_t)((((sc - dc) * a + 255) >> 8) + dc) << (8 * c);
-    }
-    return out;
+    const uint32_t a = s >> 24, na = 256u - a;
+    const uint32_t rb = __umul24(d & 0xFF00FFu, na) + __umul24(s & 0xFF00FFu, a) + 0xFF00FFu;
+    const uint32_t g = __umul24((d >> 8) & 0xFFu, na) + __umul24((s >> 8) & 0xFFu, a) + 0xFFu;
+    return ((rb >> 8) & 0xFF00FFu) | (g & 0xFF00u);
+}
+
+// floor(n / d) for 0 <= n < 2^22 and 0 < d <= 2^11, from a float reciprocal and one correction
+__device__ __forceinline__ int div_small(int n, int d, float rcp) {
+    int q = (int)((float)n * rcp);
+    const int rem = n - q * d;
+    q += rem >= d ? 1 : 0;
+    q -= rem < 0 ? 1 : 0;
+    return q;
 }
 
 template <int A, int K>
@@ -668,9 +680,13 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
                                                            const uint32_t* __restrict__ atlas,
                                                            const uint32_t* __restrict__ bg,
                                                            uint8_t* __restrict__ out) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     __shared__ uint32_t dl_off[kRenderMaxW][kRenderMaxDraw];
     __shared__ uint32_t dl_geo[kRenderMaxW][kRenderMaxDraw];  // size | offset << 16
     __shared__ int32_t dl_n[kRenderMaxW];
+    // per wave: its 1,024 pixels while it blends, then its 3 KB of packed output
+    __shared__ u32x4 pix4[kBlock / 64][64 * kRenderPx / 4];
+    __shared__ uint32_t work[kBlock / 64][64];  // listed lane | row << 6 | cell column << 16 | x in cell << 21
     const int64_t e = blockIdx.x / (uint32_t)R.H;
     const int ty = (int)(blockIdx.x % (uint32_t)R.H);
     const int W = R.W, tile = R.tile;
@@ -716,6 +732,7 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
     __syncthreads();
     const int row_px = W * tile, G = row_px / kRenderPx;  // 16-pixel groups per image row
     const int items = tile * G;
+    const float rcpG = 1.0f / (float)G, rcpT = 1.0f / (float)tile;
     const int64_t img_bytes = (int64_t)R.H * tile * row_px * 3;
     uint8_t* img = out + e * img_bytes;
     // chan_map -> v_perm selector: output byte c <- pixel byte (chan_map >> 8c), 0x0C = zero
@@ -725,21 +742,21 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
         const uint32_t ch = (R.chan_map >> (8 * c)) & 0xFFu;
         psel |= (ch >= 3u ? 0x0Cu : ch) << (8 * c);
     }
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    // The block's output rows are contiguous and group i lands at byte 48 i, so a wave's 64
-    // groups are 3 KB contiguous.  Each lane packs its 48 bytes into the wave's LDS slice, and
-    // the wave then stores the slice as three fully contiguous 1 KB instructions (16 B per
-    // lane) instead of three 16 B-per-lane instructions at a 48 B stride.
-    __shared__ u32x4 stage[kBlock / 64][64 * 3];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* const pix = (uint32_t*)pix4[wave];
     uint8_t* const blk_out = img + (int64_t)ty * tile * row_px * 3;
     for (int base = 0; base < items; base += kBlock) {
-        const int i = base + threadIdx.x;
+        const int w0 = base + wave * 64;  // the wave's first group
+        const int i = w0 + lane;
+        uint32_t p[kRenderPx];
+        bool need = false;
+        int r = 0, tx = 0, lx0 = 0;
         if (i < items) {
-            const int r = i / G, g = i - r * G;
-            const int py = ty * tile + r, px0 = kRenderPx * g;
+            r = div_small(i, G, rcpG);
+            const int py = ty * tile + r, px0 = kRenderPx * (i - r * G);
+            tx = div_small(px0, tile, rcpT);  // a group never straddles two cells
+            lx0 = px0 - tx * tile;
             const u32x4* bsrc = (const u32x4*)(bg + (int64_t)py * row_px + px0);
-            uint32_t p[kRenderPx];
 #pragma unroll
             for (int q = 0; q < kRenderPx / 4; ++q) {
                 const u32x4 v = bsrc[q];
@@ -748,22 +765,59 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
                 p[4 * q + 2] = v.z;
                 p[4 * q + 3] = v.w;
             }
-            const int tx = px0 / tile, lx0 = px0 - tx * tile;  // a group never straddles two cells
             const int n = dl_n[tx];
             for (int d = 0; d < n; ++d) {
                 const uint32_t geo = dl_geo[tx][d];
                 const int sz = (int)(geo & 0xFFFFu), o = (int)(geo >> 16);
-                const int dy = r - o;
-                if ((unsigned)dy >= (unsigned)sz || lx0 + kRenderPx <= o || lx0 >= o + sz) continue;
-                const uint32_t* spr = atlas + dl_off[tx][d] + dy * sz;
+                need |= (unsigned)(r - o) < (unsigned)sz && lx0 + kRenderPx > o && lx0 < o + sz;
+            }
+        }
+        const uint64_t mask = __ballot(need);
+        if (mask != 0ull) {
+            if (need) {
 #pragma unroll
-                for (int k = 0; k < kRenderPx; ++k) {
-                    const int dx = lx0 + k - o;
-                    if ((unsigned)dx < (unsigned)sz) p[k] = sdl_blend(p[k], spr[dx]);
+                for (int q = 0; q < kRenderPx / 4; ++q)
+                    pix4[wave][4 * lane + q] = u32x4{p[4 * q], p[4 * q + 1], p[4 * q + 2], p[4 * q + 3]};
+                const uint32_t slot =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                work[wave][slot] = (uint32_t)lane | ((uint32_t)r << 6) | ((uint32_t)tx << 16) | ((uint32_t)lx0 << 21);
+            }
+            __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave; keep the compiler from moving reads up
+            const int npx = kRenderPx * __popcll(mask);
+            for (int t = lane; t < npx; t += 64) {
+                const uint32_t ent = work[wave][t >> 4];
+                const int k = t & (kRenderPx - 1), gl = (int)(ent & 63u);
+                const int rr = (int)((ent >> 6) & 0x3FFu), ctx = (int)((ent >> 16) & 31u), lx = (int)(ent >> 21) + k;
+                uint32_t dpx = pix[kRenderPx * gl + k];
+                const int n = dl_n[ctx];
+                for (int d = 0; d < n; ++d) {
+                    const uint32_t geo = dl_geo[ctx][d];
+                    const int sz = (int)(geo & 0xFFFFu), o = (int)(geo >> 16);
+                    const int dy = rr - o, dx = lx - o;
+                    if ((unsigned)dy < (unsigned)sz && (unsigned)dx < (unsigned)sz)
+                        dpx = sdl_blend(dpx, atlas[dl_off[ctx][d] + dy * sz + dx]);
+                }
+                pix[kRenderPx * gl + k] = dpx;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (need) {
+#pragma unroll
+                for (int q = 0; q < kRenderPx / 4; ++q) {
+                    const u32x4 v = pix4[wave][4 * lane + q];
+                    p[4 * q] = v.x;
+                    p[4 * q + 1] = v.y;
+                    p[4 * q + 2] = v.z;
+                    p[4 * q + 3] = v.w;
                 }
             }
-            // 16 pixels -> 48 bytes: per 4 pixels three dwords of packed 3-byte pixels
-            uint32_t w[12];
+            __builtin_amdgcn_wave_barrier();
+        }
+        // The block's output rows are contiguous and group i lands at byte 48 i, so a wave's 64
+        // groups are 3 KB contiguous.  Each lane packs its 48 bytes into the wave's LDS slice, and
+        // the wave then stores the slice as three fully contiguous 1 KB instructions (16 B per
+        // lane) instead of three 16 B-per-lane instructions at a 48 B stride.
+        if (i < items) {
+            uint32_t w[12];  // 16 pixels -> 48 bytes: per 4 pixels three dwords of packed 3-byte pixels
 #pragma unroll
             for (int q = 0; q < kRenderPx / 4; ++q) {
                 const uint32_t a0 = __builtin_amdgcn_perm(0u, p[4 * q], psel),
@@ -775,16 +829,15 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
                 w[3 * q + 2] = (a2 >> 16) | (a3 << 8);
             }
 #pragma unroll
-            for (int q = 0; q < 3; ++q) stage[wave][3 * lane + q] = u32x4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+            for (int q = 0; q < 3; ++q) pix4[wave][3 * lane + q] = u32x4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
         }
-        __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave; keep the compiler from moving reads up
-        const int w0 = base + wave * 64;  // the wave's first group
+        __builtin_amdgcn_wave_barrier();
         const int nbytes = 48 * (items - w0 < 64 ? (items - w0 > 0 ? items - w0 : 0) : 64);
         u32x4* dst = (u32x4*)(blk_out + (int64_t)w0 * 48);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
             const int off = q * 64 + lane;  // 16-byte units
-            if (off * 16 < nbytes) __builtin_nontemporal_store(stage[wave][off], dst + off);
+            if (off * 16 < nbytes) __builtin_nontemporal_store(pix4[wave][off], dst + off);
         }
         __builtin_amdgcn_wave_barrier();
     }
