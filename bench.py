@@ -600,29 +600,33 @@ def main() -> int:
     n_per = -(-K // n_launch)
     segs = [(i, min(n_per, K - i)) for i in range(0, K, n_per)]
     # outputs of one launch (every step's state, executed actions, collision mask), reused per launch
-    # two output sets, alternated between consecutive launches (OC_BENCH_OUT_SETS=1: one set reused)
-    n_sets = int(os.environ.get("OC_BENCH_OUT_SETS", "2"))
+    # two output sets, alternated between consecutive launches (a launch starts from the previous
+    # launch's last trajectory state, so the set it writes must be the other one)
+    n_sets = 2
     outs = [(torch.empty(n_per * S, dtype=torch.uint8, device=dev),
              torch.empty(n_per * A * P, dtype=torch.uint8, device=dev),
              torch.empty(n_per * P, dtype=torch.uint8, device=dev)) for _ in range(n_sets)]
-    s_a, s_b = eb.new_state(), eb.new_state()
+    s_a = eb.new_state()
     stats = eb.new_stats()
     totals = torch.zeros(5, dtype=torch.int64, device=dev)
 
     def plan(n_steps_total):
         """The launches of a window, bound once (engine.step_n_launcher: buffers validated
-        here, each launch is then one ctypes call).  The last launch also folds the episode
-        statistics into `totals` (in-launch, no separate reduce kernel)."""
-        out, src, dst, done, li = [], s_a, s_b, 0, 0
+        here, each launch is then one ctypes call).  A launch's state_out is its trajectory's
+        last state (oc_step_n then writes the final state once), and the next launch starts
+        from there.  The last launch also folds the episode statistics into `totals`
+        (in-launch, no separate reduce kernel)."""
+        out, src, done, li = [], s_a, 0, 0
         while done < n_steps_total:
             n = min(n_per, n_steps_total - done)
             i0 = done % K
             n = min(n, K - i0)
             traj, ex_all, coll_all = outs[li % n_sets]
+            dst = traj[(n - 1) * S:n * S]
             last = done + n >= n_steps_total
-            out.append(eb.step_n_launcher(src, dst, acts[i0:i0 + n].reshape(-1), n, traj, ex_all, coll_all, stats,
-                                          totals if last else None))
-            src, dst = dst, src
+            out.append(eb.step_n_launcher(src, dst, acts[i0:i0 + n].reshape(-1), n, traj[:n * S], ex_all, coll_all,
+                                          stats, totals if last else None))
+            src = dst
             done += n
             li += 1
         return out

@@ -243,8 +243,17 @@ __global__ __launch_bounds__(kStepBlock) void oc_step_kernel(LevelArgs L, const 
 // oc_step_n: n consecutive steps per launch.  Each lane loads its chunk's state once, then
 // for every step reads that step's actions (prefetched two steps ahead), steps in registers
 // and writes the step's outputs: the full state into traj[r] (when given), the executed
-// actions and the collision mask; the state after the last step goes to sout.  Outputs are
+// actions and the collision mask; the state after the last step goes to sout (null when sout
+// is the trajectory's last state: that store already wrote it).  Outputs are
 // byte-identical to n oc_step launches with ping-pong buffers.
+// oc_step_n's completion tickets, after the statistics rows (at a 128-byte boundary, one
+// 128-byte line each): [0] counts finished groups, [1 + g] the finished blocks of group g
+// (kTicketGroup consecutive blocks).  Every counter is back at zero when a launch ends.
+constexpr int kTicketGroup = 32, kTicketStride = 16;  // u64 units
+__host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
+    return (stat_rows * OC_NSTATS + kTicketStride - 1) / kTicketStride * kTicketStride;
+}
+
 template <int A, int K, int CP = 0, int LCP = 0>
 __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
                                                            uint8_t* __restrict__ sout,
@@ -254,7 +263,9 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
                                                            uint64_t* __restrict__ stats, uint64_t* __restrict__ totals,
                                                            uint32_t stat_rows, int n) {
     __shared__ uint32_t tbl4[64];
+    __shared__ uint32_t waves_done;
     if (threadIdx.x < 64u) tbl4[threadIdx.x] = L.cls4[threadIdx.x];
+    if (threadIdx.x == 0u) waves_done = 0u;
     __syncthreads();
     const uint8_t* tbl = (const uint8_t*)tbl4;
     const uint32_t P = (uint32_t)L.pitch, nlanes = P / kEPL, stride = gridDim.x * (uint32_t)kBlock;
@@ -267,12 +278,12 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
     };
     Bufs b;
     b.sin = make_rsrc(sin, (int64_t)NP * P);
-    b.sout = make_rsrc(sout, (int64_t)NP * P);
+    b.sout = make_rsrc(sout ? (const void*)sout : (const void*)sin, sout ? (int64_t)NP * P : 0);  // null: stores dropped
     b.act = make_rsrc(actions, (int64_t)n * A * P);
     const bool has_tr = traj != nullptr, has_ex = exec_out != nullptr, has_coll = coll_out != nullptr;
-    const __amdgpu_buffer_rsrc_t tr = make_rsrc(has_tr ? (const void*)traj : (const void*)sout, has_tr ? (int64_t)n * NP * P : 0);
-    b.ex = make_rsrc(has_ex ? (const void*)exec_out : (const void*)sout, has_ex ? (int64_t)n * A * P : 0);
-    b.coll = make_rsrc(has_coll ? (const void*)coll_out : (const void*)sout, has_coll ? (int64_t)n * P : 0);
+    const __amdgpu_buffer_rsrc_t tr = make_rsrc(has_tr ? (const void*)traj : (const void*)sin, has_tr ? (int64_t)n * NP * P : 0);
+    b.ex = make_rsrc(has_ex ? (const void*)exec_out : (const void*)sin, has_ex ? (int64_t)n * A * P : 0);
+    b.coll = make_rsrc(has_coll ? (const void*)coll_out : (const void*)sin, has_coll ? (int64_t)n * P : 0);
     StepStats st;
     typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
     for (uint32_t g = blockIdx.x * (uint32_t)kBlock + threadIdx.x; g < nlanes; g += stride) {  // block-uniform
@@ -348,22 +359,34 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
         const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
                                        wave_sum(st.err)};
         unsigned long long* const part = (unsigned long long*)stats;
-        uint32_t ticket = 0u;
+        unsigned long long* const tickets = part + ticket_base(stat_rows);
+        uint32_t last = 0u;
         if ((threadIdx.x & 63u) == 0u) {
             unsigned long long* row = part + (int64_t)(blockIdx.x % stat_rows) * OC_NSTATS;
 #pragma unroll
             for (int c = 0; c < OC_NSTATS; ++c)
                 if (v[c]) atomicAdd(row + c, (unsigned long long)v[c]);
             if (totals != nullptr) {
-                // This wave's adds are performed (vmcnt drained: atomics execute at the memory
-                // side, MI355X_MICROARCH.md "Global float atomics") before it takes a ticket; the
-                // wave holding the last ticket has every wave's adds in the partial rows.
+                // Completion is counted in three levels, so that no counter takes more than
+                // kTicketGroup returning atomics (one counter for all 4,096 waves of a 2^20-env
+                // launch serialised them at the memory side: ~48 us on a one-step launch).  A
+                // wave's adds are performed (vmcnt drained: atomics execute at the memory side,
+                // MI355X_MICROARCH.md "Global float atomics") before it counts itself done in
+                // LDS; the block's last wave counts the block done in its group, the group's
+                // last block counts the group done, and the last group's block folds.
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                ticket = (uint32_t)atomicAdd(part + (int64_t)stat_rows * OC_NSTATS, 1ull);
+                if (atomicAdd(&waves_done, 1u) == (uint32_t)(kBlock / 64) - 1u) {
+                    const uint32_t grp = blockIdx.x / (uint32_t)kTicketGroup, ngrp = (gridDim.x + kTicketGroup - 1) / kTicketGroup;
+                    const uint32_t gsize = min((uint32_t)kTicketGroup, gridDim.x - grp * (uint32_t)kTicketGroup);
+                    unsigned long long* gc = tickets + (int64_t)(1 + grp) * kTicketStride;
+                    if ((uint32_t)atomicAdd(gc, 1ull) == gsize - 1u) {
+                        atomicExch(gc, 0ull);  // the group's counter ready for the next launch
+                        last = (uint32_t)atomicAdd(tickets, 1ull) == ngrp - 1u ? 1u : 0u;
+                    }
+                }
             }
         }
-        const uint32_t nwaves = gridDim.x * (uint32_t)(kBlock / 64);
-        if (totals != nullptr && (uint32_t)__builtin_amdgcn_readfirstlane((int)ticket) == nwaves - 1u) {
+        if (totals != nullptr && __builtin_amdgcn_readfirstlane((int)last) != 0) {
             // Last wave: fold the partial rows into totals (what oc_stats_reduce does after the
             // launch).  The rows are read with returning atomics, which are served at the memory
             // side, so no XCD's L2 can hand back a stale copy.
@@ -379,7 +402,7 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
             if (lane == 0u) {
 #pragma unroll
                 for (int c = 0; c < OC_NSTATS; ++c) totals[c] = acc[c];
-                atomicExch(part + (int64_t)stat_rows * OC_NSTATS, 0ull);  // ticket ready for the next launch
+                atomicExch(tickets, 0ull);  // ready for the next launch
             }
         }
     }
@@ -980,8 +1003,8 @@ struct oc_handle {
     uint8_t roll_blob_host[ocro::kBlobMax];  // the same blob on the host
 };
 
-// Statistics rows, shared by the blocks of every kernel modulo the row count; one more
-// uint64 after them is oc_step_n's ticket counter (zero between launches).
+// Statistics rows, shared by the blocks of every kernel modulo the row count; oc_step_n's
+// completion tickets follow them (ticket_base; zero between launches).
 int64_t stats_rows(const oc_handle*, int64_t B) {
     const int64_t need = pitch_for(B) / kEnvsPerBlock;
     return need < kStatRows ? need : kStatRows;
@@ -1188,11 +1211,22 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
     if (((uintptr_t)state_in | (uintptr_t)state_out | (uintptr_t)actions | (uintptr_t)traj | (uintptr_t)exec_actions |
          (uintptr_t)coll_mask) & 15u)
         return fail(OC_EINVAL, "buffers must be 16-byte aligned");
-    if (traj != nullptr && (traj == state_in || traj == state_out)) return fail(OC_EINVAL, "traj must not alias the state");
     LevelArgs L = h->args;
     L.pitch = pitch_for(B);
     L.B = B;
     const int64_t NP = 3 * h->A + 2 * h->K + 3;
+    // state_out may be the trajectory's last state (written once); nothing else may overlap it
+    const uint8_t* last_slot = traj ? (const uint8_t*)traj + (int64_t)(n - 1) * NP * L.pitch : nullptr;
+    const bool out_is_last = traj != nullptr && (const uint8_t*)state_out == last_slot;
+    if (traj != nullptr) {
+        const uint8_t *t0 = (const uint8_t*)traj, *t1 = t0 + (int64_t)n * NP * L.pitch;
+        auto overlaps = [&](const void* p) {
+            const uint8_t* q = (const uint8_t*)p;
+            return q + NP * L.pitch > t0 && q < t1;
+        };
+        if (overlaps(state_in) || (overlaps(state_out) && !out_is_last))
+            return fail(OC_EINVAL, "traj must not overlap the state (state_out may be its last state)");
+    }
     if (NP * L.pitch >= (1ll << 31)) return fail(OC_EINVAL, "batch too large for one launch (state must be < 2 GiB)");
     // steps per launch so every per-launch buffer (trajectory, actions) stays < 2 GiB of offsets
     int64_t per = ((1ll << 31) - 1) / (NP * L.pitch);
@@ -1210,8 +1244,10 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
         uint8_t* ex = exec_actions ? exec_actions + off * h->A * L.pitch : nullptr;
         uint8_t* cm = coll_mask ? coll_mask + off * L.pitch : nullptr;
         const uint8_t* ac = actions + off * h->A * L.pitch;
+        // the final state is already the trajectory's last state: no separate copy
+        uint8_t* so = (out_is_last && r0 + m >= n) ? nullptr : (uint8_t*)state_out;
 #define OC_LAUNCH_STEPN(A, K)                                                                                     \
-    hipLaunchKernelGGL((oc_step_n_kernel<A, K, kCPnt>), grid, dim3(kBlock), 0, s, L, src, (uint8_t*)state_out, ac, tr, ex, cm, \
+    hipLaunchKernelGGL((oc_step_n_kernel<A, K, kCPnt>), grid, dim3(kBlock), 0, s, L, src, so, ac, tr, ex, cm, \
                        stats, totals, rows, m)
         OC_DISPATCH(h->A, h->K, OC_LAUNCH_STEPN)
         src = (const uint8_t*)state_out;
@@ -1408,7 +1444,8 @@ int oc_state_checksum(const oc_handle* h, const void* state, int64_t B, uint64_t
 
 int oc_stats_size(const oc_handle* h, int64_t B, int64_t* nbytes) {
     if (h == nullptr || nbytes == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
-    *nbytes = (stats_rows(h, B) * OC_NSTATS + 1) * (int64_t)sizeof(uint64_t);  // + oc_step_n's ticket
+    const int64_t groups = ((int64_t)h->cus * 5 + kTicketGroup - 1) / kTicketGroup;  // oc_step_n's grid <= 5 blocks per CU
+    *nbytes = (ticket_base(stats_rows(h, B)) + (1 + groups) * kTicketStride) * (int64_t)sizeof(uint64_t);
     return OC_OK;
 }
 

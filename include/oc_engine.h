@@ -153,7 +153,9 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
  * state is read from HBM once per launch instead of once per step.
  *   actions      : n x u8 [A][pitch], step r at actions + r*A*pitch
  *   traj         : nullable; n x [num_planes][pitch]: the state after every step (traj[r] equals
- *                  the state_out of the r-th oc_step); must not alias state_in/state_out
+ *                  the state_out of the r-th oc_step).  state_in must lie outside it; state_out
+ *                  may be exactly its last state, traj + (n-1)*num_planes*pitch, which is then
+ *                  written once (no second copy of the final state); any other overlap is refused
  *   exec_actions : nullable; n x u8 [A][pitch];  coll_mask : nullable; n x u8 [pitch]
  *   stats        : accumulated over the n steps (same buffer as oc_step); nullable
  *   totals       : nullable (needs stats); OC_NSTATS device uint64: the launch's last wave

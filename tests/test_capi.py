@@ -50,7 +50,9 @@ def test_create_layout_and_validation_without_gpu():
     assert lay.pitch == 1 << 20 and lay.state_bytes == 17 << 20
     assert (lay.plane_item_loc, lay.plane_t, lay.plane_flags) == (P["item_loc"], P["t"], P["flags"])
     n = ctypes.c_int64()
-    assert lib.oc_stats_size(h, 1 << 20, ctypes.byref(n)) == 0 and n.value == (256 * 5 + 1) * 8  # 256 rows + the ticket
+    # 256 rows of 5 counters, then oc_step_n's tickets: one line for the groups, one per group of
+    # 32 blocks of its grid (<= 5 blocks per CU, 256 CUs when no device is visible)
+    assert lib.oc_stats_size(h, 1 << 20, ctypes.byref(n)) == 0 and n.value == (256 * 5 + (1 + 40) * 16) * 8
     assert lib.oc_destroy(h) == 0
     # bad levels are rejected with a message
     bad = capi.level_desc(lv, 2)

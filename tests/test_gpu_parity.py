@@ -293,3 +293,42 @@ def test_step_n_in_place_and_no_outputs(dev):
     eb.step_n(s, s, acts, n)  # in place, no trajectory / exec / coll / stats
     torch.cuda.synchronize()
     assert torch.equal(s, ref)
+
+
+@pytest.mark.parametrize("B,n", [(65536 + 17, 23), (1 << 22, 45)])
+def test_step_n_state_out_is_last_trajectory_state(dev, B, n):
+    """state_out = traj's last state (the bench's launches): the final state is written once, by
+    the trajectory store, and equals the separate-output run; at 2^22 envs n = 45 needs two
+    launches (a launch's offsets stay < 2 GiB), the first of which writes state_out for the
+    second to start from."""
+    eb = _batch("partial-divider_salad", 2, B, 30)
+    P, S, A = eb.pitch, eb.layout.state_bytes, 2
+    s0 = eb.new_state()
+    eb.reset(s0)
+    acts = torch.empty(n * A * P, dtype=torch.uint8, device="cuda:0")
+    for r in range(n):
+        eb.gen_actions(acts[r * A * P:(r + 1) * A * P], r, 5)
+    ref_out, ref_traj = eb.new_state(), torch.zeros(n * S, dtype=torch.uint8, device="cuda:0")
+    ref_stats, ref_tot = eb.new_stats(), torch.zeros(5, dtype=torch.int64, device="cuda:0")
+    eb.step_n(s0, ref_out, acts, n, ref_traj, None, None, ref_stats, ref_tot)
+    traj = torch.zeros(n * S, dtype=torch.uint8, device="cuda:0")
+    stats, tot = eb.new_stats(), torch.full((5,), -1, dtype=torch.int64, device="cuda:0")
+    eb.step_n(s0, traj[(n - 1) * S:], acts, n, traj, None, None, stats, tot)
+    torch.cuda.synchronize()
+    assert torch.equal(traj, ref_traj)
+    assert torch.equal(traj[(n - 1) * S:], ref_out)
+    assert torch.equal(tot, ref_tot)
+
+
+def test_step_n_refuses_other_trajectory_overlaps(dev):
+    eb = _batch("partial-divider_salad", 2, 4096, 30)
+    P, S, n = eb.pitch, eb.layout.state_bytes, 4
+    acts = torch.zeros(n * 2 * P, dtype=torch.uint8, device="cuda:0")
+    traj = torch.zeros((n + 1) * S, dtype=torch.uint8, device="cuda:0")
+    s = eb.new_state()
+    eb.reset(s)
+    for sin, sout in ((traj[S:2 * S], s), (s, traj[:S]), (s, traj[S:2 * S]), (traj[(n - 1) * S:n * S], s)):
+        with pytest.raises(RuntimeError, match="overlap"):
+            eb.step_n(sin, sout, acts, n, traj[:n * S])
+    eb.step_n(s, traj[(n - 1) * S:n * S], acts, n, traj[:n * S])  # the last state: accepted
+    torch.cuda.synchronize()

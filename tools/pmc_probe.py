@@ -8,7 +8,8 @@ Dispatches, on the bench workload (partial-divider_salad, 2 agents, 2^20 envs):
   oc_step_kernel      x20 -- the headline kernel (eager launches)
   oc_step_n_kernel    x3 with 20 steps, then x3 with 100 steps (bench.py's launch lengths: the
                              driver's --steps 20 and the default 100-step cap), trajectory + exec +
-                             coll written, statistics folded in-launch (as bench.py's last launch)
+                             coll written, state_out = the trajectory's last state and statistics
+                             folded in-launch (as bench.py's launches)
 tools/pmc_report.py turns the counter CSVs into profiles/pmc_traffic.json.
 """
 import os
@@ -45,7 +46,7 @@ for n in NFUSED:
     colln = torch.empty(n * eb.pitch, dtype=torch.uint8, device="cuda:0")
     flat = acts[:n].reshape(-1)
     for _ in range(3):
-        eb.step_n(a, b, flat, n, traj, exn, colln, stats, totals)
+        eb.step_n(a, traj[(n - 1) * S:], flat, n, traj, exn, colln, stats, totals)
     torch.cuda.synchronize()
     del traj, exn, colln
 torch.cuda.synchronize()
