@@ -199,8 +199,13 @@ def level1_batch(fx, make_env, **kw):
     return errs
 
 
+# The oracle-row searches are slow on the CPU (a Level-1 call sets up and expands every other
+# agent's planner at every visited state), so the sequential test takes the even-numbered
+# recorded calls and the batched test the odd-numbered ones: every call is checked once on the
+# CPU.  tests/test_planner_gpu.py runs all 32 both ways on the kernel.
 def test_host_plan_batch_level1_matches_reference_calls():
-    fx = _level1_calls()
+    fx = dict(_level1_calls())
+    fx["calls"] = fx["calls"][1::2]
     errs = level1_batch(fx, _env, expander=OracleExpander)
     assert not errs, "\n".join(errs[:10])
 
@@ -209,7 +214,7 @@ def test_host_planner_level1_matches_reference_calls():
     from gym_cooking_amd.planner import E2E_BRTDP
     fx = _level1_calls()
     errs = []
-    for i, c in enumerate(fx["calls"]):
+    for i, c in list(enumerate(fx["calls"]))[0::2]:
         got, want = run_level1_call(fx, c, E2E_BRTDP, _env, expander=OracleExpander)
         if got != want:
             errs.append("call %d (%s, others %s): got %s want %s" % (i, c["subtask"], c["others"], got, want))
