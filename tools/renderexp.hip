@@ -10,6 +10,7 @@
 //               cells idle in the blend loop
 //   product     oc_render_kernel: the wave's listed lanes put their pixels in LDS and the wave
 //               blends them one pixel per lane, two 24-bit multiply-adds per channel pair
+//   product, N blocks per strip   the strip of one (env, cell row) split over N blocks (oc_render: 2)
 //   compact E   the product's scheme with E envs per block (the level-image pixels loaded once
 //               for E envs); modes: no blend, no blend and no level-image loads (store floor),
 //               sprite loads of 4 draws batched before blending
@@ -441,6 +442,7 @@ int main() {
     R.plate_off[0] = desc.plate_off[0]; R.plate_off[1] = desc.plate_off[1];
     for (int a = 0; a < OC_MAX_AGENTS; ++a) R.agent_off[a] = desc.agent_off[a];
     R.chan_map = desc.chan_map;
+    R.parts = 1;
     R.pitch = P;
     for (int m = 0; m < 128; ++m) R.food_sprite[m] = desc.food_sprite[m];
     const dim3 grid((unsigned)(B * 7));
@@ -483,21 +485,30 @@ int main() {
         for (int64_t k = 0; k < B * img; ++k) diff += h0[k] != h1[k];
         printf("%s: %lld differing bytes\n", name, (long long)diff);
     };
+    auto parts = [&](int n) {
+        RenderArgs Rp = R;
+        Rp.parts = n;
+        hipLaunchKernelGGL((oc_render_kernel<4, 4>), dim3((unsigned)(B * 7 * n)), dim3(kBlock), 0, nullptr, Rp, st, atlas_d,
+                           bg_d, o1);
+    };
+    auto p1 = [&]() { parts(1); };
+    auto p2 = [&]() { parts(2); };
+    auto p3 = [&]() { parts(3); };
+    auto p4 = [&]() { parts(4); };
     product();
     CK(hipMemset(o1, 0, B * img)); lane_blend(); check("lane blend");
     CK(hipMemset(o1, 0, B * img)); c1(); check("compact 1");
-    CK(hipMemset(o1, 0, B * img)); c1b(); check("compact 1, batched sprite loads");
-    CK(hipMemset(o1, 0, B * img)); c2(); check("compact 2");
-    CK(hipMemset(o1, 0, B * img)); c4(); check("compact 4");
+    CK(hipMemset(o1, 0, B * img)); p1(); check("product, 1 block per strip");
+    CK(hipMemset(o1, 0, B * img)); p3(); check("product, 3 blocks per strip");
+    CK(hipMemset(o1, 0, B * img)); p4(); check("product, 4 blocks per strip");
     for (int rep = 0; rep < 3; ++rep) {
         time("lane blend (round-2 kernel)", lane_blend);
-        time("product", product);
-        time("compact 1", c1);
-        time("compact 1, batched sprite loads", c1b);
-        time("compact 2", c2);
-        time("compact 4", c4);
+        time("product (oc_render: 2 blocks per strip)", product);
+        time("product, 1 block per strip", p1);
+        time("product, 2 blocks per strip", p2);
+        time("product, 3 blocks per strip", p3);
+        time("product, 4 blocks per strip", p4);
         time("compact 1, no blend", nb1);
-        time("compact 1, no blend, no level image", nl1);
     }
     return 0;
 }
