@@ -37,6 +37,7 @@ Differences from the reference, by design:
 from __future__ import annotations
 
 import copy as _copy
+import functools
 import types
 from collections import namedtuple
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -68,6 +69,25 @@ _TILE_NAMES = {_levels.TILE_FLOOR: "Floor", _levels.TILE_COUNTER: "Counter",
 _FOODS = (("Tomato", _levels.M_TOMATO), ("Lettuce", _levels.M_LETTUCE), ("Onion", _levels.M_ONION))
 
 
+@functools.lru_cache(maxsize=256)
+def _item_names(mask: int):
+    """(contents, name, full_name) of an item mask, as Object.update_names builds them:
+    contents sorted by base name (core.py:161-171)."""
+    parts = []
+    for name, bit in _FOODS:
+        if mask & bit:
+            parts.append((name, ("Chopped" if mask & _levels.chopped(bit) else "Fresh") + name))
+    if mask & _levels.M_PLATE:
+        parts.append(("Plate", "Plate"))
+    parts.sort()
+    return [p[0] for p in parts], "-".join(p[0] for p in parts), "-".join(p[1] for p in parts)
+
+
+def item_name(mask: int) -> str:
+    """The object-group name of an item mask (ItemView.name)."""
+    return _item_names(mask)[1]
+
+
 def action_code(action) -> int:
     """(dx, dy) -> engine action code (World.NAV_ACTIONS order, (0, 0) = no-op)."""
     a = tuple(int(v) for v in action)
@@ -87,16 +107,8 @@ class ItemView:
 
     def __init__(self, slot: int, mask: int, location: Tuple[int, int], is_held: bool):
         self.slot, self.mask, self.location, self.is_held = slot, mask, location, is_held
-        parts = []
-        for name, bit in _FOODS:
-            if mask & bit:
-                parts.append((name, ("Chopped" if mask & _levels.chopped(bit) else "Fresh") + name))
-        if mask & _levels.M_PLATE:
-            parts.append(("Plate", "Plate"))
-        parts.sort()  # update_names: contents sorted by base name (core.py:161-171)
-        self.contents = [p[0] for p in parts]
-        self.name = "-".join(p[0] for p in parts)
-        self.full_name = "-".join(p[1] for p in parts)
+        contents, self.name, self.full_name = _item_names(mask)
+        self.contents = list(contents)
 
     def get_repr(self):
         return ObjectRepr(name=self.full_name, location=self.location, is_held=self.is_held)

@@ -306,7 +306,7 @@ class E2E_BRTDP:
         self._sub_key = str(subtask)
         self._kind, self._goal_mask = kind, goal
         full = env.state_bytes()
-        groups = frozenset(env._group_names) | frozenset(it.name for it in env.world.items)
+        groups = _groups(env)
         start = full.copy() if self._level else self._level0(full, exp)
         start[exp.t_plane:] = 0
         start = np.frombuffer(_canon(start.tobytes(), exp.A, exp.K), np.uint8).copy()
@@ -352,7 +352,7 @@ class E2E_BRTDP:
         """cur_obj_count of _define_goal_state (e2e_brtdp.py:435-566) on a Level-0 state."""
         A, K = exp.A, exp.K
         held = {int(s[2 * A + a]) for a in range(A)} - {0xFF}
-        deliv = {c for c, t in enumerate(level.tiles) if t == 3}
+        deliv = _level_tables(level)[1]
         locs = []
         for j in range(K):
             c, m = int(s[3 * A + j]), int(s[3 * A + K + j])
@@ -657,7 +657,7 @@ class E2E_BRTDP:
         exp = self._exp
         full = env.state_bytes()
         full[exp.t_plane:] = 0
-        groups = frozenset(env._group_names) | frozenset(it.name for it in env.world.items)
+        groups = _groups(env)
         key = (_canon(full.tobytes(), exp.A, exp.K), groups, tuple(self._agents), self._level)
         yield from self._modified_state(key)
 
@@ -698,9 +698,19 @@ class PlanEnv:
         K = (len(self._bytes) - 3 * num_agents - 3) // 2
         loc = self._bytes[3 * num_agents:3 * num_agents + K]
         mask = self._bytes[3 * num_agents + K:3 * num_agents + 2 * K]
-        items = [_envs.ItemView(j, int(m), None, False) for j, (l, m) in enumerate(zip(loc, mask)) if l != 0xFF]
-        self.world = types.SimpleNamespace(items=items)
+        self._live = [(j, int(m)) for j, (l, m) in enumerate(zip(loc, mask)) if l != 0xFF]
+        self._world = None
         self._group_names = frozenset(group_names)
+
+    @property
+    def world(self):
+        if self._world is None:  # built on first use: the planner itself only needs item_names()
+            self._world = types.SimpleNamespace(items=[_envs.ItemView(j, m, None, False) for j, m in self._live])
+        return self._world
+
+    def item_names(self) -> FrozenSet[str]:
+        """The current items' object-group names (ItemView.name of every item not merged away)."""
+        return frozenset(_envs.item_name(m) for _, m in self._live)
 
     def get_agent_names(self) -> List[str]:
         return ["agent-%d" % (a + 1) for a in range(self._A)]
@@ -709,11 +719,29 @@ class PlanEnv:
         return self._bytes.copy()
 
 
+def _level_tables(level):
+    """Per-level values the planner reads at every set-up, computed once per Level object (a
+    level is not edited once planners use it): (tiles as a tuple, the Delivery cells)."""
+    t = level.__dict__.get("_planner_tables")
+    if t is None:
+        tiles = tuple(level.tiles)
+        t = (tiles, frozenset(c for c, k in enumerate(tiles) if k == 3))
+        level.__dict__["_planner_tables"] = t
+    return t
+
+
+def _groups(env) -> FrozenSet[str]:
+    """The env's object-group names since reset plus its current items' names."""
+    fast = getattr(env, "item_names", None)
+    names = fast() if fast is not None else frozenset(it.name for it in env.world.items)
+    return frozenset(env._group_names) | names
+
+
 def expander_key(env, device=None):
     """What an expander is built for: the level's grid and tiles, the agent count, the device.
     Planners may share an expander only when their keys are equal."""
     level = env.level
-    return (level.width, tuple(level.tiles), len(env.get_agent_names()), str(device or env._device))
+    return (level.width, _level_tables(level)[0], len(env.get_agent_names()), str(device or env._device))
 
 
 def plan_batch(planners: Sequence[E2E_BRTDP], envs_, subtasks, agent_names, other_agent_planners=None) -> list:
