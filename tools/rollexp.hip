@@ -7,9 +7,12 @@
 //            load instruction)
 //   rpl4     4 consecutive rows per lane: one dword load per plane (256 B per wave instruction),
 //            the rows run one after another, outputs gathered into dwords and stored once
+//   sorted NT  rows reordered by configuration inside blocks of NT threads (counting sort of the
+//              block's alloc ids in LDS), timed on configuration-major and on shuffled alloc ids
 // The variant's next states, flags and bounds are compared with the product's.
 #include "../gym-cooking_amd/csrc/oc_engine.hip"
 
+#include <random>
 #include <vector>
 
 #define CK(x)                                                                                      \
@@ -85,6 +88,83 @@ __global__ __launch_bounds__(kBlock) void rollout_rpl4(RollArgs R, const uint8_t
     }
 }
 
+// Rows reordered by configuration inside each block of NT threads: a counting sort of the
+// tile's NT alloc ids in LDS, then lane t runs the tile's t-th row in configuration order, so a
+// wave's rows share few configurations whatever the caller's row order.  Row i's outputs still
+// go to row i: results identical to the product's.
+template <int A, int K, int NT>
+__global__ __launch_bounds__(NT) void rollout_sorted(RollArgs R, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
+                                                     const uint8_t* __restrict__ act, const uint8_t* __restrict__ alloc,
+                                                     const uint8_t* __restrict__ blob_g, uint8_t* __restrict__ out_flags,
+                                                     float* __restrict__ lb) {
+    extern __shared__ uint32_t blob_w[];
+    __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
+    __shared__ uint32_t hist[OC_MAX_SUBTASKS + 2];
+    __shared__ uint16_t order[NT];
+    for (int i = threadIdx.x; i < R.blob_words; i += NT) blob_w[i] = ((const uint32_t*)blob_g)[i];
+    constexpr int kSubWords = (int)(sizeof(ocro::Sub) / 4);
+    for (int i = threadIdx.x; i < R.nsub * kSubWords; i += NT) ((uint32_t*)subs)[i] = ((const uint32_t*)R.subs)[i];
+    const uint8_t* blob = (const uint8_t*)blob_w;
+    const int64_t P = R.pitch;
+    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+    const int nb = R.nsub + 2;  // buckets: configurations, bad alloc ids, rows past B
+    for (int64_t tile = (int64_t)blockIdx.x * NT; tile < R.B; tile += (int64_t)gridDim.x * NT) {
+        if ((int)threadIdx.x < nb) hist[threadIdx.x] = 0u;
+        __syncthreads();
+        const int64_t e0 = tile + threadIdx.x;
+        const int b = e0 >= R.B ? nb - 1 : min(alloc != nullptr ? (int)alloc[e0] : 0, R.nsub);
+        const uint32_t rank = atomicAdd(&hist[b], 1u);
+        __syncthreads();
+        if (threadIdx.x < 64) {  // exclusive scan of <= 66 buckets by one wave: 2 per lane
+            const int l = threadIdx.x;
+            const uint32_t c0 = 2 * l < nb ? hist[2 * l] : 0u, c1 = 2 * l + 1 < nb ? hist[2 * l + 1] : 0u;
+            uint32_t inc = c0 + c1;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t o = __shfl_up(inc, off);
+                if (l >= off) inc += o;
+            }
+            const uint32_t ex = inc - c0 - c1;
+            if (2 * l < nb) hist[2 * l] = ex;
+            if (2 * l + 1 < nb) hist[2 * l + 1] = ex + c0;
+        }
+        __syncthreads();
+        order[hist[b] + rank] = (uint16_t)threadIdx.x;
+        __syncthreads();
+        const int64_t e = tile + order[threadIdx.x];
+        if (e < R.B) {
+            ocro::Row r = load_row<A, K>(sin, P, e);
+            const uint16_t t = ((const uint16_t*)(sin + kPT * P))[e];
+            const uint8_t fl_in = sin[kPF * P + e];
+            const int ai = alloc != nullptr ? alloc[e] : 0;
+            float bound = 0.0f;
+            int f = OC_ROLL_BADALLOC;
+            if (ai < R.nsub) {
+                const ocro::Sub& sb = subs[ai];
+                const int c0 = act[sb.agent[0] * P + e], c1 = sb.n == 2 ? act[sb.agent[1] * P + e] : ocro::kNoop;
+                ocro::RowOps<A, K> ops(R.L, blob);
+                f = ops.run(r, sb, c0, c1, bound);
+            }
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                sout[a * P + e] = (uint8_t)r.ax(a);
+                sout[(kPY + a) * P + e] = (uint8_t)r.ay(a);
+                sout[(kPH + a) * P + e] = (uint8_t)r.ah(a);
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                sout[(kPL + j) * P + e] = (uint8_t)r.il(j);
+                sout[(kPM + j) * P + e] = (uint8_t)r.im(j);
+            }
+            ((uint16_t*)(sout + kPT * P))[e] = t;
+            sout[kPF * P + e] = fl_in;
+            out_flags[e] = (uint8_t)f;
+            lb[e] = bound;
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 int main() {
@@ -145,7 +225,7 @@ int main() {
     if (roll_args(h, subs.data(), (int)subs.size(), B, R, true)) { printf("args: %s\n", oc_last_error()); return 1; }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    auto time = [&](const char* name, auto&& fn) {
+    auto time = [&](const char* name, auto&& fn) {  // fn(0): the timed launch
         for (int i = 0; i < 3; ++i) fn(0);
         CK(hipEventRecord(e0));
         for (int i = 0; i < 50; ++i) fn(0);
@@ -158,25 +238,50 @@ int main() {
     auto product = [&](int v) {
         oc_rollout(h, s0, out[v], acts, alloc, subs.data(), (int)subs.size(), fl[v], lbd[v], B, nullptr);
     };
-    time("product (row per lane, u8 plane loads)", product);
-    for (int bpc : {1, 2, 4, 8}) {
-        const int64_t need = (B / 4 + kBlock - 1) / kBlock, cap = (int64_t)h->cus * bpc;
-        const dim3 grid((unsigned)(need < cap ? need : cap));
-        char name[80];
-        snprintf(name, sizeof name, "rpl4 (4 rows per lane, dword loads), <= %d/CU", bpc);
-        auto v4 = [&](int v) {
-            hipLaunchKernelGGL((rollout_rpl4<4, 4>), grid, dim3(kBlock), h->roll_blob_bytes, nullptr, R, s0, out[1], acts,
-                               alloc, h->roll_blob, fl[1], lbd[1]);
-        };
-        time(name, v4);
-    }
-    product(0);
-    CK(hipDeviceSynchronize());
     std::vector<uint8_t> o0(S), o1(S), f0(B), f1(B);
     std::vector<float> l0(B), l1(B);
-    CK(hipMemcpy(o0.data(), out[0], S, hipMemcpyDeviceToHost)); CK(hipMemcpy(o1.data(), out[1], S, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(f0.data(), fl[0], B, hipMemcpyDeviceToHost)); CK(hipMemcpy(f1.data(), fl[1], B, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(l0.data(), lbd[0], 4 * B, hipMemcpyDeviceToHost)); CK(hipMemcpy(l1.data(), lbd[1], 4 * B, hipMemcpyDeviceToHost));
-    printf("outputs %s\n", (o0 == o1 && f0 == f1 && l0 == l1) ? "identical" : "DIFFER");
+    auto same = [&]() {
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(o0.data(), out[0], S, hipMemcpyDeviceToHost)); CK(hipMemcpy(o1.data(), out[1], S, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(f0.data(), fl[0], B, hipMemcpyDeviceToHost)); CK(hipMemcpy(f1.data(), fl[1], B, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(l0.data(), lbd[0], 4 * B, hipMemcpyDeviceToHost)); CK(hipMemcpy(l1.data(), lbd[1], 4 * B, hipMemcpyDeviceToHost));
+        return o0 == o1 && f0 == f1 && l0 == l1;
+    };
+    std::vector<uint8_t> al_rnd(al);
+    {
+        std::mt19937 g(7);
+        for (int64_t e = B - 1; e > 0; --e) std::swap(al_rnd[e], al_rnd[g() % (e + 1)]);
+    }
+    for (int order_i = 0; order_i < 2; ++order_i) {
+        CK(hipMemcpy(alloc, order_i ? al_rnd.data() : al.data(), P, hipMemcpyHostToDevice));
+        const char* on = order_i ? "random order" : "configuration-major";
+        char name[96];
+        snprintf(name, sizeof name, "product (row per lane), %s", on);
+        time(name, product);
+        auto s256 = [&](int v) {
+            hipLaunchKernelGGL((rollout_sorted<4, 4, 256>), dim3((unsigned)((B + 255) / 256)), dim3(256), h->roll_blob_bytes,
+                               nullptr, R, s0, out[v], acts, alloc, h->roll_blob, fl[v], lbd[v]);
+        };
+        auto s1024 = [&](int v) {
+            hipLaunchKernelGGL((rollout_sorted<4, 4, 1024>), dim3((unsigned)((B + 1023) / 1024)), dim3(1024),
+                               h->roll_blob_bytes, nullptr, R, s0, out[v], acts, alloc, h->roll_blob, fl[v], lbd[v]);
+        };
+        snprintf(name, sizeof name, "sorted in 256-row blocks, %s", on);
+        time(name, s256);
+        product(0); s256(1);
+        printf("  outputs %s\n", same() ? "identical" : "DIFFER");
+        auto s512 = [&](int v) {
+            hipLaunchKernelGGL((rollout_sorted<4, 4, 512>), dim3((unsigned)((B + 511) / 512)), dim3(512),
+                               h->roll_blob_bytes, nullptr, R, s0, out[v], acts, alloc, h->roll_blob, fl[v], lbd[v]);
+        };
+        snprintf(name, sizeof name, "sorted in 512-row blocks, %s", on);
+        time(name, s512);
+        product(0); s512(1);
+        printf("  outputs %s\n", same() ? "identical" : "DIFFER");
+        snprintf(name, sizeof name, "sorted in 1024-row blocks, %s", on);
+        time(name, s1024);
+        product(0); s1024(1);
+        printf("  outputs %s\n", same() ? "identical" : "DIFFER");
+    }
     return 0;
 }
