@@ -1,7 +1,7 @@
-// tools/rollexp.hip -- oc_rollout load-width experiment (includes the engine TU).
+// tools/rollexp.hip -- oc_rollout load-width and row-order experiments (includes the engine TU).
 // Build: hipcc -O3 -std=c++20 --offload-arch=gfx950 -o tools/rollexp tools/rollexp.hip
 // Workload: bench.py's C5 rows -- full-divider_salad, 4 agents, 2^18 rows of random-play states,
-// 64 Salad configurations, configuration-major allocation ids, random joint actions.
+// 64 Salad configurations, configuration-major (then shuffled) allocation ids, random joint actions.
 // Variants:
 //   product  oc_rollout_kernel: one row per lane, one u8 load per state plane (64 B per wave
 //            load instruction)
@@ -266,6 +266,17 @@ int main() {
             hipLaunchKernelGGL((rollout_sorted<4, 4, 1024>), dim3((unsigned)((B + 1023) / 1024)), dim3(1024),
                                h->roll_blob_bytes, nullptr, R, s0, out[v], acts, alloc, h->roll_blob, fl[v], lbd[v]);
         };
+        {
+            const int64_t need = (B / 4 + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 4;
+            auto v4 = [&](int v) {
+                hipLaunchKernelGGL((rollout_rpl4<4, 4>), dim3((unsigned)(need < cap ? need : cap)), dim3(kBlock),
+                                   h->roll_blob_bytes, nullptr, R, s0, out[v], acts, alloc, h->roll_blob, fl[v], lbd[v]);
+            };
+            snprintf(name, sizeof name, "rpl4 (4 rows per lane, dword loads), %s", on);
+            time(name, v4);
+            product(0); v4(1);
+            printf("  outputs %s\n", same() ? "identical" : "DIFFER");
+        }
         snprintf(name, sizeof name, "sorted in 256-row blocks, %s", on);
         time(name, s256);
         product(0); s256(1);
