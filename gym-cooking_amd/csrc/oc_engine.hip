@@ -250,6 +250,7 @@ __global__ __launch_bounds__(kStepBlock) void oc_step_kernel(LevelArgs L, const 
 // 128-byte line each): [0] counts finished groups, [1 + g] the finished blocks of group g
 // (kTicketGroup consecutive blocks).  Every counter is back at zero when a launch ends.
 constexpr int kTicketGroup = 32, kTicketStride = 16;  // u64 units
+constexpr int64_t kStatRows = 256;  // statistics rows (stats_rows: fewer for small batches)
 __host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
     return (stat_rows * OC_NSTATS + kTicketStride - 1) / kTicketStride * kTicketStride;
 }
@@ -264,6 +265,7 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
                                                            uint32_t stat_rows, int n) {
     __shared__ uint32_t tbl4[64];
     __shared__ uint32_t waves_done;
+    __shared__ unsigned long long fold[OC_NSTATS][64 + 8];  // the folding wave's partial sums
     if (threadIdx.x < 64u) tbl4[threadIdx.x] = L.cls4[threadIdx.x];
     if (threadIdx.x == 0u) waves_done = 0u;
     __syncthreads();
@@ -390,20 +392,41 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
             // Last wave: fold the partial rows into totals (what oc_stats_reduce does after the
             // launch).  The rows are read with returning atomics, which are served at the memory
             // side, so no XCD's L2 can hand back a stale copy.
+            // All of a lane's reads are issued before any is summed (a rolled loop waited for
+            // each round's reads before issuing the next), and the 64 lanes' sums are added up
+            // in LDS in two rounds of 8 instead of 6 dependent 64-bit shuffle steps per counter.
             const uint32_t lane = threadIdx.x & 63u;
-            unsigned long long acc[OC_NSTATS] = {0ull, 0ull, 0ull, 0ull, 0ull};
-            for (uint32_t r = lane; r < stat_rows; r += 64u) {
+            constexpr int kIt = (int)(kStatRows / 64);
+            unsigned long long got[kIt][OC_NSTATS], acc[OC_NSTATS] = {0ull, 0ull, 0ull, 0ull, 0ull};
 #pragma unroll
-                for (int c = 0; c < OC_NSTATS; ++c) acc[c] += atomicAdd(part + (int64_t)r * OC_NSTATS + c, 0ull);
+            for (int it = 0; it < kIt; ++it) {  // rows past stat_rows read row 0 again and count 0
+                const uint32_t r = lane + 64u * (uint32_t)it, rr = r < stat_rows ? r : 0u;
+#pragma unroll
+                for (int c = 0; c < OC_NSTATS; ++c) got[it][c] = atomicAdd(part + (int64_t)rr * OC_NSTATS + c, 0ull);
             }
 #pragma unroll
-            for (int c = 0; c < OC_NSTATS; ++c)
-                for (int off = 32; off > 0; off >>= 1) acc[c] += __shfl_xor(acc[c], off);
-            if (lane == 0u) {
+            for (int it = 0; it < kIt; ++it)
 #pragma unroll
-                for (int c = 0; c < OC_NSTATS; ++c) totals[c] = acc[c];
-                atomicExch(tickets, 0ull);  // ready for the next launch
+                for (int c = 0; c < OC_NSTATS; ++c)
+                    acc[c] += lane + 64u * (uint32_t)it < stat_rows ? got[it][c] : 0ull;
+#pragma unroll
+            for (int c = 0; c < OC_NSTATS; ++c) fold[c][lane] = acc[c];
+            __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave; keep the compiler from moving reads up
+            if (lane < 8u * OC_NSTATS) {
+                const uint32_t c = lane >> 3, q = lane & 7u;
+                unsigned long long v = 0ull;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v += fold[c][8u * q + i];
+                fold[c][64 + q] = v;
             }
+            __builtin_amdgcn_wave_barrier();
+            if (lane < (uint32_t)OC_NSTATS) {
+                unsigned long long v = 0ull;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v += fold[lane][64 + i];
+                totals[lane] = v;
+            }
+            if (lane == 0u) atomicExch(tickets, 0ull);  // ready for the next launch
         }
     }
 }
@@ -987,7 +1010,6 @@ int hip_check(const char* what) {
 
 // Statistics rows: blocks add into row blockIdx % rows (no-return 64-bit atomics); 256 rows
 // keep the adds to one address to a few dozen per launch and let one wave fold them.
-constexpr int64_t kStatRows = 256;
 
 
 int64_t pitch_for(int64_t B) {
