@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kBlock) void render_lane_blend(RenderArgs R, const 
     }
 }
 
-template <int A, int K, int EPB, int kMode>  // kMode 0 full, 1 no blend, 2 no blend and no level-image loads, 3 full without load batching
+template <int A, int K, int EPB, int kMode>  // kMode 0 full, 1 no blend, 2 no blend and no level-image loads, 3 full without load batching, 4 stores only (constant data, no LDS staging)
 __global__ __launch_bounds__(kBlock) void render_compact(RenderArgs R, const uint8_t* __restrict__ state,
                                                          const uint32_t* __restrict__ atlas,
                                                          const uint32_t* __restrict__ bg, uint8_t* __restrict__ out,
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void render_compact(RenderArgs R, const uin
             const int py = ty * tile + r, px0 = kRenderPx * g;
             tx = div_small(px0, tile, rcpT);
             lx0 = px0 - tx * tile;
-            if (kMode == 2) {
+            if (kMode == 2 || kMode == 4) {
 #pragma unroll
                 for (int k = 0; k < kRenderPx; ++k) p0[k] = (uint32_t)(py * 977 + px0 + k);
             } else {
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void render_compact(RenderArgs R, const uin
                 }
                 __builtin_amdgcn_wave_barrier();
             }
-            if (i < items) {
+            if (kMode != 4 && i < items) {
                 uint32_t w[12];
 #pragma unroll
                 for (int q = 0; q < kRenderPx / 4; ++q) {
@@ -363,7 +363,8 @@ __global__ __launch_bounds__(kBlock) void render_compact(RenderArgs R, const uin
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
                 const int off = q * 64 + lane;
-                if (off * 16 < nbytes) __builtin_nontemporal_store(pix4[wave][off], dst + off);
+                const u32x4 val = kMode == 4 ? u32x4{(uint32_t)off, p0[0], (uint32_t)w0, 0u} : pix4[wave][off];
+                if (off * 16 < nbytes) __builtin_nontemporal_store(val, dst + off);
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -475,6 +476,7 @@ int main() {
     auto c2 = [&]() { launch(render_compact<4, 4, 2, 3>, 2); };
     auto c4 = [&]() { launch(render_compact<4, 4, 4, 3>, 4); };
     auto nb1 = [&]() { launch(render_compact<4, 4, 1, 1>, 1); };
+    auto so1 = [&]() { launch(render_compact<4, 4, 1, 4>, 1); };
     auto nl1 = [&]() { launch(render_compact<4, 4, 1, 2>, 1); };
     std::vector<uint8_t> h0(B * img), h1(B * img);
     auto check = [&](const char* name) {
@@ -509,6 +511,8 @@ int main() {
         time("product, 3 blocks per strip", p3);
         time("product, 4 blocks per strip", p4);
         time("compact 1, no blend", nb1);
+        time("compact 1, no blend, no level image", nl1);
+        time("compact 1, stores only (no LDS staging)", so1);
     }
     return 0;
 }
