@@ -653,9 +653,11 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
     }
 }
 
-// Full-state subtask bounds (oc_subtask_bounds): one env per lane, every subtask configuration
-// of the call in turn (configurations and tables in LDS).  Output [subtask][pitch], so each
-// store instruction of a wave covers 64 consecutive envs of one configuration.
+// Full-state subtask bounds (oc_subtask_bounds): one env per lane, the configurations of the
+// block's chunk (blockIdx.y of gridDim.y contiguous chunks of the call's table) in turn
+// (configurations and tables in LDS).  Output [subtask][pitch], so each store instruction of a
+// wave covers 64 consecutive envs of one configuration.  Chunking the table multiplies the
+// waves of a launch: the walk is LDS-latency bound and one chunk left 4 waves per SIMD.
 template <int A, int K>
 __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                            const uint8_t* __restrict__ blob_g,
@@ -668,7 +670,8 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
         const ocro::Row r = load_row<A, K>(sin, P, e);
         ocro::RowOps<A, K> ops(R.L, blob);
-        for (int i = 0; i < R.nsub; ++i) {
+        const int i0 = (int)(blockIdx.y * R.nsub / gridDim.y), i1 = (int)((blockIdx.y + 1) * R.nsub / gridDim.y);
+        for (int i = i0; i < i1; ++i) {
             float v;
             const bool ok = ops.full_bound(r, subs[i], v);
             lb[i * P + e] = v;
@@ -1385,7 +1388,15 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
     if (const int rc = roll_args(h, subtasks, num_subtasks, B, R)) return rc;
     if (B == 0) return OC_OK;
     const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
-    const dim3 grid((unsigned)(need < cap ? need : cap));
+    const int64_t bx = need < cap ? need : cap;
+    // configuration chunks: enough blocks for 64 per CU, at most one configuration per chunk
+    // (C5, 2^18 envs x 64 configurations: 0.75 ms unchunked, 0.53 / 0.46 / 0.44 / 0.44 ms at
+    // 16 / 32 / 64 / 128 blocks per CU, 0.47 ms at one configuration per block;
+    // profiles/r02/bounds_chunk_sweep.log)
+    int64_t chunks = ((int64_t)h->cus * 64 + bx - 1) / bx;
+    if (chunks > R.nsub) chunks = R.nsub;
+    if (chunks < 1) chunks = 1;
+    const dim3 grid((unsigned)bx, (unsigned)chunks);
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_BOUNDS(A, K)                                                                             \
     hipLaunchKernelGGL((oc_bounds_kernel<A, K>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,            \
