@@ -317,14 +317,16 @@ struct RowOps {
         return count > s.count;
     }
 
-    OC_RH int rg(int c1, int d1, int c2, int d2) const {  // nx.shortest_path_length or -1
-        const int u = T[kNodeOff + c1 * 5 + d1], v = T[kNodeOff + c2 * 5 + d2];
+    OC_RH int nid(int c, int d) const { return T[kNodeOff + c * 5 + d]; }  // graph node of (cell, approach)
+    OC_RH int dn(int u, int v) const {  // nx.shortest_path_length between node ids, or -1
         if (u == kNone || v == kNone) return -1;
         const int d = T[kDistOff + u * L.nnodes + v];
         return d == kNone ? -1 : d;
     }
 
-    // World.get_lower_bound_between_helper (world.py:148-264) with check_bound (:266-283)
+    // World.get_lower_bound_between_helper (world.py:148-264) with check_bound (:266-283).  The
+    // agents' node ids are looked up once and the A-side distances once per A approach, out of
+    // the B loop; the arithmetic and the (ia, ib) order are the reference's.
     OC_RH float helper(const Sub& s, int ag0, int ag1, int Ac, int Bc) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
@@ -332,20 +334,23 @@ struct RowOps {
         const int nA = Acoll ? 4 : 1, nB = Bcoll ? 4 : 1;
         const int dx = Ac % L.W - Bc % L.W, dy = Ac / L.W - Bc / L.W;
         const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
-        for (int ia = 0; ia < nA; ++ia)
+        const int u0 = nid(ag0, 4), u1 = s.n == 1 ? kNone : nid(ag1, 4);
+        for (int ia = 0; ia < nA; ++ia) {
+            const int vA = nid(Ac, Acoll ? ia : 4);
+            int t;
+            const int a1 = dn(u0, vA);
+            const float b1A = a1 < 0 ? per : (float)a1;
+            const float b2A = s.n == 1 ? 0.0f : ((t = dn(u1, vA)) < 0 ? per : (float)t);
             for (int ib = 0; ib < nB; ++ib) {
-                const int da = Acoll ? ia : 4, db = Bcoll ? ib : 4;
+                const int vB = nid(Bc, Bcoll ? ib : 4);
                 float bound;
                 if (s.n == 1) {
-                    const int b1 = rg(ag0, 4, Ac, da), b2 = rg(Ac, da, Bc, db);
-                    if (b1 < 0 || b2 < 0) continue;
-                    bound = (float)(b1 + b2 - 1);
+                    const int b2 = dn(vA, vB);
+                    if (a1 < 0 || b2 < 0) continue;
+                    bound = (float)(a1 + b2 - 1);
                 } else {
-                    int t;
-                    const float b1A = (t = rg(ag0, 4, Ac, da)) < 0 ? per : (float)t;
-                    const float b2A = (t = rg(ag1, 4, Ac, da)) < 0 ? per : (float)t;
-                    const float b1B = (t = rg(ag0, 4, Bc, db)) < 0 ? per : (float)t;
-                    const float b2B = (t = rg(ag1, 4, Bc, db)) < 0 ? per : (float)t;
+                    const float b1B = (t = dn(u0, vB)) < 0 ? per : (float)t;
+                    const float b2B = (t = dn(u1, vB)) < 0 ? per : (float)t;
                     float mA = b1A < b2A ? b1A : b2A, mB = b1B < b2B ? b1B : b2B;
                     if (s.kind == 1 || s.kind == 3) {
                         bound = mA + man - 1.0f;
@@ -359,6 +364,7 @@ struct RowOps {
                 }
                 if (bound < lower) lower = bound;
             }
+        }
         return lower > 1.0f ? lower : 1.0f;
     }
 
