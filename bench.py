@@ -582,6 +582,10 @@ def main() -> int:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     if args.selftest_ranks:
         return selftest_ranks(args)
+    # stdout carries exactly one JSON line: RCCL prints its version banner to file descriptor 1
+    # when the communicator comes up, so fd 1 goes to stderr and the line to a copy of stdout.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ocdist.init("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -608,7 +612,12 @@ def main() -> int:
              torch.empty(n_per * P, dtype=torch.uint8, device=dev)) for _ in range(n_sets)]
     s_a = eb.new_state()
     stats = eb.new_stats()
-    totals = torch.zeros(5, dtype=torch.int64, device=dev)
+    # the rank's summary row: the OC_NSTATS totals the last launch folds in, then the GPU's PCI
+    # (domain, bus, device), all-gathered through RCCL inside the window (at N=1 as well)
+    # (in place: the row is this rank's slice of the gathered [world, 8] buffer)
+    summary_all, summary_row = ocdist.summary_rows(5 + 3, dev)
+    summary_row[5:] = ocdist.device_ident(dev).to(dev)
+    totals = summary_row[:5]
 
     def plan(n_steps_total):
         """The launches of a window, bound once (engine.step_n_launcher: buffers validated
@@ -641,7 +650,7 @@ def main() -> int:
         eb.reset(s_a)
         for f in warm:
             f()
-        ocdist.gather_summaries(totals)
+        ocdist.gather_summaries(summary_row, summary_all)
         torch.cuda.synchronize()
         warm_steps += len(warm) * n_per
         if warm_steps >= W and (time.perf_counter() - t_w) * 1e3 >= args.min_warmup_ms:
@@ -656,7 +665,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for f in timed:
         f()
-    gathered = ocdist.gather_summaries(totals)
+    gathered = ocdist.gather_summaries(summary_row, summary_all)
     torch.cuda.synchronize()
     ocdist.barrier()
     elapsed = time.perf_counter() - t0
@@ -708,7 +717,7 @@ def main() -> int:
         "value": value,
         "unit": "env-steps/s",
         "n_gpus": world,
-        "rccl_ranks": world if torch.distributed.is_initialized() else 0,
+        "rccl_ranks": ocdist.rccl_ranks(),
         "steps": K,
         "warmup": W,
         "ms_per_step": elapsed_max * 1e3 / K,
@@ -754,22 +763,31 @@ def main() -> int:
         line["planner"] = measure_planner(dev, world)
         line["bayes"] = measure_bayes(dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # the C restatement over all host cores (nproc).  The GPU pool gives each
-        # GPU's job a CPU share (cgroup quota, OMP_NUM_THREADS); the same sample threaded to that
-        # share is reported beside it ("job_share").
+        # the C restatement on the host cores this job actually has (the CPU
+        # affinity set capped by the cgroup quota; the GPU pool gives each GPU's job a share of
+        # the machine, and nproc there counts every core of the host).  The same sample on nproc
+        # threads is reported beside it, labelled oversubscribed when nproc exceeds the share.
         hc = host_cores()
         nproc = hc["limits"]["nproc"]
-        line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget, nproc)
+        line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget,
+                                            hc["threads"])
         line["cpu_baseline"]["host_cpu_limits"] = hc["limits"]
+        line["cpu_baseline"]["nproc"] = nproc
         if hc["threads"] != nproc:
-            share = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget / 2, hc["threads"])
-            line["cpu_baseline"]["job_share"] = {k: share[k] for k in ("value", "cores", "sample")}
+            o = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget / 2, nproc)
+            line["cpu_baseline"]["nproc_threads_oversubscribed"] = dict(
+                {k: o[k] for k in ("value", "cores", "sample")},
+                note="%d threads (nproc) on a job granted %d CPUs" % (nproc, hc["threads"]))
+        line["cpu_baseline"]["reference_python_container"] = {
+            "full_step": 695, "logic_only": 9076, "unit": "env-steps/s", "cores": 1,
+            "host": "survey container (Intel Xeon, 8 cores, Python 3.10.12), not the GPU box; BASELINE.md section 2",
+            "sample": "reference OvercookedEnvironment.step() on one partial-divider_salad 2-agent env; logic_only = "
+                      "check_collisions + execute_navigation + done + reward without the copies"}
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(line), flush=True)
-    if torch.distributed.is_initialized():
-        torch.distributed.destroy_process_group()
+        print(json.dumps(line), file=json_out, flush=True)
+    ocdist.shutdown()
     return 0
 
 

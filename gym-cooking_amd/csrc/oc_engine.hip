@@ -699,6 +699,7 @@ struct RenderArgs {
     int32_t plate_off[2], agent_off[OC_MAX_AGENTS];
     uint32_t chan_map;
     int32_t parts;  // blocks per (env, cell row), each a contiguous run of whole waves of groups
+    int32_t counts; // item masks in OC_ENC_COUNTS: translated to the presence masks food_sprite reads
     int64_t pitch;
     uint8_t food_sprite[128];
 };
@@ -761,6 +762,12 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
         };
         // an item: a plate first, its contents at the container class; else the food itself
         auto push_item = [&](uint32_t m, int cls_plain, int cls_in_plate, int plate) {
+            if (R.counts) {  // counts -> presence; two of one food have no sprite (the reference's
+                             // draw opens "<full_name>.png", which does not exist: it raises)
+                const uint32_t c = m & 0x3Fu, pres = (c & 1u) | ((c >> 1) & 2u) | ((c >> 2) & 4u);
+                const uint32_t pl = (m & OC_MC_PLATE) ? OC_M_PLATE : 0u;
+                m = (c & 0x2Au) ? pl : pl | pres | ((m & OC_MC_FRESH) ? 0u : pres << OC_M_CHOPPED_SHIFT);
+            }
             const uint32_t f = m & ~OC_M_PLATE;
             if (m & OC_M_PLATE) push(R.plate_off[plate], cls_plain);
             const int cls = (m & OC_M_PLATE) ? cls_in_plate : cls_plain;
@@ -1070,7 +1077,11 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
         if (t == OC_TILE_DELIVERY && L.done_cell < 0) L.done_cell = c;
     }
     if (L.done_cell < 0) return fail(OC_ELEVEL, "no Delivery tile");
+    if (lv->encoding != OC_ENC_PRESENCE && lv->encoding != OC_ENC_COUNTS)
+        return fail(OC_EINVAL, "encoding %d", lv->encoding);
+    const bool counts = lv->encoding == OC_ENC_COUNTS;
     uint32_t seen_food = 0;
+    int per_food[3] = {0, 0, 0};
     const int K = lv->num_items <= 4 ? 4 : 8;
     uint8_t cell[8], mask[8];
     for (int j = 0; j < 8; ++j) {
@@ -1080,9 +1091,19 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     for (int j = 0; j < lv->num_items; ++j) {
         const int c = lv->item_cell[j], m = lv->item_mask[j];
         if (c >= W * H || lv->tiles[c] == OC_TILE_FLOOR) return fail(OC_ELEVEL, "item %d not on a counter", j);
-        if (m == 0 || (m & 0x80) || (((m >> OC_M_CHOPPED_SHIFT) & 7) & ~(m & 7))) return fail(OC_ELEVEL, "item mask 0x%x", m);
-        if (seen_food & m & 7u) return fail(OC_ELEVEL, "food type present twice (mask ambiguity)");
-        seen_food |= m & 7u;
+        if (counts) {  // a level item is one content: a fresh food (Fresh bit + count 1) or a Plate
+            const int f = m == (int)(OC_MC_FRESH | OC_MC_TOMATO) ? 0 : m == (int)(OC_MC_FRESH | OC_MC_LETTUCE) ? 1
+                          : m == (int)(OC_MC_FRESH | OC_MC_ONION) ? 2 : -1;
+            if (f < 0 && m != (int)OC_MC_PLATE) return fail(OC_ELEVEL, "item mask 0x%x (counts encoding)", m);
+            if (f >= 0 && ++per_food[f] > OC_MC_MAX_PER_FOOD)
+                return fail(OC_ELEVEL, "more than %d of one food type (2-bit counts)", OC_MC_MAX_PER_FOOD);
+        } else {
+            if (m == 0 || (m & 0x80) || (((m >> OC_M_CHOPPED_SHIFT) & 7) & ~(m & 7)))
+                return fail(OC_ELEVEL, "item mask 0x%x", m);
+            if (seen_food & m & 7u)
+                return fail(OC_ELEVEL, "food type present twice: the level needs OC_ENC_COUNTS");
+            seen_food |= m & 7u;
+        }
         cell[j] = (uint8_t)c;
         mask[j] = (uint8_t)m;
     }
@@ -1103,7 +1124,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     for (int c = 0; c < 5; ++c) L.dcell_lut |= (uint64_t)((dcell[c] + 128) & 0xFF) << (8 * c);
     if (max_T > 0x7FFF) return fail(OC_EINVAL, "max_T %d > 32767", max_T);
     ocsw::build_swar_level(L.sw, W, H, L.done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y,
-                           num_agents, cell, mask);
+                           num_agents, cell, mask, lv->encoding);
     oc_handle* h = new oc_handle;
     h->level = *lv;
     h->A = num_agents;
@@ -1122,7 +1143,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     // planner rollout: the static reachability graph's BFS table (world.py:67-108) and the
     // level's other static tables, one blob per level (oc_rollout.h)
     {
-        const int n = ocro::build_roll_level(h->roll, h->roll_blob_host, W, H, lv->tiles);
+        const int n = ocro::build_roll_level(h->roll, h->roll_blob_host, W, H, lv->tiles, lv->encoding);
         if (n < 0) {
             h->roll.nnodes = -1;
         } else {
@@ -1436,6 +1457,7 @@ int oc_render(const oc_handle* h, const void* state, const uint32_t* atlas, cons
     R.plate_off[1] = desc->plate_off[1];
     for (int a = 0; a < OC_MAX_AGENTS; ++a) R.agent_off[a] = desc->agent_off[a];
     R.chan_map = desc->chan_map;
+    R.counts = h->level.encoding == OC_ENC_COUNTS;
     R.pitch = pitch_for(B);
     for (int m = 0; m < 128; ++m) R.food_sprite[m] = desc->food_sprite[m];
     R.parts = 2;  // two blocks per (env, cell row): 0.198 vs 0.214 ms per 1,024 images (3 or 4: 0.211-0.213)

@@ -49,6 +49,7 @@ OC_RH int blob_bytes(int nnodes) { return (kDistOff + nnodes * nnodes + 3) & ~3;
 struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t W, H, perimeter, nnodes;
     int32_t ncut, ndeliv;
+    int32_t enc;  // item mask encoding (OC_ENC_*)
 };
 
 struct Sub {  // oc_subtask, device copy
@@ -84,8 +85,9 @@ OC_RH bool has_byte(uint32_t w, uint32_t v) {
 // Builds the reachability graph of make_reachability_graph (world.py:67-108) and its BFS
 // distances into `blob` (kBlobMax bytes).  Returns the node count, or -1 when the level has
 // more than kMaxCells cells or the graph more than kMaxNodes nodes.
-inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uint8_t* tiles) {
+inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uint8_t* tiles, int enc) {
     L.W = W;
+    L.enc = enc;
     L.H = H;
     L.perimeter = 2 * (W + H);
     L.ncut = L.ndeliv = 0;
@@ -214,13 +216,24 @@ struct RowOps {
         return o;
     }
 
-    static OC_RH int ncontents(int m) { return __builtin_popcount((unsigned)m & 0x0Fu); }
-    static OC_RH bool deliverable(int m) { return ncontents(m) >= 2 && ((m & 7) & ~(m >> 4)) == 0; }
-    static OC_RH bool mergeable(int a, int b) {
-        const int u = a | b;
-        return !(a & b & 8) && ((u & 7) & ~(u >> 4)) == 0;
+    // Object predicates (core.py:176-241) in the level's mask encoding.  OC_ENC_COUNTS: 2-bit
+    // T/L/O counts, 0x40 Plate, 0x80 Fresh (a single fresh food; merged objects are all-Chopped).
+    OC_RH int ncontents(int m) const {
+        return L.enc ? (m & 3) + ((m >> 2) & 3) + ((m >> 4) & 3) + ((m >> 6) & 1)
+                     : __builtin_popcount((unsigned)m & 0x0Fu);
     }
-    static OC_RH bool needs_chopped(int m) { return ncontents(m) == 1 && (m & 0x78) == 0; }
+    OC_RH bool deliverable(int m) const {
+        return L.enc ? ncontents(m) >= 2 : ncontents(m) >= 2 && ((m & 7) & ~(m >> 4)) == 0;
+    }
+    OC_RH bool mergeable(int a, int b) const {
+        const int u = a | b;
+        return L.enc ? !(a & b & 0x40) && !(u & 0x80) : !(a & b & 8) && ((u & 7) & ~(u >> 4)) == 0;
+    }
+    OC_RH bool needs_chopped(int m) const {
+        return L.enc ? (m & 0x80) != 0 : ncontents(m) == 1 && (m & 0x78) == 0;
+    }
+    OC_RH int merged(int a, int b) const { return L.enc ? a + b : a | b; }        // Object.merge
+    OC_RH int chopped(int m) const { return L.enc ? m & 0x7F : m | ((m << 4) & 0x70); }  // Object.chop
 
     // interact(agent, world), play = False (utils/interact.py:4-89)
     OC_RH void interact(Row& r, int a, int code) const {
@@ -244,12 +257,12 @@ struct RowOps {
                 const int o = item_at(r, tc);
                 if (o >= 0) {
                     if (mergeable(hm, r.im(o))) {  // the holder's item absorbs o
-                        Row::s64(r.mask, h, (uint32_t)(hm | r.im(o)));
+                        Row::s64(r.mask, h, (uint32_t)merged(hm, r.im(o)));
                         Row::s64(r.loc, o, kNone);
                         Row::s64(r.mask, o, 0);
                     }
                 } else if (t == kCutboard && needs_chopped(hm)) {
-                    Row::s64(r.mask, h, (uint32_t)(hm | ((hm << 4) & 0x70)));
+                    Row::s64(r.mask, h, (uint32_t)chopped(hm));
                 } else {  // put down
                     Row::s64(r.loc, h, (uint32_t)tc);
                     Row::s32(r.h, a, kNone);

@@ -78,15 +78,18 @@ struct SwarLevel {
                              // and the move delta is added as (positive part) - (negative part)
                              // (each byte stays in 0..254, no carry between envs)
     uint32_t dp_lo, dp_hi, dn_lo, dn_hi;  // big: v_perm LUTs action code -> max(delta, 0), max(-delta, 0)
+    int32_t counts;          // item masks in OC_ENC_COUNTS (a food type repeats on the map): the
+                             // content predicates below read 2-bit counts, a plate bit and a Fresh bit
 };
 
 // Host-side construction of the SwarLevel constants (called by oc_create after validation).
 // cell/mask: item slot templates (OC_LOC_DEAD / 0 past the level's items).
 __host__ __device__ inline void build_swar_level(SwarLevel& S, int W, int H, int done_cell, const uint8_t* goal_mask,
                              int ngoals, int max_T, const uint8_t* spawn_x, const uint8_t* spawn_y,
-                             int num_agents, const uint8_t* cell, const uint8_t* mask) {
+                             int num_agents, const uint8_t* cell, const uint8_t* mask, int encoding) {
     S = SwarLevel{};
     S.W = (uint32_t)W;
+    S.counts = encoding != 0;
     S.tall = H > 8;
     S.big = W * H > 128;
     const int dcell[5] = {W, -W, -1, 1, 0};
@@ -235,16 +238,32 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         const uint32_t hl = gather<K>(Lc, sh, fh1, fh2);
 
         const uint32_t nf = andn(go80, isF80), mv = go80 & isF80;
-        // Object.is_deliverable (core.py:214-219): >= 2 contents, all foods chopped
-        const uint32_t c4 = hm & k0F;
-        const uint32_t two = nz80(((c4 | k80) - k01) & c4);
-        const uint32_t allch = z80(bop3<OC_LUT((!a) & b & c)>(hm >> 4, hm, k07));
-        // mergeable (core.py:222-241): <= 1 plate, every food chopped
-        const uint32_t cu = hm | om;
-        const uint32_t plate_ok = z80(and3(hm, om, k08));
-        const uint32_t food_ok = z80(bop3<OC_LUT((!a) & b & c)>(cu >> 4, cu, k07));
-        // Object.needs_chopped (core.py:176-178): exactly one content, a fresh food
-        const uint32_t nch = bop3<OC_LUT(a & !b & c)>(nz80(c4), two, z80(hm & k78));
+        uint32_t two, allch, plate_ok, food_ok, nch, cu, chopped;
+        if (L.counts) {  // wave-uniform: OC_ENC_COUNTS masks (T/L/O 2-bit counts, 0x40 Plate, 0x80 Fresh)
+            const uint32_t x = hm & k7F;
+            // >= 2 contents: the count bits are not a single unit (0x01, 0x04, 0x10, 0x40) nor zero;
+            // ((x | 0x80) - 1) & x clears the lowest set bit without a borrow into the next env
+            two = nz80(bop3<OC_LUT((a & b) | c)>((x | k80) - k01, x, x & 0x2A2A2A2Au));
+            allch = k80;  // a merged object is all-Chopped (mergeable admits last-state foods only)
+            plate_ok = z80(and3(hm, om, 0x40404040u));
+            food_ok = andn(k80, hm | om);  // no Fresh food on either side
+            nch = hm & k80;                // Object.needs_chopped: a single fresh food
+            cu = x + (om & k7F);           // contents add up; every field sum stays in its bits
+            chopped = x;                   // Object.chop: the Fresh bit goes
+        } else {
+            // Object.is_deliverable (core.py:214-219): >= 2 contents, all foods chopped
+            const uint32_t c4 = hm & k0F;
+            two = nz80(((c4 | k80) - k01) & c4);
+            allch = z80(bop3<OC_LUT((!a) & b & c)>(hm >> 4, hm, k07));
+            // mergeable (core.py:222-241): <= 1 plate, every food chopped
+            cu = hm | om;
+            plate_ok = z80(and3(hm, om, k08));
+            food_ok = z80(bop3<OC_LUT((!a) & b & c)>(cu >> 4, cu, k07));
+            // Object.needs_chopped (core.py:176-178): exactly one content, a fresh food
+            nch = bop3<OC_LUT(a & !b & c)>(nz80(c4), two, z80(hm & k78));
+            // Object.chop (core.py:187-192): the single food's chopped bit (bits 4..6, no cross-byte spill)
+            chopped = bop3<OC_LUT((a & b) | c)>(hm << 4, 0x70707070u, hm);
+        }
         const uint32_t nfh = nf & hold80;
         const uint32_t deliver = and3(nfh & isD80, two, allch);                  // :35-40
         const uint32_t cnt = andn(nfh, isD80);
@@ -264,8 +283,6 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         const uint32_t newOl = fmg | sel(fpk, loc[k], tc);  // merged away: dead (0xFF)
         const uint32_t newOm = andn(om, fmg);
         const uint32_t newHl = sel(full80(reloc), tc, hl);
-        // Object.chop (core.py:187-192): the single food's chopped bit (bits 4..6, no cross-byte spill)
-        const uint32_t chopped = bop3<OC_LUT((a & b) | c)>(hm << 4, 0x70707070u, hm);
         const uint32_t newHm = sel(fmg, cu, sel(full80(chop), chopped, hm));
         // scatter: target slot on merge / pick, held slot on reloc / merge / chop.  The per-slot
         // select masks are one v_perm each: selector byte = slot index (h, or the target slot

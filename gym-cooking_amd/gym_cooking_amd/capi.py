@@ -20,7 +20,7 @@ OC_MAX_CELLS = 255
 OC_MAX_GOALS = 4
 OC_PITCH_ALIGN = 4096
 OC_NSTATS = 5
-OC_ABI_VERSION = 3  # include/oc_engine.h
+OC_ABI_VERSION = 4  # include/oc_engine.h
 OC_EINVAL, OC_EHIP, OC_ELEVEL = -1, -2, -3
 
 OC_FLAG_DONE = 0x01
@@ -45,6 +45,7 @@ class OcLevelDesc(ctypes.Structure):
         ("item_cell", ctypes.c_uint8 * OC_MAX_ITEMS), ("item_mask", ctypes.c_uint8 * OC_MAX_ITEMS),
         ("spawn_x", ctypes.c_uint8 * OC_MAX_AGENTS), ("spawn_y", ctypes.c_uint8 * OC_MAX_AGENTS),
         ("goal_mask", ctypes.c_uint8 * OC_MAX_GOALS),
+        ("encoding", ctypes.c_int32),
     ]
 
 
@@ -126,6 +127,7 @@ def level_desc(level: "_lv.Level", num_agents: int) -> OcLevelDesc:
         d.spawn_y[i] = y
     for i, g in enumerate(goals):
         d.goal_mask[i] = g
+    d.encoding = level.encoding
     return d
 
 

@@ -130,7 +130,7 @@ class BayesianDelegator:
     @staticmethod
     def _config(env, subtask, subtask_agent_names):
         names = env.get_agent_names()
-        kind, starts, goal = _recipes.subtask_masks(subtask)
+        kind, starts, goal = _recipes.subtask_masks(subtask, _planner._encoding(env.level))
         return capi.subtask(kind, [names.index(n) for n in subtask_agent_names], list(starts), goal, 0)
 
     def _doability(self, env, pairs) -> Dict[tuple, bool]:

@@ -66,26 +66,19 @@ COLORS = ["blue", "magenta", "yellow", "green"]  # utils/agent.py:25
 NAV_ACTIONS = [(0, 1), (0, -1), (-1, 0), (1, 0)]  # utils/world.py:16
 _TILE_NAMES = {_levels.TILE_FLOOR: "Floor", _levels.TILE_COUNTER: "Counter",
                _levels.TILE_CUTBOARD: "Cutboard", _levels.TILE_DELIVERY: "Delivery"}
-_FOODS = (("Tomato", _levels.M_TOMATO), ("Lettuce", _levels.M_LETTUCE), ("Onion", _levels.M_ONION))
 
 
-@functools.lru_cache(maxsize=256)
-def _item_names(mask: int):
-    """(contents, name, full_name) of an item mask, as Object.update_names builds them:
-    contents sorted by base name (core.py:161-171)."""
-    parts = []
-    for name, bit in _FOODS:
-        if mask & bit:
-            parts.append((name, ("Chopped" if mask & _levels.chopped(bit) else "Fresh") + name))
-    if mask & _levels.M_PLATE:
-        parts.append(("Plate", "Plate"))
-    parts.sort()
+@functools.lru_cache(maxsize=1024)
+def _item_names(mask: int, enc: int = _levels.ENC_PRESENCE):
+    """(contents, name, full_name) of an item mask in encoding `enc`, as Object.update_names
+    builds them: contents sorted by base name (core.py:161-171)."""
+    parts = _levels.mask_contents(mask, enc)
     return [p[0] for p in parts], "-".join(p[0] for p in parts), "-".join(p[1] for p in parts)
 
 
-def item_name(mask: int) -> str:
+def item_name(mask: int, enc: int = _levels.ENC_PRESENCE) -> str:
     """The object-group name of an item mask (ItemView.name)."""
-    return _item_names(mask)[1]
+    return _item_names(mask, enc)[1]
 
 
 def action_code(action) -> int:
@@ -105,9 +98,10 @@ class ItemView:
     collidable = False
     dynamic = False
 
-    def __init__(self, slot: int, mask: int, location: Tuple[int, int], is_held: bool):
-        self.slot, self.mask, self.location, self.is_held = slot, mask, location, is_held
-        contents, self.name, self.full_name = _item_names(mask)
+    def __init__(self, slot: int, mask: int, location: Tuple[int, int], is_held: bool,
+                 enc: int = _levels.ENC_PRESENCE):
+        self.slot, self.mask, self.location, self.is_held, self.enc = slot, mask, location, is_held, enc
+        contents, self.name, self.full_name = _item_names(mask, enc)
         self.contents = list(contents)
 
     def get_repr(self):
@@ -117,12 +111,10 @@ class ItemView:
         return c_name in self.contents
 
     def needs_chopped(self) -> bool:  # core.py:176-178
-        foods = self.mask & _levels.M_FOODS
-        return len(self.contents) == 1 and foods != 0 and not (self.mask >> 4) & foods
+        return _levels.needs_chopped(self.mask, self.enc)
 
     def is_deliverable(self) -> bool:  # core.py:214-219
-        foods = self.mask & _levels.M_FOODS
-        return len(self.contents) >= 2 and ((self.mask >> 4) & foods) == foods
+        return _levels.is_deliverable(self.mask, self.enc)
 
     def __eq__(self, other):  # core.py:142-146
         return (getattr(other, "name", None) == self.name and getattr(other, "full_name", None) == self.full_name
@@ -222,14 +214,14 @@ class ReachabilityGraph:
         return g
 
 
-def get_subtask_obj(subtask):
+def get_subtask_obj(subtask, enc: int = _levels.ENC_PRESENCE):
     """nav_utils.get_subtask_obj (navigation_planner/utils.py:181-246): (start, goal) objects of
     a subtask (a list of two for Merge; (None, None) for None), compared by contents like the
     reference's Objects."""
-    kind, (sa, sb), goal = _recipes.subtask_masks(subtask)
+    kind, (sa, sb), goal = _recipes.subtask_masks(subtask, enc)
     if kind == 0:
         return None, None
-    obj = lambda m: ItemView(-1, m, None, False)  # noqa: E731
+    obj = lambda m: ItemView(-1, m, None, False, enc)  # noqa: E731
     start = [obj(sa), obj(sb)] if kind == 2 else obj(sa)
     return start, obj(goal)
 
@@ -421,7 +413,7 @@ def build_views(level: _levels.Level, A: int, K: int, env_bytes: np.ndarray, act
     for j in range(K):
         if loc[j] == _levels.LOC_DEAD:
             continue
-        items[j] = ItemView(j, mask[j], level.xy(loc[j]), j in held)
+        items[j] = ItemView(j, mask[j], level.xy(loc[j]), j in held, level.encoding)
     agents = []
     for a in range(A):
         act = None if actions is None else actions[a]
@@ -645,7 +637,7 @@ class OvercookedEnvironment:
     def _subtask_bound(self, subtask, subtask_agent_names):
         names = self.get_agent_names()
         agents = sorted(names.index(n) for n in subtask_agent_names)
-        kind, starts, goal = _recipes.subtask_masks(subtask)
+        kind, starts, goal = _recipes.subtask_masks(subtask, self.level.encoding)
         lb, ok = self._engine.bounds(self._host, [capi.subtask(kind, agents, list(starts), goal, 0)])
         return float(lb[0]), bool(ok[0])
 

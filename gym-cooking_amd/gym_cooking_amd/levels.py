@@ -24,11 +24,18 @@ goal masks.  It restates the parsing rules of the reference loader
   contributes one ``Deliver(full_plate_name)`` subtask (recipe.py:39-47) whose goal
   object has every food in its last state (navigation_planner/utils.py:231-238).
 
-Item contents are encoded as a 7-bit mask: bit0 Tomato,
-bit1 Lettuce, bit2 Onion, bit3 Plate, bit4/5/6 Tomato/Lettuce/Onion chopped.  The
-mask is exact because a level may hold at most one of each food type (validated: a
-second Tomato, Lettuce or Onion is rejected, since a merged dish of two of one food has
-no mask).  Grids of up to 255 cells are supported (cell ids are bytes, 0xFF = dead).
+Item contents are encoded as a byte mask in one of two encodings (include/oc_engine.h):
+* ENC_PRESENCE, for levels with at most one of each food type
+  (every shipped level): bit0 Tomato, bit1 Lettuce, bit2 Onion, bit3 Plate, bit4/5/6
+  Tomato/Lettuce/Onion chopped;
+* ENC_COUNTS, chosen when the map holds a food type more than once (load_level makes one
+  Object per map character with no uniqueness check, overcooked_environment.py:158-165, and
+  merges may then stack two of one food, core.py:194-202): 2-bit counts of Tomato (bits 0-1),
+  Lettuce (2-3) and Onion (4-5), bit6 Plate, bit7 Fresh.  An object's identity is its
+  full_name, a sorted multiset of content names (core.py:143-171); a merged object holds only
+  foods in their last state and at most one plate (mergeable, core.py:222-241), so the Fresh
+  bit only ever marks a single fresh food and the mask is exact for up to 3 of each food.
+Grids of up to 255 cells are supported (cell ids are bytes, 0xFF = dead).
 """
 from __future__ import annotations
 
@@ -50,6 +57,15 @@ M_LETTUCE_CHOPPED = 0x20
 M_ONION_CHOPPED = 0x40
 M_FOODS = M_TOMATO | M_LETTUCE | M_ONION
 
+ENC_PRESENCE = 0
+ENC_COUNTS = 1
+MC_TOMATO = 0x01   # count fields: Tomato bits 0-1, Lettuce 2-3, Onion 4-5
+MC_LETTUCE = 0x04
+MC_ONION = 0x10
+MC_PLATE = 0x40
+MC_FRESH = 0x80
+MAX_PER_FOOD = 3   # ENC_COUNTS: 2-bit counts
+
 # Engine limits (include/oc_engine.h).
 MAX_AGENTS = 4
 MAX_ITEMS = 8
@@ -64,8 +80,9 @@ NOOP = 4
 ACTION_CODE = {a: i for i, a in enumerate(ACTIONS)}
 
 _CHAR_TILE = {" ": TILE_FLOOR, "-": TILE_COUNTER, "/": TILE_CUTBOARD, "*": TILE_DELIVERY}
-_CHAR_ITEM = {"t": M_TOMATO, "l": M_LETTUCE, "o": M_ONION, "p": M_PLATE}
+_CHAR_ITEM = {"t": "FreshTomato", "l": "FreshLettuce", "o": "FreshOnion", "p": "Plate"}  # content full names
 _FOOD_NAMES = (("Tomato", M_TOMATO), ("Lettuce", M_LETTUCE), ("Onion", M_ONION))
+_FOOD_COUNT = {"Tomato": MC_TOMATO, "Lettuce": MC_LETTUCE, "Onion": MC_ONION}
 
 
 def chopped(mask_bit: int) -> int:
@@ -73,46 +90,109 @@ def chopped(mask_bit: int) -> int:
     return mask_bit << 4
 
 
-# Recipe -> Deliver goal mask (recipe.py:199-228; foods in last state, plated).
-RECIPE_GOALS: Dict[str, int] = {
-    "SimpleTomato": M_PLATE | M_TOMATO | chopped(M_TOMATO),
-    "SimpleLettuce": M_PLATE | M_LETTUCE | chopped(M_LETTUCE),
-    "Salad": M_PLATE | M_TOMATO | M_LETTUCE | chopped(M_TOMATO) | chopped(M_LETTUCE),
-    "OnionSalad": (M_PLATE | M_TOMATO | M_LETTUCE | M_ONION
-                   | chopped(M_TOMATO) | chopped(M_LETTUCE) | chopped(M_ONION)),
+# Recipe -> Deliver goal object full name (recipe.py:199-228; foods in last state, plated).
+RECIPE_GOAL_NAMES: Dict[str, str] = {
+    "SimpleTomato": "ChoppedTomato-Plate",
+    "SimpleLettuce": "ChoppedLettuce-Plate",
+    "Salad": "ChoppedLettuce-ChoppedTomato-Plate",
+    "OnionSalad": "ChoppedLettuce-ChoppedOnion-ChoppedTomato-Plate",
 }
 
 
-def mask_full_name(mask: int) -> str:
-    """Reference ``Object.full_name`` of an item mask (core.py:161-171): contents sorted by
-    base name, foods prefixed by their state, joined by '-'."""
+def mask_contents(mask: int, enc: int = ENC_PRESENCE) -> List[Tuple[str, str]]:
+    """The (name, full_name) of every content of an item mask, sorted by name as
+    Object.update_names sorts them (core.py:161-171)."""
     parts = []
-    for name, bit in _FOOD_NAMES:
-        if mask & bit:
-            parts.append((name, ("Chopped" if mask & chopped(bit) else "Fresh") + name))
-    if mask & M_PLATE:
-        parts.append(("Plate", "Plate"))
-    parts.sort()
-    return "-".join(p[1] for p in parts)
+    if enc == ENC_COUNTS:
+        for name, bit in _FOOD_COUNT.items():
+            n = (mask // bit) & 3
+            state = "Fresh" if mask & MC_FRESH else "Chopped"
+            parts += [(name, state + name)] * n
+        if mask & MC_PLATE:
+            parts.append(("Plate", "Plate"))
+    else:
+        for name, bit in _FOOD_NAMES:
+            if mask & bit:
+                parts.append((name, ("Chopped" if mask & chopped(bit) else "Fresh") + name))
+        if mask & M_PLATE:
+            parts.append(("Plate", "Plate"))
+    parts.sort(key=lambda p: p[0])
+    return parts
 
 
-def full_name_mask(full_name: str) -> int:
-    """Inverse of :func:`mask_full_name`."""
+def contents_mask(full_names: Sequence[str], enc: int = ENC_PRESENCE) -> int:
+    """The item mask of an object whose contents have these full names ("FreshTomato",
+    "ChoppedLettuce", "Plate", ...).  Raises ValueError for contents the encoding cannot hold
+    (two of one food under ENC_PRESENCE, a fresh food inside a merge or more than 3 of one
+    food under ENC_COUNTS, two plates)."""
     mask = 0
-    for part in full_name.split("-"):
+    plates = 0
+    foods = []
+    for part in full_names:
         if part == "Plate":
-            mask |= M_PLATE
+            plates += 1
             continue
         for name, bit in _FOOD_NAMES:
-            if part == "Fresh" + name:
-                mask |= bit
-                break
-            if part == "Chopped" + name:
-                mask |= bit | chopped(bit)
+            if part in ("Fresh" + name, "Chopped" + name):
+                foods.append((name, part.startswith("Chopped")))
                 break
         else:
             raise ValueError("unknown content %r" % part)
+    if plates > 1:
+        raise ValueError("two plates in one object")
+    if enc == ENC_COUNTS:
+        mask = MC_PLATE if plates else 0
+        for name, ch in foods:
+            if (mask // _FOOD_COUNT[name]) & 3 == MAX_PER_FOOD:
+                raise ValueError("more than %d %s in one object" % (MAX_PER_FOOD, name))
+            mask += _FOOD_COUNT[name]
+        fresh = [not ch for _, ch in foods]
+        if any(fresh):
+            if len(foods) + plates != 1:
+                raise ValueError("a fresh food inside a merged object")
+            mask |= MC_FRESH
+        return mask
+    mask = M_PLATE if plates else 0
+    for name, ch in foods:
+        bit = dict(_FOOD_NAMES)[name]
+        if mask & bit:
+            raise ValueError("two %s in one object: use ENC_COUNTS" % name)
+        mask |= bit | (chopped(bit) if ch else 0)
     return mask
+
+
+def mask_full_name(mask: int, enc: int = ENC_PRESENCE) -> str:
+    """Reference ``Object.full_name`` of an item mask (core.py:161-171): contents sorted by
+    base name, foods prefixed by their state, joined by '-'."""
+    return "-".join(p[1] for p in mask_contents(mask, enc))
+
+
+def full_name_mask(full_name: str, enc: int = ENC_PRESENCE) -> int:
+    """Inverse of :func:`mask_full_name`."""
+    return contents_mask(full_name.split("-"), enc)
+
+
+def goal_mask(recipe: str, enc: int = ENC_PRESENCE) -> int:
+    """The Deliver goal mask of a recipe class in an encoding."""
+    return full_name_mask(RECIPE_GOAL_NAMES[recipe], enc)
+
+
+# Recipe -> Deliver goal mask in the presence encoding (every shipped level).
+RECIPE_GOALS: Dict[str, int] = {r: goal_mask(r) for r in RECIPE_GOAL_NAMES}
+
+
+def needs_chopped(mask: int, enc: int = ENC_PRESENCE) -> bool:
+    """Object.needs_chopped (core.py:176-178): one content, a fresh food."""
+    if enc == ENC_COUNTS:
+        return bool(mask & MC_FRESH)
+    foods = mask & M_FOODS
+    return len(mask_contents(mask)) == 1 and foods != 0 and not (mask >> 4) & foods
+
+
+def is_deliverable(mask: int, enc: int = ENC_PRESENCE) -> bool:
+    """Object.is_deliverable (core.py:214-219): merged, every food in its last state."""
+    parts = mask_contents(mask, enc)
+    return len(parts) >= 2 and all(fn == "Plate" or fn.startswith("Chopped") for _, fn in parts)
 
 
 @dataclasses.dataclass
@@ -126,6 +206,7 @@ class Level:
     items: List[Tuple[int, int]]          # (cell, mask) in map scan order
     spawns: List[Tuple[int, int]]         # (x, y) spawn lines
     recipes: List[str]
+    encoding: int = ENC_PRESENCE  # item / goal mask encoding (ENC_COUNTS when a food type repeats)
     # ragged maps: grid squares with no map character (a row shorter than the last one) and
     # map characters past the world width (a row longer than the last one), as (x, y, char)
     missing: List[Tuple[int, int]] = dataclasses.field(default_factory=list)
@@ -140,7 +221,7 @@ class Level:
         """Unique Deliver goal masks, in recipe order."""
         out: List[int] = []
         for r in self.recipes:
-            g = RECIPE_GOALS[r]
+            g = goal_mask(r, self.encoding)
             if g not in out:
                 out.append(g)
         return out
@@ -153,6 +234,15 @@ class Level:
             if t == TILE_DELIVERY:
                 return c
         raise ValueError("level %s has no Delivery" % self.name)
+
+    def food_counts(self) -> Dict[str, int]:
+        """Items of each food type on the map."""
+        out = {name: 0 for name, _ in _FOOD_NAMES}
+        for _, m in self.items:
+            for name, _fn in mask_contents(m, self.encoding):
+                if name != "Plate":
+                    out[name] += 1
+        return out
 
     def tile_at(self, x: int, y: int) -> int:
         return self.tiles[y * self.width + x]
@@ -200,9 +290,12 @@ class Level:
             raise ValueError("level %s has %d cells > %d" % (self.name, self.ncells, MAX_CELLS))
         if len(self.items) > MAX_ITEMS:
             raise ValueError("level %s has %d items > %d" % (self.name, len(self.items), MAX_ITEMS))
-        for bit in (M_TOMATO, M_LETTUCE, M_ONION):
-            if sum(1 for _, m in self.items if m & bit) > 1:
-                raise ValueError("level %s holds a food type twice; masks would be ambiguous" % self.name)
+        per_food = self.food_counts()
+        if self.encoding == ENC_PRESENCE and max(per_food.values()) > 1:
+            raise ValueError("level %s holds a food type twice: it needs ENC_COUNTS" % self.name)
+        if max(per_food.values()) > MAX_PER_FOOD:
+            raise ValueError("level %s holds %d of one food type > %d (2-bit content counts)"
+                             % (self.name, max(per_food.values()), MAX_PER_FOOD))
         if not self.recipes:
             raise ValueError("level %s has no recipe (done() asserts a Deliver subtask)" % self.name)
         if len(self.goals) > MAX_GOALS:
@@ -239,7 +332,7 @@ def parse_level_text(text: str, name: str = "custom") -> Level:
         elif phase == 1:
             rows.append(line)
         elif phase == 2:
-            if line not in RECIPE_GOALS:
+            if line not in RECIPE_GOAL_NAMES:
                 raise ValueError("unknown recipe %r" % line)
             recipes.append(line)
         elif phase == 3:
@@ -249,7 +342,7 @@ def parse_level_text(text: str, name: str = "custom") -> Level:
         raise ValueError("empty map")
     width = len(rows[-1])  # world.width = x + 1 of the last map row (:196)
     tiles: List[int] = []
-    items: List[Tuple[int, int]] = []
+    items: List[Tuple[int, str]] = []
     missing: List[Tuple[int, int]] = []
     overflow: List[Tuple[int, int, str]] = []
     for y, row in enumerate(rows):
@@ -265,8 +358,11 @@ def parse_level_text(text: str, name: str = "custom") -> Level:
             else:
                 tiles.append(_CHAR_TILE.get(ch, TILE_FLOOR))
         overflow.extend((x, y, row[x]) for x in range(width, len(row)))
-    return Level(name=name, width=width, height=len(rows), tiles=tiles, items=items,
-                 spawns=spawns, recipes=recipes, missing=missing, overflow=overflow)
+    foods = [fn for _, fn in items if fn != "Plate"]
+    enc = ENC_COUNTS if len(foods) != len(set(foods)) else ENC_PRESENCE
+    return Level(name=name, width=width, height=len(rows), tiles=tiles,
+                 items=[(c, contents_mask([fn], enc)) for c, fn in items], spawns=spawns, recipes=recipes,
+                 encoding=enc, missing=missing, overflow=overflow)
 
 
 def _builtin(divider: str, recipes: Sequence[str], name: str) -> Level:

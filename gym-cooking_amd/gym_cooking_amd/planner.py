@@ -40,6 +40,7 @@ import torch
 
 from . import capi
 from . import envs as _envs
+from . import levels as _levels
 from .engine import _ptr
 from . import recipes as _recipes
 
@@ -47,21 +48,29 @@ _NAV = [(0, 1), (0, -1), (-1, 0), (1, 0), (0, 0)]  # action codes 0..4 (World.NA
 _NOOP = 4
 
 
-_NAMES: Dict[int, str] = {}
+_NAMES: Dict[tuple, str] = {}
 
 
-def _group_name(mask: int) -> str:
-    """World.objects group name of an item mask (its base contents, core.py:161-171)."""
-    n = _NAMES.get(mask)
+def _group_name(mask: int, enc: int = 0) -> str:
+    """World.objects group name of an item mask in encoding `enc` (its base contents,
+    core.py:161-171)."""
+    n = _NAMES.get((mask, enc))
     if n is None:
-        n = _NAMES[mask] = _envs.ItemView(-1, mask, None, False).name
+        n = _NAMES[(mask, enc)] = _envs.item_name(mask, enc)
     return n
+
+
+def _encoding(level) -> int:
+    """The item-mask encoding of a level (a levels.Level or a builtin name / level file)."""
+    if isinstance(level, str):
+        level = _levels.load_level(level)
+    return level.encoding
 
 
 _CAND = {n: list(itertools.product(range(5), repeat=n)) for n in (1, 2)}
 
 
-def _canon(sb: bytes, A: int, K: int) -> bytes:
+def _canon(sb: bytes, A: int, K: int, enc: int = 0) -> bytes:
     """The planner's form of a state: live item slots ordered by (object-group name, slot).
     The reference's repr lists each group's objects in insertion order and nothing else, so
     an item's identity is its group name plus its rank in that group; which slot a merged
@@ -70,7 +79,7 @@ def _canon(sb: bytes, A: int, K: int) -> bytes:
     relative slot order, as they keep their order in World.objects."""
     b = bytearray(sb)
     l0, m0 = 3 * A, 3 * A + K
-    live = sorted((_group_name(b[m0 + j]), j) for j in range(K) if b[l0 + j] != 0xFF)
+    live = sorted((_group_name(b[m0 + j], enc), j) for j in range(K) if b[l0 + j] != 0xFF)
     order = [j for _, j in live]
     if order == list(range(len(order))):
         return bytes(b)
@@ -116,6 +125,7 @@ class _Expander:
         from .engine import OvercookedBatch  # raises without liboc_engine.so / a GPU
         self.eb = OvercookedBatch(level, num_agents, self.ROWS, max_T=0, device=device)
         self.A, self.K, self.P = self.eb.A, self.eb.K, self.eb.pitch
+        self.enc = self.eb.level.encoding
         self.NP = self.eb.layout.num_planes
         self.t_plane = self.eb.layout.plane_t
         dev = self.eb.device
@@ -302,14 +312,14 @@ class E2E_BRTDP:
             self._exp = self._make_expander(level, A, self.device or env._device)
             self._exp_key = key
         exp = self._exp
-        kind, starts, goal = _recipes.subtask_masks(subtask)
+        kind, starts, goal = _recipes.subtask_masks(subtask, exp.enc)
         self._sub_key = str(subtask)
         self._kind, self._goal_mask = kind, goal
         full = env.state_bytes()
         groups = _groups(env)
         start = full.copy() if self._level else self._level0(full, exp)
         start[exp.t_plane:] = 0
-        start = np.frombuffer(_canon(start.tobytes(), exp.A, exp.K), np.uint8).copy()
+        start = np.frombuffer(_canon(start.tobytes(), exp.A, exp.K, exp.enc), np.uint8).copy()
         self.cur_obj_count = self._obj_count(start, exp, env.level)  # _define_goal_state on the Level-0 env
         self._sub = capi.subtask(kind, agents, list(starts), goal, self.cur_obj_count, self._level)
         self._level_name = env.level
@@ -415,7 +425,7 @@ class E2E_BRTDP:
     def _expanded(self, key, cand, res) -> None:
         nxt, fl, lb = res
         sb, groups, agents, lvl = key
-        NP, K, A = len(sb), self._exp.K, self._exp.A
+        NP, K, A, enc = len(sb), self._exp.K, self._exp.A, self._exp.enc
         l0, m0 = 3 * A, 3 * A + K
         raw = nxt.tobytes()
         pmask = sb[m0:m0 + K]
@@ -433,8 +443,8 @@ class E2E_BRTDP:
             ns = raw[r * NP:(r + 1) * NP]
             ng = groups
             if ns[m0:m0 + K] != pmask:  # a chop or a merge: a merge makes a new object group (world.py:304-306)
-                ns = _canon(ns, A, K)
-                ng = groups | frozenset(_group_name(m) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
+                ns = _canon(ns, A, K, enc)
+                ng = groups | frozenset(_group_name(m, enc) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
             nk = (ns, ng, agents, lvl)
             if lvl and _copy_crashes(ns, A):
                 crash = crash or set()
@@ -658,7 +668,7 @@ class E2E_BRTDP:
         full = env.state_bytes()
         full[exp.t_plane:] = 0
         groups = _groups(env)
-        key = (_canon(full.tobytes(), exp.A, exp.K), groups, tuple(self._agents), self._level)
+        key = (_canon(full.tobytes(), exp.A, exp.K, exp.enc), groups, tuple(self._agents), self._level)
         yield from self._modified_state(key)
 
     def _modified_state(self, key):
@@ -701,16 +711,18 @@ class PlanEnv:
         self._live = [(j, int(m)) for j, (l, m) in enumerate(zip(loc, mask)) if l != 0xFF]
         self._world = None
         self._group_names = frozenset(group_names)
+        self._enc = _encoding(level)
 
     @property
     def world(self):
         if self._world is None:  # built on first use: the planner itself only needs item_names()
-            self._world = types.SimpleNamespace(items=[_envs.ItemView(j, m, None, False) for j, m in self._live])
+            self._world = types.SimpleNamespace(items=[_envs.ItemView(j, m, None, False, self._enc)
+                                                       for j, m in self._live])
         return self._world
 
     def item_names(self) -> FrozenSet[str]:
         """The current items' object-group names (ItemView.name of every item not merged away)."""
-        return frozenset(_envs.item_name(m) for _, m in self._live)
+        return frozenset(_envs.item_name(m, self._enc) for _, m in self._live)
 
     def get_agent_names(self) -> List[str]:
         return ["agent-%d" % (a + 1) for a in range(self._A)]

@@ -175,10 +175,10 @@ def _ordered_adds(recipe: str) -> List[Subtask]:
 def initial_state(level: "_levels.Level") -> Tuple[str, ...]:
     """STRIPSWorld initial predicates (stripsworld.py:13-31): None + Fresh(name) per content."""
     preds = [_NONE]
-    for _cell, mask in level.items:
-        for name, bit in (("Plate", _levels.M_PLATE),) + tuple(zip(_FOODS, (_levels.M_TOMATO, _levels.M_LETTUCE,
-                                                                             _levels.M_ONION))):
-            if mask & bit:
+    for _cell, mask in level.items:  # Object.contains per name: one predicate per name it holds
+        names = {n for n, _ in _levels.mask_contents(mask, level.encoding)}
+        for name in ("Plate",) + _FOODS:
+            if name in names:
                 preds.append("Fresh(%s)" % name)
     return tuple(sorted(preds))
 
@@ -245,30 +245,24 @@ def all_subtasks(level: "_levels.Level", max_path_length: int = 14) -> List[Subt
     return out
 
 
-def _name_mask(names: str, chopped: bool) -> int:
-    m = 0
-    for n in names.split("-"):
-        if n == "Plate":
-            m |= _levels.M_PLATE
-            continue
-        bit = {"Tomato": _levels.M_TOMATO, "Lettuce": _levels.M_LETTUCE, "Onion": _levels.M_ONION}[n]
-        m |= bit | (_levels.chopped(bit) if chopped else 0)
-    return m
+def _name_mask(names: str, chopped: bool, enc: int) -> int:
+    return _levels.contents_mask([n if n == "Plate" else ("Chopped" if chopped else "Fresh") + n
+                                  for n in names.split("-")], enc)
 
 
-def subtask_masks(subtask: Optional[Subtask]) -> Tuple[int, Tuple[int, int], int]:
+def subtask_masks(subtask: Optional[Subtask], enc: int = _levels.ENC_PRESENCE) -> Tuple[int, Tuple[int, int], int]:
     """(OC_SUB_* kind, (start mask a, start mask b), goal mask) as nav_utils.get_subtask_obj
-    builds them (navigation_planner/utils.py:181-246): Chop: fresh -> chopped food;
-    Merge: both arguments with every food in its last (chopped) state, a bare Plate as is,
-    goal = their union; Deliver: the plated dish, start == goal."""
+    builds them (navigation_planner/utils.py:181-246), in the level's mask encoding `enc`:
+    Chop: fresh -> chopped food; Merge: both arguments with every food in its last (chopped)
+    state, a bare Plate as is, goal = their merge; Deliver: the plated dish, start == goal."""
     if subtask is None:
         return 0, (0, 0), 0
     if subtask.name == "Chop":
-        return 1, (_name_mask(subtask.args[0], False), 0), _name_mask(subtask.args[0], True)
+        return 1, (_name_mask(subtask.args[0], False, enc), 0), _name_mask(subtask.args[0], True, enc)
     if subtask.name == "Merge":
-        a, b = _name_mask(subtask.args[0], True), _name_mask(subtask.args[1], True)
-        return 2, (a, b), a | b
+        a, b = _name_mask(subtask.args[0], True, enc), _name_mask(subtask.args[1], True, enc)
+        return 2, (a, b), _name_mask(subtask.args[0] + "-" + subtask.args[1], True, enc)
     if subtask.name == "Deliver":
-        m = _name_mask(subtask.args[0], True)
+        m = _name_mask(subtask.args[0], True, enc)
         return 3, (m, 0), m
     raise NotImplementedError("{} was not recognized".format(subtask))  # utils.py:244-245

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define OC_ABI_VERSION 3
+#define OC_ABI_VERSION 4
 
 #define OC_MAX_AGENTS 4
 #define OC_MAX_ITEMS 8
@@ -55,12 +55,29 @@ extern "C" {
 #define OC_TILE_CUTBOARD 2
 #define OC_TILE_DELIVERY 3
 
-/* item content mask bits: presence T,L,O,P + chopped T,L,O */
+/* Item content masks, two encodings (oc_level_desc.encoding).
+ * OC_ENC_PRESENCE: presence T,L,O,P + chopped T,L,O; exact for levels with at
+ *   most one of each food type (every shipped level).
+ * OC_ENC_COUNTS: the multiset of a core.Object's contents (equality is by full_name, a sorted
+ *   multiset: gym_cooking/utils/core.py:143-171): a 2-bit count per food, a plate bit and a
+ *   Fresh bit.  Exact for levels with up to 3 of each food type (load_level makes one Object
+ *   per map character with no uniqueness check, overcooked_environment.py:158-165): an object
+ *   of more than one content is a merge, and mergeable() (core.py:222-241) admits only foods
+ *   in their last state and at most one plate, so a merged object is all-Chopped and the
+ *   Fresh bit only ever marks a single fresh food.  Goal masks never carry it. */
 #define OC_M_TOMATO 0x01u
 #define OC_M_LETTUCE 0x02u
 #define OC_M_ONION 0x04u
 #define OC_M_PLATE 0x08u
 #define OC_M_CHOPPED_SHIFT 4
+#define OC_ENC_PRESENCE 0
+#define OC_ENC_COUNTS 1
+#define OC_MC_TOMATO 0x01u   /* count field bits 0-1 */
+#define OC_MC_LETTUCE 0x04u  /* bits 2-3 */
+#define OC_MC_ONION 0x10u    /* bits 4-5 */
+#define OC_MC_PLATE 0x40u
+#define OC_MC_FRESH 0x80u    /* a single food in its Fresh state */
+#define OC_MC_MAX_PER_FOOD 3
 
 /* action codes: World.NAV_ACTIONS order (gym_cooking/utils/world.py:16) + no-op.
  * Codes > 4 are treated as OC_ACT_NOOP. */
@@ -90,7 +107,8 @@ extern "C" {
 
 typedef struct oc_level_desc {
     int32_t width, height;           /* 3..; width*height <= OC_MAX_CELLS; non-Floor border */
-    int32_t num_items;               /* <= OC_MAX_ITEMS, at most one of each food type */
+    int32_t num_items;               /* <= OC_MAX_ITEMS; OC_ENC_PRESENCE: at most one of each food
+                                        type, OC_ENC_COUNTS: at most OC_MC_MAX_PER_FOOD */
     int32_t num_spawns;              /* >= num_agents */
     int32_t num_goals;               /* 1..OC_MAX_GOALS Deliver goal masks */
     uint8_t tiles[OC_MAX_CELLS];     /* OC_TILE_* per cell, cell = y*width + x */
@@ -99,6 +117,8 @@ typedef struct oc_level_desc {
     uint8_t spawn_x[OC_MAX_AGENTS];
     uint8_t spawn_y[OC_MAX_AGENTS];
     uint8_t goal_mask[OC_MAX_GOALS];
+    int32_t encoding;                /* OC_ENC_*: how item_mask / goal_mask (and every state's item
+                                        masks and oc_subtask masks) encode contents */
 } oc_level_desc;
 
 typedef struct oc_layout {

@@ -25,14 +25,15 @@
 
 typedef struct { int x, y; } Loc;
 
-/* core.Object (gym_cooking/utils/core.py:130-219).  Contents: at most one of each food
- * (level validation) with its FRESH_CHOPPED state index (core.py:250-252, 310-346), plus
- * a plate count. */
+/* core.Object (gym_cooking/utils/core.py:130-219).  Contents: a count of each food type
+ * with the FRESH_CHOPPED state index of those foods (core.py:250-252, 310-346; the foods of
+ * one object share a state: a merge takes only foods in their last state, core.py:222-241),
+ * plus a plate count.  Under OC_ENC_PRESENCE a level holds at most one of each food. */
 typedef struct {
     int alive; /* present in World.objects */
     Loc location;
     int is_held;
-    int food_present[NFOOD];
+    int food_count[NFOOD];
     int food_state[NFOOD]; /* 0 = Fresh, 1 = Chopped */
     int plates;
 } Obj;
@@ -109,8 +110,42 @@ static int object_at(const Env* e, Loc l, int find_held) {
 
 static int n_contents(const Obj* o) {
     int n = o->plates;
-    for (int f = 0; f < NFOOD; ++f) n += o->food_present[f];
+    for (int f = 0; f < NFOOD; ++f) n += o->food_count[f];
     return n;
+}
+
+/* The content mask of an object in the level's encoding (include/oc_engine.h OC_ENC_*): the
+ * canonical identity of Object.full_name (core.py:143-171). */
+static int obj_mask_enc(const Obj* o, int enc) {
+    if (enc == OC_ENC_COUNTS) {
+        static const int unit[NFOOD] = {OC_MC_TOMATO, OC_MC_LETTUCE, OC_MC_ONION};
+        int m = o->plates ? OC_MC_PLATE : 0, fresh = 0;
+        for (int f = 0; f < NFOOD; ++f) {
+            m += o->food_count[f] * unit[f];
+            if (o->food_count[f] && o->food_state[f] == 0) fresh = 1;
+        }
+        return m | (fresh ? OC_MC_FRESH : 0);
+    }
+    int m = o->plates ? OC_M_PLATE : 0;
+    for (int f = 0; f < NFOOD; ++f)
+        if (o->food_count[f]) m |= (1 << f) | (o->food_state[f] << (f + OC_M_CHOPPED_SHIFT));
+    return m;
+}
+
+static void obj_set_mask(Obj* o, int m, int enc) {
+    if (enc == OC_ENC_COUNTS) {
+        o->plates = (m & OC_MC_PLATE) ? 1 : 0;
+        for (int f = 0; f < NFOOD; ++f) {
+            o->food_count[f] = (m >> (2 * f)) & 3;
+            o->food_state[f] = (m & OC_MC_FRESH) ? 0 : 1;
+        }
+        return;
+    }
+    o->plates = (m & OC_M_PLATE) ? 1 : 0;
+    for (int f = 0; f < NFOOD; ++f) {
+        o->food_count[f] = (m >> f) & 1;
+        o->food_state[f] = (m >> (f + OC_M_CHOPPED_SHIFT)) & 1;
+    }
 }
 
 /* Food.done (core.py:293-296): state index is the last of FRESH_CHOPPED */
@@ -122,20 +157,20 @@ static int needs_chopped(const Obj* o) {
     if (n_contents(o) > 1) return 0;
     if (o->plates) return 0;
     for (int f = 0; f < NFOOD; ++f)
-        if (o->food_present[f]) return o->food_state[f] == 0; /* next state is Chopped */
+        if (o->food_count[f]) return o->food_state[f] == 0; /* next state is Chopped */
     return 0;
 }
 
 /* Object.chop (core.py:187-192) */
 static void chop(Obj* o) {
     for (int f = 0; f < NFOOD; ++f)
-        if (o->food_present[f]) o->food_state[f] += 1;
+        if (o->food_count[f]) o->food_state[f] += 1;
 }
 
 /* Object.is_deliverable (core.py:214-219) */
 static int is_deliverable(const Obj* o) {
     for (int f = 0; f < NFOOD; ++f)
-        if (o->food_present[f] && !food_done(o, f)) return 0;
+        if (o->food_count[f] && !food_done(o, f)) return 0;
     return n_contents(o) > 1; /* is_merged */
 }
 
@@ -145,19 +180,19 @@ static int mergeable(const Obj* a, const Obj* b) {
     int plates = a->plates + b->plates;
     if (plates >= 2) return 0;
     for (int f = 0; f < NFOOD; ++f) {
-        if (a->food_present[f] && !food_done(a, f)) return 0;
-        if (b->food_present[f] && !food_done(b, f)) return 0;
+        if (a->food_count[f] && !food_done(a, f)) return 0;
+        if (b->food_count[f] && !food_done(b, f)) return 0;
     }
     return 1;
 }
 
-/* Object.merge (core.py:194-202): contents += other's contents */
+/* Object.merge (core.py:194-202): contents += other's contents (merged foods are all in their
+ * last state, so the counts add up under one state) */
 static void merge(Obj* a, const Obj* b) {
     a->plates += b->plates;
     for (int f = 0; f < NFOOD; ++f)
-        if (b->food_present[f]) {
-            if (a->food_present[f]) abort(); /* duplicate food: outside the level envelope */
-            a->food_present[f] = 1;
+        if (b->food_count[f]) {
+            a->food_count[f] += b->food_count[f];
             a->food_state[f] = b->food_state[f];
         }
 }
@@ -291,10 +326,7 @@ static int done_flags(const Env* e, int max_T) {
         for (int i = 0; i < e->K; ++i) {
             const Obj* o = &e->objs[i];
             if (!o->alive || !loc_eq(o->location, dloc)) continue;
-            int m = o->plates ? OC_M_PLATE : 0; /* goal_obj == o (core.py:143-148) */
-            for (int f = 0; f < NFOOD; ++f)
-                if (o->food_present[f]) m |= (1 << f) | (o->food_state[f] << (f + OC_M_CHOPPED_SHIFT));
-            if (m == gm) ok = 1;
+            if (obj_mask_enc(o, L->encoding) == gm) ok = 1; /* goal_obj == o (core.py:143-148) */
         }
         if (!ok) return 0;
     }
@@ -331,11 +363,7 @@ static void unpack(const Cfg* c, const uint8_t* s, int64_t e, Env* env, int* fla
         o->alive = loc != OC_LOC_DEAD;
         o->location.x = loc % c->L->width;
         o->location.y = loc / c->L->width;
-        o->plates = (m & OC_M_PLATE) ? 1 : 0;
-        for (int f = 0; f < NFOOD; ++f) {
-            o->food_present[f] = (m >> f) & 1;
-            o->food_state[f] = (m >> (f + OC_M_CHOPPED_SHIFT)) & 1;
-        }
+        obj_set_mask(o, m, c->L->encoding);
     }
     for (int a = 0; a < A; ++a) {
         Agent* g = &env->agents[a];
@@ -379,10 +407,7 @@ static void pack(const Cfg* c, const Env* env, int flags, uint8_t* s, int64_t e)
             continue;
         }
         il[k * P + e] = (uint8_t)(o->location.y * c->L->width + o->location.x);
-        int m = o->plates ? OC_M_PLATE : 0;
-        for (int f = 0; f < NFOOD; ++f)
-            if (o->food_present[f]) m |= (1 << f) | (o->food_state[f] << (f + OC_M_CHOPPED_SHIFT));
-        im[k * P + e] = (uint8_t)m;
+        im[k * P + e] = (uint8_t)obj_mask_enc(o, c->L->encoding);
     }
 }
 
@@ -399,12 +424,7 @@ static void template_env(const Cfg* c, Env* env) {
         o->alive = 1;
         o->location.x = c->L->item_cell[k] % c->L->width;
         o->location.y = c->L->item_cell[k] / c->L->width;
-        int m = c->L->item_mask[k];
-        o->plates = (m & OC_M_PLATE) ? 1 : 0;
-        for (int f = 0; f < NFOOD; ++f) {
-            o->food_present[f] = (m >> f) & 1;
-            o->food_state[f] = (m >> (f + OC_M_CHOPPED_SHIFT)) & 1;
-        }
+        obj_set_mask(o, c->L->item_mask[k], c->L->encoding);
     }
     for (int a = 0; a < c->A; ++a) {
         env->agents[a].location.x = c->L->spawn_x[a];
@@ -529,12 +549,6 @@ int oco_gen_actions(int A, uint8_t* act, int64_t B, int64_t pitch, int64_t env_o
  * Navigation-planner rollout, restated from the reference planner.
  * ========================================================================================= */
 
-static int obj_mask(const Obj* o) {
-    int m = o->plates ? OC_M_PLATE : 0;
-    for (int f = 0; f < NFOOD; ++f)
-        if (o->food_present[f]) m |= (1 << f) | (o->food_state[f] << (f + OC_M_CHOPPED_SHIFT));
-    return m;
-}
 
 static int cell_of(const Env* e, Loc l) { return l.y * e->L->width + l.x; }
 
@@ -618,7 +632,7 @@ static int is_goal_state(const Env* e, const oc_subtask* s) {
     if (s->kind == OC_SUB_DELIVER) { /* un-held goal objects on a Delivery square */
         for (int i = 0; i < e->K; ++i) {
             const Obj* o = &e->objs[i];
-            if (o->alive && !o->is_held && obj_mask(o) == s->goal_mask &&
+            if (o->alive && !o->is_held && obj_mask_enc(o, e->L->encoding) == s->goal_mask &&
                 gridsquare_at(e, o->location) == OC_TILE_DELIVERY)
                 ++count;
         }
@@ -626,7 +640,7 @@ static int is_goal_state(const Env* e, const oc_subtask* s) {
         Loc seen[OC_MAX_ITEMS];
         for (int i = 0; i < e->K; ++i) {
             const Obj* o = &e->objs[i];
-            if (!o->alive || obj_mask(o) != s->goal_mask) continue;
+            if (!o->alive || obj_mask_enc(o, e->L->encoding) != s->goal_mask) continue;
             int dup = 0;
             for (int j = 0; j < count; ++j) dup |= loc_eq(seen[j], o->location);
             if (!dup) seen[count++] = o->location;
@@ -756,7 +770,7 @@ static double lower_bound_parts(const Env* e, const Reach* R, const oc_subtask* 
         agent_locs[na++] = e->agents[a].location;
         const int h = e->agents[a].holding;
         if (h >= 0 && s->kind != OC_SUB_MERGE) {
-            const int m = obj_mask(&e->objs[h]);
+            const int m = obj_mask_enc(&e->objs[h], e->L->encoding);
             if (m != s->start_mask[0] && m != s->goal_mask) penalty += 1.0;
         }
     }
@@ -767,13 +781,13 @@ static double lower_bound_parts(const Env* e, const Reach* R, const oc_subtask* 
 #define OBJ_LOCS(mask, out, n)                                                                    \
     do {                                                                                          \
         for (int i = 0; i < e->K; ++i)                                                            \
-            if (e->objs[i].alive && !e->objs[i].is_held && obj_mask(&e->objs[i]) == (mask))       \
+            if (e->objs[i].alive && !e->objs[i].is_held && obj_mask_enc(&e->objs[i], e->L->encoding) == (mask))       \
                 out[n++] = e->objs[i].location;                                                   \
         for (int a = 0; a < e->A; ++a) {                                                          \
             int in = 0;                                                                           \
             for (int q = 0; q < s->num_agents; ++q) in |= s->agent[q] == a;                       \
             if (in && e->active[a] && e->agents[a].holding >= 0 &&                                \
-                obj_mask(&e->objs[e->agents[a].holding]) == (mask))                               \
+                obj_mask_enc(&e->objs[e->agents[a].holding], e->L->encoding) == (mask))                               \
                 out[n++] = e->agents[a].location;                                                 \
         }                                                                                         \
     } while (0)

@@ -50,13 +50,23 @@ def _blit(screen, img, x0, y0):
     screen[y0:y0 + h, x0:x0 + w] = np.where(a == 0, d, (((s - d) * a + 255) >> 8) + d).astype(np.uint8)
 
 
-def _full_name(mask):
-    """Object.full_name without the plate: state + name, sorted by name."""
+COUNT_NAMES = [(2, "Lettuce"), (4, "Onion"), (0, "Tomato")]   # counts encoding: field shift, name
+
+
+def _full_name(mask, enc=0):
+    """Object.full_name without the plate: state + name, sorted by name (counts encoding:
+    include/oc_engine.h OC_ENC_COUNTS, 2-bit counts, 0x40 Plate, 0x80 Fresh)."""
+    if enc:
+        st = "Fresh" if mask & 0x80 else "Chopped"
+        return "-".join("%s%s" % (st, n) for sh, n in COUNT_NAMES for _ in range((mask >> sh) & 3))
     parts = ["%s%s" % ("Chopped" if mask & (bit << 4) else "Fresh", n) for bit, n in NAMES if mask & bit]
     return "-".join(parts)
 
 
-def _draw_obj(screen, spr, mask, x, y, held):
+def _draw_obj(screen, spr, mask, x, y, held, enc=0):
+    """A sprite named after an object of two of one food does not exist: the lookup raises
+    KeyError, as the reference's image load raises (game.py:111-114 opens <full_name>.png)."""
+    plate, foods = (0x40, mask & 0x3F) if enc else (0x08, mask & 0x07)
     holding, container = int(0.5 * SCALE), int(0.7 * SCALE)
     hc = int(0.7 * holding)
     if held:
@@ -66,12 +76,13 @@ def _draw_obj(screen, spr, mask, x, y, held):
     else:
         off_plain, off_in = 0, int(SCALE * (1 - 0.7) / 2)
         size_plain, size_in = SCALE, container
-    if mask & 0x08:  # any Plate in contents
+    if mask & plate:  # any Plate in contents
         _blit(screen, spr["Plate@%d" % size_plain], x * SCALE + off_plain, y * SCALE + off_plain)
-        if mask & 0x07:  # len(obj.contents) > 1
-            _blit(screen, spr["%s@%d" % (_full_name(mask), size_in)], x * SCALE + off_in, y * SCALE + off_in)
+        if foods:  # len(obj.contents) > 1
+            _blit(screen, spr["%s@%d" % (_full_name(mask, enc), size_in)], x * SCALE + off_in, y * SCALE + off_in)
     else:
-        _blit(screen, spr["%s@%d" % (_full_name(mask), size_plain)], x * SCALE + off_plain, y * SCALE + off_plain)
+        _blit(screen, spr["%s@%d" % (_full_name(mask, enc), size_plain)], x * SCALE + off_plain,
+              y * SCALE + off_plain)
 
 
 def render_env(level, env_bytes, A, K, spr=None, channels="reference"):
@@ -102,11 +113,11 @@ def render_env(level, env_bytes, A, K, spr=None, channels="reference"):
     held = {h for h in ah if h < K}
     for j in range(K):
         if loc[j] != 0xFF and j not in held:
-            _draw_obj(screen, spr, mask[j], loc[j] % W, loc[j] // W, False)
+            _draw_obj(screen, spr, mask[j], loc[j] % W, loc[j] // W, False, level.encoding)
     for a in range(A):
         _blit(screen, spr["agent-%s@80" % COLORS[a]], ax[a] * SCALE, ay[a] * SCALE)
         if ah[a] < K:
-            _draw_obj(screen, spr, mask[ah[a]], ax[a], ay[a], True)
+            _draw_obj(screen, spr, mask[ah[a]], ax[a], ay[a], True, level.encoding)
     if channels == "rgb":
         return screen
     out = np.zeros_like(screen)  # Color(0x00RRGGBB) -> r=0, g=R, b=G; stored (g, b, r)

@@ -16,7 +16,7 @@ static void run(const oc_level_desc* lv, const uint8_t* sin, uint8_t* sout, cons
                 const oc_subtask* subs, int nsub, uint8_t* flags, float* lb, int64_t B, int64_t P) {
     static uint8_t blob[ocro::kBlobMax];
     ocro::RollLevel L;
-    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles) < 0) return;
+    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
     for (int64_t e = 0; e < B; ++e) {
         ocro::Row r;
@@ -63,7 +63,7 @@ static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* take
                 int64_t B, int64_t P) {
     static uint8_t blob[ocro::kBlobMax];
     ocro::RollLevel L;
-    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles) < 0) return;
+    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
     for (int64_t e = 0; e < B; ++e) {
         const int ai = alloc ? alloc[e] : 0;
@@ -119,7 +119,7 @@ static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask
                    uint8_t* doable, int64_t B, int64_t P) {
     static uint8_t blob[ocro::kBlobMax];
     ocro::RollLevel L;
-    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles) < 0) return;
+    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
     for (int64_t e = 0; e < B; ++e) {
         ocro::Row r;

@@ -47,7 +47,8 @@ static void run(const oc_level_desc* lv, int max_T, const uint8_t* sin, uint8_t*
     uint8_t cell[8], mask[8];
     for (int j = 0; j < 8; ++j) { cell[j] = j < lv->num_items ? lv->item_cell[j] : 0xFF; mask[j] = j < lv->num_items ? lv->item_mask[j] : 0; }
     ocsw::SwarLevel S;
-    ocsw::build_swar_level(S, W, H, done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y, A, cell, mask);
+    ocsw::build_swar_level(S, W, H, done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y, A, cell, mask,
+                           lv->encoding);
     auto cls_of = [&](uint32_t cells) -> uint32_t {
         return (uint32_t)tbl[cells & 0xFF] | ((uint32_t)tbl[(cells >> 8) & 0xFF] << 8) |
                ((uint32_t)tbl[(cells >> 16) & 0xFF] << 16) | ((uint32_t)tbl[cells >> 24] << 24);

@@ -1,6 +1,6 @@
 """User levels outside the nine shipped 7x7 kitchens (CPU): grids of 120, 169 and 255 cells, a
 9x9 OnionSalad kitchen of 6 items (the engine's 8-slot layout, which no shipped level uses),
-ragged maps and a repeated food type.  Pinned to what the reference itself does with the same
+and ragged maps.  Pinned to what the reference itself does with the same
 level files (tests/golden/gen_biglevels.py: load_level/reset tables, 54 + 21 recorded episodes,
 3,865 + 5,400 subtask-bound rows, the exceptions ragged maps raise):
   * levels.parse_level_text builds the reference's tables (overcooked_environment.py:144-198);
@@ -8,9 +8,8 @@ level files (tests/golden/gen_biglevels.py: load_level/reset tables, 54 + 21 rec
     bit for bit (cell ids >= 128 take the SWAR step's full-byte compare path);
   * the host build of the planner-table row (oc_rollout.h) reproduces the reference's lower
     bounds and allocation feasibility on the 120- and 169-cell kitchens;
-  * ragged maps raise what the reference raises (KeyError at reset, IndexError at step);
-  * a second Tomato / Lettuce / Onion is refused by the level check and by oc_create."""
-import ctypes
+  * ragged maps raise what the reference raises (KeyError at reset, IndexError at step).
+Levels that repeat a food type are tests/test_duplevels.py's."""
 import json
 import os
 
@@ -134,28 +133,6 @@ def test_ragged_long_map_loads_and_step_raises_indexerror():
     with pytest.raises(IndexError):  # the batched engine refuses a level the reference cannot step
         lv.validate(2)
     lv.within_width().validate(2)
-
-
-def test_repeated_food_type_is_refused():
-    text = "\n".join(["-----t-", "/     l", "/     t", "*     -", "-     -", "-     p", "-----p-"]) + \
-        "\n\nSalad\n\n2 1\n4 1\n"
-    lv = levels.parse_level_text(text, "two-tomatoes")
-    with pytest.raises(ValueError, match="food type twice"):
-        lv.validate(2)
-    # the C-ABI refuses it too (oc_create's own check; no device needed)
-    lib = capi.load_library()
-    d = capi.OcLevelDesc()
-    d.width, d.height, d.num_items, d.num_spawns, d.num_goals = lv.width, lv.height, len(lv.items), 2, 1
-    for c, t in enumerate(lv.tiles):
-        d.tiles[c] = t
-    for j, (c, m) in enumerate(lv.items):
-        d.item_cell[j], d.item_mask[j] = c, m
-    for a, (x, y) in enumerate(lv.spawns[:2]):
-        d.spawn_x[a], d.spawn_y[a] = x, y
-    d.goal_mask[0] = lv.goals[0]
-    h = ctypes.c_void_p()
-    assert lib.oc_create(ctypes.byref(d), 2, 100, 0, ctypes.byref(h)) == capi.OC_ELEVEL
-    assert b"twice" in lib.oc_last_error()
 
 
 def test_grid_past_255_cells_is_refused():

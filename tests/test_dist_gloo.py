@@ -88,3 +88,11 @@ def test_shard_arithmetic():
     assert [ocdist.shard(100, r, 4).env_offset for r in range(4)] == [0, 100, 200, 300]
     parts = [ocdist.shard_global(10, r, 3) for r in range(3)]
     assert [(p.env_offset, p.batch) for p in parts] == [(0, 4), (4, 3), (7, 3)]
+
+
+def test_summarize_lists_device_ids():
+    g = torch.tensor([[3, 1, 300, 2, 0, 0, 0x75, 0], [4, 2, 400, 1, 1, 0, 0x05, 0]], dtype=torch.int64)
+    s = ocdist.summarize(g)
+    assert s["episodes"] == 7 and s["successes"] == 3 and s["errors"] == 1
+    assert s["per_rank_pci"] == ["0000:75:00", "0000:05:00"] and s["distinct_devices"] == 2
+    assert "per_rank_pci" not in ocdist.summarize(g[:, :5])
