@@ -1295,13 +1295,16 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
         uint8_t* ex = exec_actions ? exec_actions + off * h->A * L.pitch : nullptr;
         uint8_t* cm = coll_mask ? coll_mask + off * L.pitch : nullptr;
         const uint8_t* ac = actions + off * h->A * L.pitch;
-        // the final state is already the trajectory's last state: no separate copy
-        uint8_t* so = (out_is_last && r0 + m >= n) ? nullptr : (uint8_t*)state_out;
+        // With a trajectory, a launch's final state is its last trajectory slot: the next launch
+        // starts from there, and state_out is written by the last launch only (and not at all
+        // when it is the trajectory's last state).  So no launch reads a buffer it also writes.
+        const bool last = r0 + m >= n;
+        uint8_t* so = (traj != nullptr && !last) || (out_is_last && last) ? nullptr : (uint8_t*)state_out;
 #define OC_LAUNCH_STEPN(A, K)                                                                                     \
     hipLaunchKernelGGL((oc_step_n_kernel<A, K, kCPnt>), grid, dim3(kBlock), 0, s, L, src, so, ac, tr, ex, cm, \
-                       stats, totals, rows, m)
+                       stats, last ? totals : nullptr, rows, m)
         OC_DISPATCH(h->A, h->K, OC_LAUNCH_STEPN)
-        src = (const uint8_t*)state_out;
+        src = traj != nullptr ? tr + (int64_t)(m - 1) * NP * L.pitch : (const uint8_t*)state_out;
         if (const int rc = hip_check("oc_step_n launch")) return rc;
     }
     return OC_OK;

@@ -43,13 +43,16 @@ constexpr int kNodeOff = 256;                      // [256 * 5] cell * 5 + appro
 constexpr int kCutOff = kNodeOff + 256 * 5;        // [256] Cutboard cells, L.ncut of them
 constexpr int kDelivOff = kCutOff + 256;           // [256] Delivery cells, L.ndeliv of them
 constexpr int kDistOff = kDelivOff + 256;          // [nnodes][nnodes] BFS distances
-constexpr int kBlobMax = kDistOff + kMaxNodes * kMaxNodes;
-OC_RH int blob_bytes(int nnodes) { return (kDistOff + nnodes * nnodes + 3) & ~3; }
+// after the distances, at dmin_off: [2][nnodes] the distance from a node to the nearest
+// Cutboard (row 0) / Delivery (row 1) approach node, 0xFF = none reachable
+constexpr int kBlobMax = kDistOff + kMaxNodes * kMaxNodes + 2 * kMaxNodes;
+OC_RH int blob_bytes(int nnodes) { return (kDistOff + nnodes * nnodes + 2 * nnodes + 3) & ~3; }
 
 struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t W, H, perimeter, nnodes;
     int32_t ncut, ndeliv;
-    int32_t enc;  // item mask encoding (OC_ENC_*)
+    int32_t enc;       // item mask encoding (OC_ENC_*)
+    int32_t dmin_off;  // blob offset of the nearest-Cutboard / nearest-Delivery distance rows
 };
 
 struct Sub {  // oc_subtask, device copy
@@ -158,6 +161,26 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
                     q[qt++] = v;
                 }
             }
+        }
+    }
+    // Chop and Deliver have a static B side (every Cutboard / every Delivery square, from any
+    // side it is approached from): the single-agent bound's min over B of dist(A node, B node)
+    // is this per-node table (world.py:175-189 evaluated once per level)
+    L.dmin_off = kDistOff + n * n;
+    for (int side = 0; side < 2; ++side) {
+        const uint8_t* cells = blob + (side == 0 ? kCutOff : kDelivOff);
+        const int nc = side == 0 ? L.ncut : L.ndeliv;
+        uint8_t* dm = blob + L.dmin_off + side * n;
+        for (int v = 0; v < n; ++v) {
+            int best = kNone;
+            for (int i = 0; i < nc; ++i)
+                for (int d = 0; d < 4; ++d) {
+                    const int b = node[cells[i] * 5 + d];
+                    if (b == kNone) continue;
+                    const int dd = dist[v * n + b];
+                    if (dd != kNone && dd < best) best = dd;
+                }
+            dm[v] = (uint8_t)best;
         }
     }
     return n;
@@ -338,8 +361,10 @@ struct RowOps {
     }
 
     // World.get_lower_bound_between_helper (world.py:148-264) with check_bound (:266-283).  The
-    // agents' node ids are looked up once and the A-side distances once per A approach, out of
-    // the B loop; the arithmetic and the (ia, ib) order are the reference's.
+    // agents' node ids are looked up once, the A-side distances once per A approach and (two
+    // agents) the B-side distances once per B approach, out of the pair loop; the arithmetic
+    // and the (ia, ib) order are the reference's.  Only Merge comes here: Chop and Deliver have
+    // a static B side (helper_static).
     OC_RH float helper(const Sub& s, int ag0, int ag1, int Ac, int Bc) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
@@ -347,36 +372,97 @@ struct RowOps {
         const int nA = Acoll ? 4 : 1, nB = Bcoll ? 4 : 1;
         const int dx = Ac % L.W - Bc % L.W, dy = Ac / L.W - Bc / L.W;
         const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
-        const int u0 = nid(ag0, 4), u1 = s.n == 1 ? kNone : nid(ag1, 4);
+        const int u0 = nid(ag0, 4);
+        if (s.n == 1) {
+            for (int ia = 0; ia < nA; ++ia) {
+                const int vA = nid(Ac, Acoll ? ia : 4);
+                const int a1 = dn(u0, vA);
+                if (a1 < 0) continue;
+                for (int ib = 0; ib < nB; ++ib) {
+                    const int b2 = dn(vA, nid(Bc, Bcoll ? ib : 4));
+                    if (b2 < 0) continue;
+                    const float bound = (float)(a1 + b2 - 1);
+                    if (bound < lower) lower = bound;
+                }
+            }
+            return lower > 1.0f ? lower : 1.0f;
+        }
+        const int u1 = nid(ag1, 4);
+        float b1B[4], b2B[4];
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) {
+            b1B[ib] = b2B[ib] = per;
+            if (ib < nB) {
+                const int vB = nid(Bc, Bcoll ? ib : 4);
+                int t;
+                if ((t = dn(u0, vB)) >= 0) b1B[ib] = (float)t;
+                if ((t = dn(u1, vB)) >= 0) b2B[ib] = (float)t;
+            }
+        }
         for (int ia = 0; ia < nA; ++ia) {
             const int vA = nid(Ac, Acoll ? ia : 4);
             int t;
-            const int a1 = dn(u0, vA);
-            const float b1A = a1 < 0 ? per : (float)a1;
-            const float b2A = s.n == 1 ? 0.0f : ((t = dn(u1, vA)) < 0 ? per : (float)t);
-            for (int ib = 0; ib < nB; ++ib) {
-                const int vB = nid(Bc, Bcoll ? ib : 4);
-                float bound;
-                if (s.n == 1) {
-                    const int b2 = dn(vA, vB);
-                    if (a1 < 0 || b2 < 0) continue;
-                    bound = (float)(a1 + b2 - 1);
-                } else {
-                    const float b1B = (t = dn(u0, vB)) < 0 ? per : (float)t;
-                    const float b2B = (t = dn(u1, vB)) < 0 ? per : (float)t;
-                    float mA = b1A < b2A ? b1A : b2A, mB = b1B < b2B ? b1B : b2B;
-                    if (s.kind == 1 || s.kind == 3) {
-                        bound = mA + man - 1.0f;
-                    } else {
-                        if ((b1A == mA && b1B == mB) || (b2A == mA && b2B == mB)) {
-                            mA *= 2.0f;
-                            mB *= 2.0f;
-                        }
-                        bound = (mA > mB ? mA : mB) + (man - 1.0f) * 0.5f;
-                    }
+            const float b1A = (t = dn(u0, vA)) < 0 ? per : (float)t;
+            const float b2A = (t = dn(u1, vA)) < 0 ? per : (float)t;
+#pragma unroll
+            for (int ib = 0; ib < 4; ++ib) {
+                if (ib >= nB) continue;
+                float mA = b1A < b2A ? b1A : b2A, mB = b1B[ib] < b2B[ib] ? b1B[ib] : b2B[ib];
+                if ((b1A == mA && b1B[ib] == mB) || (b2A == mA && b2B[ib] == mB)) {
+                    mA *= 2.0f;
+                    mB *= 2.0f;
                 }
+                const float bound = (mA > mB ? mA : mB) + (man - 1.0f) * 0.5f;
                 if (bound < lower) lower = bound;
             }
+        }
+        return lower > 1.0f ? lower : 1.0f;
+    }
+
+    // min over a static B side (every Cutboard for Chop, every Delivery for Deliver) of
+    // helper(s, ag0, ag1, Ac, B), without walking the B squares:
+    //  * one agent: bound = d(agent, A) + d(A, B) - 1 over reachable pairs, and min over B of
+    //    d(A node, B node) is the level's per-node table dm (world.py:175-189);
+    //  * two agents: bound = min(d1(A), d2(A)) + manhattan(A, B) - 1 (world.py:215, 242-244),
+    //    where B enters only through manhattan(A, B): the nearest square of the side, whichever
+    //    approach node.
+    // helper() clamps each pair's result to >= 1 and starts from perimeter + 1; both are
+    // monotone, so the min over B of helper() is this with the same clamp.  Exact in fp32.
+    OC_RH float helper_static(const Sub& s, int ag0, int ag1, int Ac, const uint8_t* bl, int nb,
+                              const uint8_t* dm) const {
+        const float per = (float)L.perimeter;
+        float lower = per + 1.0f;
+        if (nb == 0) return lower;
+        const bool Acoll = tile(Ac) != kFloor;
+        const int nA = Acoll ? 4 : 1;
+        const int u0 = nid(ag0, 4);
+        if (s.n == 1) {
+            for (int ia = 0; ia < nA; ++ia) {
+                const int vA = nid(Ac, Acoll ? ia : 4);
+                const int a1 = dn(u0, vA);
+                if (a1 < 0 || dm[vA] == kNone) continue;
+                const float bound = (float)(a1 + (int)dm[vA] - 1);
+                if (bound < lower) lower = bound;
+            }
+        } else {
+            const int u1 = nid(ag1, 4), ax = Ac % L.W, ay = Ac / L.W;
+            int man = 0x7FFF;
+            for (int i = 0; i < nb; ++i) {
+                const int dx = ax - bl[i] % L.W, dy = ay - bl[i] / L.W;
+                const int m = (dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy);
+                man = m < man ? m : man;
+            }
+            float mA = per;
+            for (int ia = 0; ia < nA; ++ia) {
+                const int vA = nid(Ac, Acoll ? ia : 4);
+                int t;
+                const float b1A = (t = dn(u0, vA)) < 0 ? per : (float)t;
+                const float b2A = (t = dn(u1, vA)) < 0 ? per : (float)t;
+                const float m2 = b1A < b2A ? b1A : b2A;
+                mA = m2 < mA ? m2 : mA;
+            }
+            const float bound = mA + (float)man - 1.0f;
+            if (bound < lower) lower = bound;
         }
         return lower > 1.0f ? lower : 1.0f;
     }
@@ -427,14 +513,13 @@ struct RowOps {
             if (h != kNone && s.kind != 2 && r.im(h) != s.start[0] && r.im(h) != s.goal) pen = 1.0f;
         }
         float lower = (float)L.perimeter + 1.0f;
-        if (s.kind == 1 || s.kind == 3) {
+        if (s.kind == 1 || s.kind == 3) {  // static B side: one table lookup per A approach
             const uint8_t* bl = T + (s.kind == 1 ? kCutOff : kDelivOff);
             const int nb = s.kind == 1 ? L.ncut : L.ndeliv;
+            const uint8_t* dm = T + L.dmin_off + (s.kind == 1 ? 0 : L.nnodes);
             visit_objs(r, s.start[0], s.kind == 3, [&](int Ac) OC_RL {
-                for (int i = 0; i < nb; ++i) {
-                    const float b = helper(s, ag0, ag1, Ac, bl[i]);
-                    if (b < lower) lower = b;
-                }
+                const float b = helper_static(s, ag0, ag1, Ac, bl, nb, dm);
+                if (b < lower) lower = b;
             });
         } else if (s.kind == 2) {
             visit_objs(r, s.start[0], false, [&](int Ac) OC_RL {

@@ -81,6 +81,10 @@ class OvercookedBatch:
         return torch.empty(self.pitch, dtype=torch.uint8, device=self.device)
 
     def new_stats(self) -> torch.Tensor:
+        """A zeroed statistics buffer.  Besides the partial rows it holds step_n's completion
+        counters, which must be zero when a launch with `totals` starts (every completed launch
+        leaves them zero): zero it again after a faulted launch, and do not share one buffer
+        between concurrent step_n calls on different streams."""
         return torch.zeros(self.stats_bytes // 8, dtype=torch.uint64, device=self.device)
 
     def planes(self, state: torch.Tensor) -> Dict[str, torch.Tensor]:
@@ -136,8 +140,9 @@ class OvercookedBatch:
                         coll: Optional[torch.Tensor] = None, stats: Optional[torch.Tensor] = None,
                         totals: Optional[torch.Tensor] = None):
         """Validate the buffers of an oc_step_n call once and return a zero-argument callable
-        that issues it on the current stream (the buffers must stay alive and unchanged in
-        shape): a repeated launch then costs one ctypes call, no per-call checks."""
+        that issues it (the buffers must stay alive and unchanged in shape): a repeated launch
+        then costs one ctypes call, no per-call checks.  The stream is bound here: the callable
+        launches on the stream that was current when it was made, whichever is current later."""
         self._check(state_in, self.layout.state_bytes)
         self._check(state_out, self.layout.state_bytes)
         self._check(actions, n * self.A * self.pitch)
@@ -174,6 +179,8 @@ class OvercookedBatch:
         flags = torch.empty(self.pitch, dtype=torch.uint8, device=self.device) if flags is None else flags
         lower_bound = (torch.empty(self.pitch, dtype=torch.float32, device=self.device)
                        if lower_bound is None else lower_bound)
+        self._check(flags, self.pitch)
+        self._check(lower_bound, 4 * self.pitch, (torch.float32,))
         subs = capi.subtask_array(subtasks)
         capi.check(self.lib.oc_rollout(self._h, _ptr(state_in), _ptr(state_out), _ptr(actions), _ptr(alloc), subs,
                                        len(subtasks), _ptr(flags), _ptr(lower_bound), self.B, self._stream()))

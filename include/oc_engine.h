@@ -177,10 +177,17 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
  *                  may be exactly its last state, traj + (n-1)*num_planes*pitch, which is then
  *                  written once (no second copy of the final state); any other overlap is refused
  *   exec_actions : nullable; n x u8 [A][pitch];  coll_mask : nullable; n x u8 [pitch]
- *   stats        : accumulated over the n steps (same buffer as oc_step); nullable
+ *   stats        : accumulated over the n steps (the oc_step layout, plus completion counters
+ *                  after the statistics rows that must be zero when a launch with totals starts:
+ *                  a zeroed buffer from the caller, which every completed launch leaves zeroed);
+ *                  nullable.  Concurrent oc_step_n calls with totals (different streams) must
+ *                  not share a stats buffer, and a buffer whose launch faulted must be re-zeroed
  *   totals       : nullable (needs stats); OC_NSTATS device uint64: the launch's last wave
  *                  folds the stats buffer into it, i.e. oc_stats_reduce after the steps
- *                  without a second launch (main.py's per-episode bookkeeping for the window). */
+ *                  without a second launch (main.py's per-episode bookkeeping for the window).
+ * A call longer than one launch can carry (the trajectory and action offsets of a launch stay
+ * < 2 GiB, and at most 4096 steps) runs as several launches, each starting from the previous
+ * one's last trajectory state; the results are the same. */
 int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions, void* traj,
               uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, uint64_t* totals, int64_t B, int32_t n,
               void* stream);

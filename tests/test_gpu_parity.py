@@ -332,3 +332,31 @@ def test_step_n_refuses_other_trajectory_overlaps(dev):
             eb.step_n(sin, sout, acts, n, traj[:n * S])
     eb.step_n(s, traj[(n - 1) * S:n * S], acts, n, traj[:n * S])  # the last state: accepted
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("with_traj", [True, False])
+def test_step_n_past_4096_steps_splits_launches(dev, with_traj):
+    """n = 4100 steps on a small batch runs as two launches (at most 4096 steps each); the second
+    starts from the first one's last trajectory state (or from state_out without a trajectory)
+    and the outputs equal 4100 oc_step calls."""
+    B, n, A = 300, 4100, 2
+    eb = _batch("open-divider_salad", A, B, 37)
+    P, S = eb.pitch, eb.layout.state_bytes
+    acts = torch.empty(n * A * P, dtype=torch.uint8, device="cuda:0")
+    for r in range(n):
+        eb.gen_actions(acts[r * A * P:(r + 1) * A * P], r, 8)
+    s0 = eb.new_state()
+    eb.reset(s0)
+    traj = torch.zeros(n * S, dtype=torch.uint8, device="cuda:0") if with_traj else None
+    out = traj[(n - 1) * S:] if with_traj else eb.new_state()
+    stats, tot = eb.new_stats(), torch.zeros(5, dtype=torch.int64, device="cuda:0")
+    eb.step_n(s0, out, acts, n, traj, None, None, stats, tot)
+    s, s2, st1 = s0.clone(), eb.new_state(), eb.new_stats()
+    for r in range(n):
+        eb.step(s, s2, acts[r * A * P:(r + 1) * A * P], None, None, st1)
+        if with_traj and r in (0, 4095, 4096, n - 1):
+            assert torch.equal(traj[r * S:(r + 1) * S], s2), r
+        s, s2 = s2, s
+    torch.cuda.synchronize()
+    assert torch.equal(out, s)
+    assert torch.equal(tot, eb.reduce_stats(st1))
