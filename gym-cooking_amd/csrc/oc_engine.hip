@@ -73,6 +73,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// Wave-uniform "some env of the wave": the step's rare-event split (ocsw::step4).
+struct WaveAny {
+    __device__ __forceinline__ bool operator()(uint32_t v) const { return __ballot(v != 0u) != 0ull; }
+};
+
 // One lane's slice of the batch: kEPL consecutive envs, one dword per byte plane.
 template <int A, int K>
 struct Chunk {
@@ -135,7 +140,7 @@ struct StepStats {
 };
 
 // Step the kEPL envs of chunk c (SWAR, oc_swar.h) and store every output plane word of lane g.
-template <int A, int K, int CP = 0>
+template <int A, int K, int CP = 0, int MODE = 1>
 __device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tbl, Chunk<A, K>& c, const Bufs& b,
                                            bool has_ex, bool has_coll, uint32_t P, uint32_t g, StepStats& st) {
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
@@ -146,21 +151,26 @@ __device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tb
     };
     const uint32_t f_in = c.wf;
     uint32_t T0 = c.wt.x, T1 = c.wt.y, ex[A], cm;
-    ocsw::step4<A, K>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, c.wa, ex, cm, cls_of);
+    uint32_t pending = ocsw::at_done80<K, MODE>(L.sw, c.wl);  // a loaded state: the full path once
+    const bool full = ocsw::step4<A, K, MODE>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, c.wa, ex, cm,
+                                              cls_of, WaveAny{}, pending);
 
-    // statistics over the valid envs: an episode ended iff DONE is newly set
+    // statistics over the valid envs: an episode ended iff DONE is newly set (only on the
+    // full path: without a rare event no flag is set)
     const int64_t rem = L.B - (int64_t)g * kEPL;
     const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (rem <= 0 ? 0u : (1u << (8 * (uint32_t)rem)) - 1u);
-    const uint32_t ended = (c.wf & ~f_in & vmask) & ocsw::k01;  // bit0 per env
-    st.eps += __popc(ended);
-    st.succ += __popc(c.wf & (ended << 1));
-    st.err += __popc(c.wf & (ended << 2));
     st.coll += __popc(cm & vmask);
-    const uint32_t efull = (0x80808080u - ended) ^ 0x80808080u;  // 0x01 -> 0xFF per byte, no multiply
-    const uint32_t e16a = __builtin_amdgcn_perm(0u, efull, 0x01010000u);  // env 0,1 -> u16 masks
-    const uint32_t e16b = __builtin_amdgcn_perm(0u, efull, 0x03030202u);  // env 2,3
-    const uint32_t sa = T0 & e16a, sb = T1 & e16b;
-    st.steps += (sa & 0xFFFFu) + (sa >> 16) + (sb & 0xFFFFu) + (sb >> 16);
+    if (full) {
+        const uint32_t ended = (c.wf & ~f_in & vmask) & ocsw::k01;  // bit0 per env
+        st.eps += __popc(ended);
+        st.succ += __popc(c.wf & (ended << 1));
+        st.err += __popc(c.wf & (ended << 2));
+        const uint32_t efull = (0x80808080u - ended) ^ 0x80808080u;  // 0x01 -> 0xFF per byte, no multiply
+        const uint32_t e16a = __builtin_amdgcn_perm(0u, efull, 0x01010000u);  // env 0,1 -> u16 masks
+        const uint32_t e16b = __builtin_amdgcn_perm(0u, efull, 0x03030202u);  // env 2,3
+        const uint32_t sa = T0 & e16a, sb = T1 & e16b;
+        st.steps += (sa & 0xFFFFu) + (sa >> 16) + (sb & 0xFFFFu) + (sb >> 16);
+    }
 
     const uint32_t vo = g * 4u;
 #pragma unroll
@@ -193,7 +203,7 @@ __device__ __forceinline__ void step_chunk(const LevelArgs& L, const uint8_t* tb
 // software-pipelined chunk loop (2 chunks per lane at this size: mostly ramp and drain),
 // 10.2 with 256-thread blocks, 9.1 with 2 chunks per lane, and 6.5 for the same loads and
 // stores with no compute.  Staggering block start times did not help (9.2-9.3).
-template <int A, int K>
+template <int A, int K, int MODE>
 __global__ __launch_bounds__(kStepBlock) void oc_step_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
                                                              uint8_t* __restrict__ sout,
                                                              const uint8_t* __restrict__ actions,
@@ -227,7 +237,7 @@ __global__ __launch_bounds__(kStepBlock) void oc_step_kernel(LevelArgs L, const 
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     StepStats st;
-    step_chunk<A, K, kCPsc1>(L, tbl, c, b, has_ex, has_coll, P, g, st);
+    step_chunk<A, K, kCPsc1, MODE>(L, tbl, c, b, has_ex, has_coll, P, g, st);
     if (stats != nullptr) {  // wave sums, then fire-and-forget 64-bit atomics into this block's row
         const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
                                        wave_sum(st.err)};
@@ -255,7 +265,7 @@ __host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
     return (stat_rows * OC_NSTATS + kTicketStride - 1) / kTicketStride * kTicketStride;
 }
 
-template <int A, int K, int CP = 0, int LCP = 0>
+template <int A, int K, int CP, int LCP, int MODE>
 __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
                                                            uint8_t* __restrict__ sout,
                                                            const uint8_t* __restrict__ actions,
@@ -293,6 +303,7 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
         load_chunk<A, K>(c, b, P, g);
         const uint32_t vo = g * 4u;
         uint32_t T0 = c.wt.x, T1 = c.wt.y, nxt[A];
+        uint32_t pending = ocsw::at_done80<K, MODE>(L.sw, c.wl);  // the loaded state: the full path once
         const int64_t rem = L.B - (int64_t)g * kEPL;
         const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (rem <= 0 ? 0u : (1u << (8 * (uint32_t)rem)) - 1u);
 #pragma unroll
@@ -309,16 +320,19 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
                 for (int a = 0; a < A; ++a) nxt[a] = bld32<LCP>(b.act, vo, (uint32_t)((r + 2) * A + a) * P);
             }
             const uint32_t f_in = c.wf;
-            ocsw::step4<A, K>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, act, ex, cm, cls_of);
-            const uint32_t ended = (c.wf & ~f_in & vmask) & ocsw::k01;
-            st.eps += __popc(ended);
-            st.succ += __popc(c.wf & (ended << 1));
-            st.err += __popc(c.wf & (ended << 2));
+            const bool full = ocsw::step4<A, K, MODE>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, act, ex,
+                                                      cm, cls_of, WaveAny{}, pending);
             st.coll += __popc(cm & vmask);
-            const uint32_t efull = (0x80808080u - ended) ^ 0x80808080u;  // no multiply
-            const uint32_t sa = T0 & __builtin_amdgcn_perm(0u, efull, 0x01010000u);
-            const uint32_t sb2 = T1 & __builtin_amdgcn_perm(0u, efull, 0x03030202u);
-            st.steps += (sa & 0xFFFFu) + (sa >> 16) + (sb2 & 0xFFFFu) + (sb2 >> 16);
+            if (full) {  // episode ends only on the full path
+                const uint32_t ended = (c.wf & ~f_in & vmask) & ocsw::k01;
+                st.eps += __popc(ended);
+                st.succ += __popc(c.wf & (ended << 1));
+                st.err += __popc(c.wf & (ended << 2));
+                const uint32_t efull = (0x80808080u - ended) ^ 0x80808080u;  // no multiply
+                const uint32_t sa = T0 & __builtin_amdgcn_perm(0u, efull, 0x01010000u);
+                const uint32_t sb2 = T1 & __builtin_amdgcn_perm(0u, efull, 0x03030202u);
+                st.steps += (sa & 0xFFFFu) + (sa >> 16) + (sb2 & 0xFFFFu) + (sb2 >> 16);
+            }
             // Unconditional stores: an absent output's descriptor has num_records 0, so its
             // stores are dropped by the buffer range check.  Guarding them with branches made
             // the waitcnt pass merge a store-free path into the loop back-edge and wait for
@@ -1215,6 +1229,31 @@ int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
         default: return fail(OC_EINVAL, "unsupported (A,K)=(%d,%d)", (A_), (K_));           \
     }
 
+// The step kernels: 4-slot levels of the common class (H <= 8, W*H <= 128, presence masks:
+// every shipped kitchen) take the MODE 0 build of the SWAR step, everything else MODE 1.
+#define OC_DISPATCH_STEP(h_, LAUNCH)                                                        \
+    if ((h_)->K == 4 && !(h_)->args.sw.tall && !(h_)->args.sw.big && !(h_)->args.sw.counts) {  \
+        switch ((h_)->A) {                                                                  \
+            case 1: LAUNCH(1, 4, 0); break;                                                 \
+            case 2: LAUNCH(2, 4, 0); break;                                                 \
+            case 3: LAUNCH(3, 4, 0); break;                                                 \
+            case 4: LAUNCH(4, 4, 0); break;                                                 \
+            default: return fail(OC_EINVAL, "unsupported A=%d", (h_)->A);                   \
+        }                                                                                   \
+    } else {                                                                                \
+        switch ((h_)->A * 10 + (h_)->K) {                                                   \
+            case 14: LAUNCH(1, 4, 1); break;                                                \
+            case 24: LAUNCH(2, 4, 1); break;                                                \
+            case 34: LAUNCH(3, 4, 1); break;                                                \
+            case 44: LAUNCH(4, 4, 1); break;                                                \
+            case 18: LAUNCH(1, 8, 1); break;                                                \
+            case 28: LAUNCH(2, 8, 1); break;                                                \
+            case 38: LAUNCH(3, 8, 1); break;                                                \
+            case 48: LAUNCH(4, 8, 1); break;                                                \
+            default: return fail(OC_EINVAL, "unsupported (A,K)=(%d,%d)", (h_)->A, (h_)->K); \
+        }                                                                                   \
+    }
+
 int oc_reset(const oc_handle* h, void* state, int64_t B, void* stream) {
     if (h == nullptr || state == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
     if (B == 0) return OC_OK;
@@ -1244,10 +1283,10 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
     const dim3 grid((unsigned)(L.pitch / kEPL / kStepBlock));  // pitch is a multiple of 4096
     const uint32_t rows = (uint32_t)stats_rows(h, B);
     hipStream_t s = (hipStream_t)stream;
-#define OC_LAUNCH_STEP(A, K)                                                                              \
-    hipLaunchKernelGGL((oc_step_kernel<A, K>), grid, dim3(kStepBlock), 0, s, L, (const uint8_t*)state_in, \
+#define OC_LAUNCH_STEP(A, K, MODE)                                                                        \
+    hipLaunchKernelGGL((oc_step_kernel<A, K, MODE>), grid, dim3(kStepBlock), 0, s, L, (const uint8_t*)state_in, \
                        (uint8_t*)state_out, actions, exec_actions, coll_mask, stats, rows)
-    OC_DISPATCH(h->A, h->K, OC_LAUNCH_STEP)
+    OC_DISPATCH_STEP(h, OC_LAUNCH_STEP)
     return hip_check("oc_step launch");
 }
 
@@ -1300,10 +1339,10 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
         // when it is the trajectory's last state).  So no launch reads a buffer it also writes.
         const bool last = r0 + m >= n;
         uint8_t* so = (traj != nullptr && !last) || (out_is_last && last) ? nullptr : (uint8_t*)state_out;
-#define OC_LAUNCH_STEPN(A, K)                                                                                     \
-    hipLaunchKernelGGL((oc_step_n_kernel<A, K, kCPnt>), grid, dim3(kBlock), 0, s, L, src, so, ac, tr, ex, cm, \
-                       stats, last ? totals : nullptr, rows, m)
-        OC_DISPATCH(h->A, h->K, OC_LAUNCH_STEPN)
+#define OC_LAUNCH_STEPN(A, K, MODE)                                                                    \
+    hipLaunchKernelGGL((oc_step_n_kernel<A, K, kCPnt, 0, MODE>), grid, dim3(kBlock), 0, s, L, src, so, ac, tr, ex, \
+                       cm, stats, last ? totals : nullptr, rows, m)
+        OC_DISPATCH_STEP(h, OC_LAUNCH_STEPN)
         src = traj != nullptr ? tr + (int64_t)(m - 1) * NP * L.pitch : (const uint8_t*)state_out;
         if (const int rc = hip_check("oc_step_n launch")) return rc;
     }

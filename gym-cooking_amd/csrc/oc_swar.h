@@ -151,12 +151,41 @@ OC_SW uint32_t gather(const uint32_t (&V)[K], uint32_t s, uint32_t f1, uint32_t 
     }
 }
 
+// h80 per env: some item of the env lies on the first Delivery square (done()'s square).
+template <int K, int MODE = 1>
+OC_SW uint32_t at_done80(const SwarLevel& L, const uint32_t (&Lc)[K]) {
+    const bool big = MODE ? (bool)L.big : false;
+    uint32_t hit = 0u;
+#pragma unroll
+    for (int j = 0; j < K; ++j) hit |= big ? zf80(Lc[j] ^ L.done_rep) : eq80(Lc[j], L.done_rep);
+    return hit;
+}
+
 // One step of 4 envs x A agents x K item slots.  `cls_of(cellword)` returns per byte the
 // tile class bits of that cell: 0x80 Floor, 0x40 Delivery, 0x20 Cutboard.
-template <int A, int K, class ClassOf>
-OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_t (&H)[A],
+//
+// Rare-event split.  done()'s success test, the auto-reset selects and the episode-end flags
+// only matter in a step with a rare event: an env reset, the timeout, the copy crash (ERR),
+// or a delivery.  Items reach a Delivery square only by being delivered and never leave it (no
+// pick-up from, no merge onto a Delivery, interact.py:35-40, 73-84), and a state whose
+// success test held was DONE and is reset in the next step; so in a state this step produced,
+// success can newly hold only in a step that delivered.  `any_of(word)` is true when the word
+// is nonzero in any env of the wave (a ballot; the host harness tests its own lane), and
+// `pending` marks envs of a state that came from outside (a launch's loaded state): they take
+// the full path once, since an item may already sit on the Delivery square (the gym shim
+// clears DONE and steps again, as the reference keeps stepping a finished env).  Without a
+// rare event in the wave the step leaves flags 0, keeps every item, and only advances t.
+// Random play at the bench's shapes meets one in about 1 % of wave-steps.
+// MODE 0 compiles the step for the common level class (H <= 8 rows, W*H <= 128 cells, presence
+// masks: every shipped kitchen) with the tall / big / counts paths removed; MODE 1 reads the
+// level's flags (wave-uniform branches).  Returns whether the wave took the full path.
+template <int A, int K, int MODE = 1, class ClassOf, class AnyOf>
+OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_t (&H)[A],
                  uint32_t (&Lc)[K], uint32_t (&M)[K], uint32_t& T0, uint32_t& T1, uint32_t& F,
-                 const uint32_t (&ACT)[A], uint32_t (&EX)[A], uint32_t& CM, ClassOf cls_of) {
+                 const uint32_t (&ACT)[A], uint32_t (&EX)[A], uint32_t& CM, ClassOf cls_of, AnyOf any_of,
+                 uint32_t& pending) {
+    const bool tall = MODE ? (bool)L.tall : false, big = MODE ? (bool)L.big : false;
+    const bool counts = MODE ? (bool)L.counts : false;
     const uint32_t rst = full80((F << 7) & k80);  // input DONE => next-step auto-reset
 
     // ---- positions, next squares, collidability (is_collision :692-700) ----
@@ -169,12 +198,12 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         act[a] = c;
         nn80[a] = nz80(c ^ k04);
         uint32_t yw;
-        if (L.tall)  // wave-uniform: H > 8 rows
+        if (tall)  // wave-uniform: H > 8 rows
             yw = Y[a] * L.W;
         else
             yw = perm(L.yw_hi, L.yw_lo, Y[a]);
         loc[a] = yw + X[a];
-        if (L.big)  // wave-uniform: cells up to 254, loc + delta in two carry-free halves
+        if (big)  // wave-uniform: cells up to 254, loc + delta in two carry-free halves
             nraw[a] = loc[a] + perm(L.dp_hi, L.dp_lo, c) - perm(L.dn_hi, L.dn_lo, c);
         else  // cells < 128: loc + (delta + 0x80) stays in its byte, bias removed
             nraw[a] = (loc[a] + perm(L.dc_hi, L.dc_lo, c)) ^ k80;
@@ -193,7 +222,7 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
 #pragma unroll
         for (int j = i + 1; j < A; ++j, ++p) {
             uint32_t eq, sw;
-            if (L.big) {  // cell bytes reach bit 7: full-byte zero tests (no carry between envs)
+            if (big) {  // cell bytes reach bit 7: full-byte zero tests (no carry between envs)
                 eq = zf80(nxt[i] ^ nxt[j]);
                 sw = zf80(loc[i] ^ nxt[j]) & zf80(loc[j] ^ nxt[i]);
             } else {
@@ -210,6 +239,7 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
     }
 
     // ---- execute_navigation: interact per agent, in order (:767-770, interact.py:4-89) ----
+    uint32_t dlv = 0u;  // h80: some agent delivered
 #pragma unroll
     for (int k = 0; k < A; ++k) {
         const uint32_t go80 = andn(nn80[k], blk80[k]);
@@ -224,22 +254,31 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         uint32_t at80[K], seen = 0u, ob0 = 0u, ob1 = 0u, ob2 = 0u;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            at80[j] = L.big ? zf80(Lc[j] ^ tc) : eq80(Lc[j], tc);
+            at80[j] = big ? zf80(Lc[j] ^ tc) : eq80(Lc[j], tc);
             seen |= at80[j];
             if (j & 1) ob0 |= at80[j];
             if (j & 2) ob1 |= at80[j];
             if (j & 4) ob2 |= at80[j];
         }
-        const uint32_t fo1 = full80(ob1), fo2 = (K == 8) ? full80(ob2) : 0u;
-        const uint32_t om = gather<K>(M, (ob0 >> 5) | kLanes, fo1, fo2);
+        const uint32_t so1 = (ob0 >> 5) | kLanes;                            // (o & 1) * 4 + q
         const uint32_t sh = bop3<OC_LUT((a & b) | c)>(h << 2, k04, kLanes);  // (h & 1) * 4 + q
-        const uint32_t fh1 = full80((h << 6) & k80), fh2 = (K == 8) ? full80((h << 5) & k80) : 0u;
-        const uint32_t hm = gather<K>(M, sh, fh1, fh2);
-        const uint32_t hl = gather<K>(Lc, sh, fh1, fh2);
+        uint32_t om, hm, hl;
+        if constexpr (K == 4) {  // the pair select is a second v_perm on the index's bit 1
+            const uint32_t so2 = (ob1 >> 5) | kLanes, sh2 = bop3<OC_LUT(a | (b & c))>(kLanes, h << 1, k04);
+            om = perm(perm(M[3], M[2], so1), perm(M[1], M[0], so1), so2);
+            hm = perm(perm(M[3], M[2], sh), perm(M[1], M[0], sh), sh2);
+            hl = perm(perm(Lc[3], Lc[2], sh), perm(Lc[1], Lc[0], sh), sh2);
+        } else {
+            const uint32_t fo1 = full80(ob1), fo2 = full80(ob2);
+            const uint32_t fh1 = full80((h << 6) & k80), fh2 = full80((h << 5) & k80);
+            om = gather<K>(M, so1, fo1, fo2);
+            hm = gather<K>(M, sh, fh1, fh2);
+            hl = gather<K>(Lc, sh, fh1, fh2);
+        }
 
         const uint32_t nf = andn(go80, isF80), mv = go80 & isF80;
         uint32_t two, allch, plate_ok, food_ok, nch, cu, chopped;
-        if (L.counts) {  // wave-uniform: OC_ENC_COUNTS masks (T/L/O 2-bit counts, 0x40 Plate, 0x80 Fresh)
+        if (counts) {  // wave-uniform: OC_ENC_COUNTS masks (T/L/O 2-bit counts, 0x40 Plate, 0x80 Fresh)
             const uint32_t x = hm & k7F;
             // >= 2 contents: the count bits are not a single unit (0x01, 0x04, 0x10, 0x40) nor zero;
             // ((x | 0x80) - 1) & x clears the lowest set bit without a borrow into the next env
@@ -273,11 +312,13 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         const uint32_t put = andn(empty, chop);
         const uint32_t pick = andn(bop3<OC_LUT(a & !b & c)>(nf, hold80, seen), isD80);  // :73-84
         const uint32_t reloc = or3(mv, deliver, put);  // the held item ends on tc
+        dlv |= deliver;
 
-        // SimAgent.move_to (agent.py:420-423)
-        const uint32_t fmv = full80(mv);
-        X[k] = sel(fmv, X[k] + perm(kDXhi, kDXlo, act[k]) - k01, X[k]);
-        Y[k] = sel(fmv, Y[k] + perm(kDYhi, kDYlo, act[k]) - k01, Y[k]);
+        // SimAgent.move_to (agent.py:420-423): an env that does not move reads its action code
+        // as 4..7 (act | 4), whose delta is (0, 0) (each byte stays >= 1 before the - 1)
+        const uint32_t amv = bop3<OC_LUT(a | ((!b) & c))>(act[k], mv >> 5, k04);
+        X[k] = X[k] + perm(kDXhi, kDXlo, amv) - k01;
+        Y[k] = Y[k] + perm(kDYhi, kDYlo, amv) - k01;
         // new values of the target slot o and the held slot h
         const uint32_t fmg = full80(merge), fpk = full80(pick);
         const uint32_t newOl = fmg | sel(fpk, loc[k], tc);  // merged away: dead (0xFF)
@@ -327,10 +368,18 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         const uint32_t z1 = andn(0x80008000u, ((d1 & 0x7FFF7FFFu) + 0x7FFF7FFFu) | d1);
         tout = perm(z1, z0, 0x07050301u);  // high byte of each u16 half -> env byte
     }
+    if (!any_of(or3(rst, tout | err, dlv | pending))) {  // wave-uniform: no rare event
+        T0 = __builtin_bit_cast(uint32_t, t0);
+        T1 = __builtin_bit_cast(uint32_t, t1);
+        F = 0u;
+        CM = cm;
+        return false;
+    }
+    pending = 0u;
     uint32_t ok = k80;
     for (int g = 0; g < L.ngoals; ++g) {  // every Deliver goal: an item == goal at the delivery cell
         uint32_t hit = 0u;
-        if (L.big) {  // masks are < 0x80, so bit 7 of the OR comes from the cell compare only
+        if (big) {  // masks are < 0x80, so bit 7 of the OR comes from the cell compare only
 #pragma unroll
             for (int j = 0; j < K; ++j) hit |= zf80((Lc[j] ^ L.done_rep) | (M[j] ^ L.goals_rep[g]));
         } else {
@@ -361,6 +410,16 @@ OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
     T1 = andn(__builtin_bit_cast(uint32_t, t1), perm(rst, rst, 0x03030202u));
     F = andn(fl, rst);
     CM = andn(cm, rst);
+    return true;
+}
+
+// The step without the rare-event split (every wave takes the full path).
+template <int A, int K, class ClassOf>
+OC_SW void step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_t (&H)[A],
+                 uint32_t (&Lc)[K], uint32_t (&M)[K], uint32_t& T0, uint32_t& T1, uint32_t& F,
+                 const uint32_t (&ACT)[A], uint32_t (&EX)[A], uint32_t& CM, ClassOf cls_of) {
+    uint32_t pending = kFF;
+    step4<A, K>(L, X, Y, H, Lc, M, T0, T1, F, ACT, EX, CM, cls_of, [](uint32_t) { return true; }, pending);
 }
 
 }  // namespace ocsw

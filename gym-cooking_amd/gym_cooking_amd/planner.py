@@ -108,8 +108,20 @@ _COST = {c: _cost(c) for n in (1, 2) for c in _CAND[n]}
 def argmin(vector, rng=np.random):
     """e2e_brtdp.py:27-30: the index of a minimum, ties broken by numpy's global generator
     (one ``multinomial`` draw per call, ties or not).  `rng` is the module ``np.random`` (the
-    reference's generator) or a ``np.random.RandomState`` of a batched search."""
-    e_x = np.array(vector) == min(vector)
+    reference's generator) or a ``np.random.RandomState`` of a batched search.
+
+    A unique minimum is answered without the multinomial, consuming what it would: the legacy
+    multinomial(1, one-hot at i) draws binomial(1, 0) -> 0 with no variate for every entry
+    before i, then binomial(1, 1.0) = 1 - binomial-inversion(1, 0.0), which reads one uniform
+    double; at the last index it draws nothing (numpy's legacy distributions, mtrand
+    multinomial; checked against multinomial itself in tests/test_planner_host.py)."""
+    m = min(vector)
+    i = vector.index(m) if isinstance(vector, list) else int(np.argmin(vector))
+    if vector.count(m) == 1 if isinstance(vector, list) else (np.asarray(vector) == m).sum() == 1:
+        if i != len(vector) - 1:
+            rng.random_sample()
+        return i
+    e_x = np.array(vector) == m
     return np.where(rng.multinomial(1, e_x / e_x.sum()))[0][0]
 
 
@@ -433,8 +445,9 @@ class E2E_BRTDP:
         actions, succ, goals, lbs = [], [], [], []
         illegal = {}
         crash = None
+        fl, lb = fl.tolist(), lb.tolist()  # Python ints / floats (the f32 bounds exactly)
         for r, c in enumerate(cand):
-            f = int(fl[r])
+            f = fl[r]
             if not f & capi.ROLL_LEGAL:
                 illegal[c] = r
                 continue
@@ -452,12 +465,15 @@ class E2E_BRTDP:
             actions.append(c)
             succ.append(nk)
             goals.append(bool(f & capi.ROLL_GOAL))
-            lbs.append(float(lb[r]))
+            lbs.append(lb[r])
         # T's value_init of a successor runs when T is first asked for it (e2e_brtdp.py:145-148):
         # all of them by _init_succ on the first full Q pass, one by T / _expected_diff before
-        # that, so that value tables shared between planners fill in the reference's order
-        self._succ[(key, sk)] = [actions, succ, [_COST[c] for c in actions],
-                                 [(self._repr(nk), sk) for nk in succ], goals, lbs, False, crash]
+        # that, so that value tables shared between planners fill in the reference's order.
+        # [actions, successor keys, costs, successor value keys, goal flags, bounds,
+        #  successors initialised, copy-crash action indices, this state's value key]
+        rep = self._repr
+        self._succ[(key, sk)] = [actions, succ, [_COST[c] for c in actions], [(rep(nk), sk) for nk in succ],
+                                 goals, lbs, False, crash, (rep(key), sk)]
         if illegal:  # what T would do with them (only asked for by taken_action_error)
             self._illegal[(key, sk)] = {c: (raw[r * NP:(r + 1) * NP], int(fl[r])) for c, r in illegal.items()}
 
@@ -545,7 +561,7 @@ class E2E_BRTDP:
         got = self._succ[(key, self._sub_key)]
         if not got[6]:
             self._init_succ(got)
-        return [float(c + 1.0 * value_f[vk]) for c, vk in zip(got[2], got[3])]
+        return [c + value_f[vk] for c, vk in zip(got[2], got[3])]  # floats: c + 1.0 * v, exactly
 
     def _expected_diff(self, key, action):  # get_expected_diff, e2e_brtdp.py:828-840
         got = self._succ[(key, self._sub_key)]
@@ -559,38 +575,45 @@ class E2E_BRTDP:
 
     # ---- search (e2e_brtdp.py:208-331, 842-878), as generators --------------------------------
     def _sample_trial(self):  # runSampleTrial
+        """runSampleTrial; _q_all / _expected_diff / _need inlined (the same float64 operations
+        in the same order)."""
         x = self.start
         traj = []
         counter = 0
         sk = self._sub_key
+        succ, v_u, v_l, rng, lvl = self._succ, self.v_u, self.v_l, self._rng, self._level
+        rs = (self._repr(self.start), sk)
         while True:
             counter += 1
             if counter > self.cap:
                 break
             traj.append(x)
-            yield from self._modified_state(x)
-            yield from self._need(x)
-            actions = self._succ[(x, sk)][0]
-            new_upper = min(self._q_all(x, self.v_u))
-            rx = (self._repr(x), sk)
-            self.v_u[rx] = new_upper
-            ql = self._q_all(x, self.v_l)
-            action_index = argmin(ql, self._rng)
-            a = actions[action_index]
-            new_lower = ql[action_index]  # = Q(x, a, v_l): that table did not change since
-            self.v_l[rx] = new_lower
-            b = self._expected_diff(x, a)
-            B = sum(b.values())
-            rs = (self._repr(self.start), sk)
-            diff = (self.v_u[rs] - self.v_l[rs]) / self.tau
+            if lvl:
+                yield from self._modified_state(x)
+            if (x, sk) not in succ:
+                yield from self._need(x)
+            got = succ[(x, sk)]
+            if not got[6]:
+                self._init_succ(got)
+            costs, vks, rx = got[2], got[3], got[8]
+            v_u[rx] = min([c + v_u[vk] for c, vk in zip(costs, vks)])
+            ql = [c + v_l[vk] for c, vk in zip(costs, vks)]
+            i = argmin(ql, rng)
+            v_l[rx] = ql[i]  # = Q(x, a, v_l): that table did not change since
+            if got[7] and i in got[7]:  # get_expected_diff's T raises
+                _raise_copy_crash(got[0][i])
+            vk = vks[i]
+            B = v_u[vk] - v_l[vk]
+            diff = (v_u[rs] - v_l[rs]) / self.tau
             if B <= diff:
                 break
-            x = list(b.keys())[0]
+            x = got[1][i]
         while traj:
             x = traj.pop()
-            rx = (self._repr(x), sk)
-            self.v_u[rx] = min(self._q_all(x, self.v_u))
-            self.v_l[rx] = min(self._q_all(x, self.v_l))
+            got = succ[(x, sk)]
+            costs, vks, rx = got[2], got[3], got[8]
+            v_u[rx] = min([c + v_u[vk] for c, vk in zip(costs, vks)])
+            v_l[rx] = min([c + v_l[vk] for c, vk in zip(costs, vks)])
 
     def _main(self):  # main
         main_counter = 0

@@ -34,9 +34,13 @@ static inline uint32_t host_bitop3(uint32_t a, uint32_t b, uint32_t c, uint32_t 
 #include "../../gym-cooking_amd/csrc/oc_swar.h"
 #include "../../include/oc_engine.h"
 
+// n steps per call with the state kept between steps (what oc_step_n_kernel does per lane):
+// the loaded state is `pending` once, later steps take the rare-event split on their own
+// (any_of tests this lane's 4 envs).  n = 1 is one oc_step.  Outputs of step r go to
+// sout + r * NP * P, exo + r * A * P, coll + r * P.
 template <int A, int K>
 static void run(const oc_level_desc* lv, int max_T, const uint8_t* sin, uint8_t* sout, const uint8_t* act,
-                uint8_t* exo, uint8_t* coll, int64_t B, int64_t P) {
+                uint8_t* exo, uint8_t* coll, int64_t B, int64_t P, int n = 1) {
     const int W = lv->width, H = lv->height;
     int done_cell = -1;
     uint8_t tbl[256] = {0};
@@ -63,14 +67,33 @@ static void run(const oc_level_desc* lv, int max_T, const uint8_t* sin, uint8_t*
         memcpy(&T0, sin + pt * P + 8 * g, 4);
         memcpy(&T1, sin + pt * P + 8 * g + 4, 4);
         F = rd(sin, pt + 2, g);
-        ocsw::step4<A, K>(S, X, Y, Hh, Lc, M, T0, T1, F, AC, EX, CM, cls_of);
-        for (int a = 0; a < A; ++a) { wr(sout, a, g, X[a]); wr(sout, A + a, g, Y[a]); wr(sout, 2 * A + a, g, Hh[a]); if (exo) wr(exo, a, g, EX[a]); }
-        for (int j = 0; j < K; ++j) { wr(sout, 3 * A + j, g, Lc[j]); wr(sout, 3 * A + K + j, g, M[j]); }
-        memcpy(sout + pt * P + 8 * g, &T0, 4);
-        memcpy(sout + pt * P + 8 * g + 4, &T1, 4);
-        wr(sout, pt + 2, g, F);
-        if (coll) memcpy(coll + 4 * g, &CM, 4);
+        uint32_t pending = ocsw::at_done80<K, 1>(S, Lc);
+        const int64_t NP = pt + 3;
+        for (int r = 0; r < n; ++r) {
+            for (int a = 0; a < A; ++a) AC[a] = rd(act + (int64_t)r * A * P, a, g);
+            // the device's dispatch: 4-slot levels of the common class take the MODE 0 build
+            if (K == 4 && !S.tall && !S.big && !S.counts)
+                ocsw::step4<A, K, 0>(S, X, Y, Hh, Lc, M, T0, T1, F, AC, EX, CM, cls_of,
+                                     [](uint32_t v) { return v != 0u; }, pending);
+            else
+                ocsw::step4<A, K, 1>(S, X, Y, Hh, Lc, M, T0, T1, F, AC, EX, CM, cls_of,
+                                     [](uint32_t v) { return v != 0u; }, pending);
+            uint8_t* so = sout + (int64_t)r * NP * P;
+            for (int a = 0; a < A; ++a) { wr(so, a, g, X[a]); wr(so, A + a, g, Y[a]); wr(so, 2 * A + a, g, Hh[a]); if (exo) wr(exo + (int64_t)r * A * P, a, g, EX[a]); }
+            for (int j = 0; j < K; ++j) { wr(so, 3 * A + j, g, Lc[j]); wr(so, 3 * A + K + j, g, M[j]); }
+            memcpy(so + pt * P + 8 * g, &T0, 4);
+            memcpy(so + pt * P + 8 * g + 4, &T1, 4);
+            wr(so, pt + 2, g, F);
+            if (coll) memcpy(coll + (int64_t)r * P + 4 * g, &CM, 4);
+        }
     }
+}
+
+extern "C" int swar_host_step_n(const oc_level_desc* lv, int A, int K, int max_T, const uint8_t* sin, uint8_t* traj,
+                                const uint8_t* act, uint8_t* exo, uint8_t* coll, int64_t B, int64_t P, int n) {
+#define RN(a, k) if (A == a && K == k) { run<a, k>(lv, max_T, sin, traj, act, exo, coll, B, P, n); return 0; }
+    RN(1, 4) RN(2, 4) RN(3, 4) RN(4, 4) RN(1, 8) RN(2, 8) RN(3, 8) RN(4, 8)
+    return -1;
 }
 
 extern "C" int swar_host_step(const oc_level_desc* lv, int A, int K, int max_T, const uint8_t* sin, uint8_t* sout,

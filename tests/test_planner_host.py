@@ -221,3 +221,33 @@ def test_host_planner_level1_matches_reference_calls():
             errs.append("call %d (%s, others %s): got %s want %s" % (i, c["subtask"], c["others"], got, want))
     assert fx["calls"]
     assert not errs, "%d of %d calls differ:\n%s" % (len(errs), len(fx["calls"]), "\n".join(errs[:10]))
+
+
+def test_argmin_matches_multinomial_draws():
+    """planner.argmin answers a unique minimum without numpy's multinomial but consumes the
+    generator exactly as it (one uniform double unless the minimum is the last entry): same
+    index and same generator state as the reference's formula (e2e_brtdp.py:27-30), with and
+    without ties, on a RandomState and on the global generator."""
+    from gym_cooking_amd.planner import argmin
+
+    def ref(vector, rng):
+        e_x = np.array(vector) == min(vector)
+        return np.where(rng.multinomial(1, e_x / e_x.sum()))[0][0]
+
+    gen = np.random.default_rng(0)
+    for trial in range(3000):
+        n = int(gen.integers(1, 26))
+        v = [float(x) for x in gen.integers(0, 4 if trial % 2 else 50, n) * 0.5]
+        r1, r2 = np.random.RandomState(trial), np.random.RandomState(trial)
+        r1.random_sample(int(gen.integers(0, 700)))
+        r2.set_state(r1.get_state())
+        assert argmin(v, r1) == ref(v, r2)
+        s1, s2 = r1.get_state(), r2.get_state()
+        assert s1[2] == s2[2] and np.array_equal(s1[1], s2[1])
+    np.random.seed(7)
+    a = [argmin([1.0, 0.5, 2.0, 0.5][:k], np.random) for k in (1, 2, 3, 4)]
+    np.random.seed(7)
+    b = [ref([1.0, 0.5, 2.0, 0.5][:k], np.random) for k in (1, 2, 3, 4)]
+    assert a == b and np.random.random_sample() == (np.random.seed(7), [ref([1.0, 0.5, 2.0, 0.5][:k], np.random)
+                                                                        for k in (1, 2, 3, 4)],
+                                                    np.random.random_sample())[2]

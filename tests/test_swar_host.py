@@ -113,3 +113,78 @@ def test_swar_invalid_action_codes():
         sb.step(s, o2, act)
         assert np.array_equal(tl.env_view(o1, 2, 4, ob.pitch, B), tl.env_view(o2, 2, 4, ob.pitch, B))
         s = o1
+
+
+def _step_n_host(sb, s, acts, n):
+    """swar_host_step_n: n steps per lane with the state kept between steps (oc_step_n's lane
+    loop: the loaded state takes the full path once, then the rare-event split decides)."""
+    L = _load()
+    if not hasattr(L, "_sn"):
+        vp = ctypes.c_void_p
+        L.swar_host_step_n.restype = ctypes.c_int
+        L.swar_host_step_n.argtypes = [ctypes.POINTER(capi.OcLevelDesc), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       vp, vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
+        L._sn = True
+    S = s.size
+    traj = np.zeros(n * S, np.uint8)
+    ex = np.zeros(n * sb.A * sb.pitch, np.uint8)
+    coll = np.zeros(n * sb.pitch, np.uint8)
+    rc = L.swar_host_step_n(ctypes.byref(sb.desc), sb.A, sb.K, sb.max_T, _p(s), _p(traj), _p(acts), _p(ex), _p(coll),
+                            sb.B, sb.pitch, n)
+    assert rc == 0
+    return traj.reshape(n, S), ex.reshape(n, sb.A, sb.pitch), coll.reshape(n, sb.pitch)
+
+
+@pytest.mark.parametrize("level,A,max_T", [("partial-divider_salad", 2, 30), ("full-divider_tl", 3, 45),
+                                           ("open-divider_salad", 4, 25), ("open-divider_tl", 2, 0),
+                                           ("levels/dup-12x12_salad3t.txt", 3, 40)])
+def test_swar_step_n_rare_event_split_matches_oracle(level, A, max_T):
+    """The rare-event split over long multi-step runs (resets at max_T, goal-directed-ish play
+    from the reference fixtures' states, deliveries), every step against the oracle."""
+    _load()
+    B, n = 2003, 120
+    lv = tl.load_level(level)
+    ob = oracle.OracleBatch(lv, A, max_T, B)
+    sb = SwarHostBatch(lv, A, max_T, B)
+    s = ob.new_state()
+    ob.reset(s)
+    acts = np.zeros(n * A * ob.pitch, np.uint8)
+    a1 = ob.new_actions()
+    for t in range(n):
+        ob.gen_actions(a1, 0, t, 5 + A)
+        acts[t * A * ob.pitch:(t + 1) * A * ob.pitch] = a1
+    traj, ex, coll = _step_n_host(sb, s, acts, n)
+    c, c2 = s.copy(), ob.new_state()
+    e1, c1 = np.zeros(A * ob.pitch, np.uint8), np.zeros(ob.pitch, np.uint8)
+    for t in range(n):
+        ob.step(c, c2, acts[t * A * ob.pitch:(t + 1) * A * ob.pitch], e1, c1)
+        c, c2 = c2, c
+        assert np.array_equal(tl.env_view(traj[t], A, ob.K, ob.pitch, B), tl.env_view(c, A, ob.K, ob.pitch, B)), t
+        assert np.array_equal(ex[t][:, :B], e1.reshape(A, -1)[:, :B]), t
+        assert np.array_equal(coll[t][:B], c1[:B]), t
+
+
+def test_swar_step_n_pending_state_with_items_on_delivery():
+    """A loaded state that already has the goal dish on the Delivery square but DONE cleared
+    (the gym shim keeps stepping a finished env, as the reference does): the first step of the
+    launch must report success again, with no delivery in that step."""
+    _load()
+    fx = tl.load_fixture("kat.npz")
+    g = next(g for g in tl.episode_groups(fx) if any(fx["flags"][fx["ep_state_off"][e] + fx["ep_T"][e]] & 2
+                                                      for e in g.idx))
+    b = next(i for i, e in enumerate(g.idx) if fx["flags"][fx["ep_state_off"][e] + fx["ep_T"][e]] & 2)
+    e = g.idx[b]
+    o = fx["ep_state_off"][e] + fx["ep_T"][e]
+    ob = oracle.OracleBatch(g.level, g.A, 0, 1)
+    sb = SwarHostBatch(g.level, g.A, 0, 1)
+    s = tl.state_from_canonical(g.level, g.A, ob.K, ob.pitch, fx["agents"][o][None], fx["items"][o][None],
+                                fx["t"][o][None])
+    acts = np.full(3 * g.A * ob.pitch, 4, np.uint8)
+    traj, _, _ = _step_n_host(sb, s, acts, 3)
+    c, c2 = s.copy(), ob.new_state()
+    for t in range(3):
+        ob.step(c, c2, acts[:g.A * ob.pitch])
+        c, c2 = c2, c
+        assert np.array_equal(tl.env_view(traj[t], g.A, ob.K, ob.pitch, 1), tl.env_view(c, g.A, ob.K, ob.pitch, 1)), t
+    fl = tl.planes_view(traj[0], g.A, ob.K, ob.pitch)["fl"][0]
+    assert (fl & 3) == 3  # done and successful again after a no-op step
