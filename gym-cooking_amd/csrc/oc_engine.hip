@@ -50,14 +50,14 @@ struct LevelArgs {
     uint32_t goals;       // up to 4 goal masks, one per byte
     int32_t ngoals;
     uint32_t tmpl_x, tmpl_y;          // spawn x / y of agents 0..3, one per byte
-    uint32_t tmpl_cell[2], tmpl_mask[2];  // item slots 0..7, one per byte
+    uint32_t tmpl_cell[4], tmpl_mask[4];  // item slots 0..15, one per byte
     int64_t pitch;
     int64_t B;
     ocsw::SwarLevel sw;  // replicated constants / LUTs of the SWAR step
 };
 
 __device__ __forceinline__ uint32_t byte_of(uint32_t w, int j) { return (w >> (8 * j)) & 0xFFu; }
-__device__ __forceinline__ uint32_t byte_of2(const uint32_t (&w)[2], int j) { return byte_of(w[j >> 2], j & 3); }
+__device__ __forceinline__ uint32_t byte_of4(const uint32_t (&w)[4], int j) { return byte_of(w[j >> 2], j & 3); }
 
 // Statistics partial sums, one row of OC_NSTATS uint64 per block.  Wave sum over DPP (VALU
 // lane moves, no LDS round trips): an inclusive scan inside each 16-lane row (row_shr 1, 2,
@@ -469,9 +469,9 @@ __device__ __forceinline__ void stage_roll_tables(const RollArgs& R, const uint8
 }
 
 template <int A, int K>
-__device__ __forceinline__ ocro::Row load_row(const uint8_t* __restrict__ sin, int64_t P, int64_t e) {
+__device__ __forceinline__ ocro::RowT<K> load_row(const uint8_t* __restrict__ sin, int64_t P, int64_t e) {
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
-    ocro::Row r;
+    ocro::RowT<K> r;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
         r.x |= (uint32_t)sin[a * P + e] << (8 * a);
@@ -480,8 +480,8 @@ __device__ __forceinline__ ocro::Row load_row(const uint8_t* __restrict__ sin, i
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        r.loc |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
-        r.mask |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
+        r.loc[j >> 3] |= (uint64_t)sin[(kPL + j) * P + e] << (8 * (j & 7));
+        r.mask[j >> 3] |= (uint64_t)sin[(kPM + j) * P + e] << (8 * (j & 7));
     }
     return r;
 }
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
     const int64_t P = R.pitch;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-        ocro::Row r = load_row<A, K>(sin, P, e);
+        ocro::RowT<K> r = load_row<A, K>(sin, P, e);
         const uint16_t t = ((const uint16_t*)(sin + kPT * P))[e];
         const uint8_t fl_in = sin[kPF * P + e];
         const int ai = alloc != nullptr ? alloc[e] : 0;
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
         int f = OC_LIK_BADALLOC;
         if (ai < R.nsub) {
             const ocro::Sub& s = subs[ai];
-            ocro::Row r = load_row<A, K>(sin, P, e);
+            ocro::RowT<K> r = load_row<A, K>(sin, P, e);
             uint32_t taken = 0;
 #pragma unroll
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
@@ -682,7 +682,7 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
     const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-        const ocro::Row r = load_row<A, K>(sin, P, e);
+        const ocro::RowT<K> r = load_row<A, K>(sin, P, e);
         ocro::RowOps<A, K> ops(R.L, blob);
         const int i0 = (int)(blockIdx.y * R.nsub / gridDim.y), i1 = (int)((blockIdx.y + 1) * R.nsub / gridDim.y);
         for (int i = i0; i < i1; ++i) {
@@ -933,8 +933,8 @@ __global__ __launch_bounds__(kBlock) void oc_reset_kernel(LevelArgs L, uint8_t* 
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        st32(3 * A + j, rep(byte_of2(L.tmpl_cell, j)));
-        st32(3 * A + K + j, rep(byte_of2(L.tmpl_mask, j)));
+        st32(3 * A + j, rep(byte_of4(L.tmpl_cell, j)));
+        st32(3 * A + K + j, rep(byte_of4(L.tmpl_mask, j)));
     }
     *reinterpret_cast<uint2*>(s + (3 * A + 2 * K) * P + 2 * e0) = make_uint2(0u, 0u);
     st32(3 * A + 2 * K + 2, 0u);
@@ -1096,9 +1096,9 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     const bool counts = lv->encoding == OC_ENC_COUNTS;
     uint32_t seen_food = 0;
     int per_food[3] = {0, 0, 0};
-    const int K = lv->num_items <= 4 ? 4 : 8;
-    uint8_t cell[8], mask[8];
-    for (int j = 0; j < 8; ++j) {
+    const int K = lv->num_items <= 4 ? 4 : (lv->num_items <= 8 ? 8 : 16);
+    uint8_t cell[16], mask[16];
+    for (int j = 0; j < 16; ++j) {
         cell[j] = OC_LOC_DEAD;
         mask[j] = 0;
     }
@@ -1127,7 +1127,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
         L.tmpl_x |= (uint32_t)x << (8 * a);
         L.tmpl_y |= (uint32_t)y << (8 * a);
     }
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 16; ++j) {
         L.tmpl_cell[j >> 2] |= (uint32_t)cell[j] << (8 * (j & 3));
         L.tmpl_mask[j >> 2] |= (uint32_t)mask[j] << (8 * (j & 3));
     }
@@ -1217,7 +1217,7 @@ int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
 }
 
 #define OC_DISPATCH(A_, K_, LAUNCH)                                                         \
-    switch ((A_) * 10 + (K_)) {                                                             \
+    switch ((A_) * ((K_) >= 10 ? 100 : 10) + (K_)) {                                        \
         case 14: LAUNCH(1, 4); break;                                                       \
         case 24: LAUNCH(2, 4); break;                                                       \
         case 34: LAUNCH(3, 4); break;                                                       \
@@ -1226,6 +1226,10 @@ int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
         case 28: LAUNCH(2, 8); break;                                                       \
         case 38: LAUNCH(3, 8); break;                                                       \
         case 48: LAUNCH(4, 8); break;                                                       \
+        case 116: LAUNCH(1, 16); break;                                                     \
+        case 216: LAUNCH(2, 16); break;                                                     \
+        case 316: LAUNCH(3, 16); break;                                                     \
+        case 416: LAUNCH(4, 16); break;                                                     \
         default: return fail(OC_EINVAL, "unsupported (A,K)=(%d,%d)", (A_), (K_));           \
     }
 
@@ -1241,7 +1245,7 @@ int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
             default: return fail(OC_EINVAL, "unsupported A=%d", (h_)->A);                   \
         }                                                                                   \
     } else {                                                                                \
-        switch ((h_)->A * 10 + (h_)->K) {                                                   \
+        switch ((h_)->A * ((h_)->K >= 10 ? 100 : 10) + (h_)->K) {                           \
             case 14: LAUNCH(1, 4, 1); break;                                                \
             case 24: LAUNCH(2, 4, 1); break;                                                \
             case 34: LAUNCH(3, 4, 1); break;                                                \
@@ -1250,6 +1254,10 @@ int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
             case 28: LAUNCH(2, 8, 1); break;                                                \
             case 38: LAUNCH(3, 8, 1); break;                                                \
             case 48: LAUNCH(4, 8, 1); break;                                                \
+            case 116: LAUNCH(1, 16, 1); break;                                              \
+            case 216: LAUNCH(2, 16, 1); break;                                              \
+            case 316: LAUNCH(3, 16, 1); break;                                              \
+            case 416: LAUNCH(4, 16, 1); break;                                              \
             default: return fail(OC_EINVAL, "unsupported (A,K)=(%d,%d)", (h_)->A, (h_)->K); \
         }                                                                                   \
     }

@@ -61,21 +61,47 @@ struct Sub {  // oc_subtask, device copy
 };
 
 // One row's state, packed so that run-time slot / agent indices are shifts, not memory:
-// agent a in byte a of x, y, h (h = held slot or kNone); slot j in byte j of loc, mask.
-struct Row {
+// agent a in byte a of x, y, h (h = held slot or kNone); slot j in byte j % 8 of word j / 8 of
+// loc, mask (one word for K <= 8, two for K = 16; a run-time j picks the word with a select).
+template <int K>
+struct RowT {
+    static constexpr int NW = (K + 7) / 8;
     uint32_t x = 0, y = 0, h = 0;
-    uint64_t loc = 0, mask = 0;
+    uint64_t loc[NW] = {}, mask[NW] = {};
     static OC_RH uint32_t b32(uint32_t w, int i) { return (w >> (8 * i)) & 0xFFu; }
     static OC_RH uint32_t b64(uint64_t w, int i) { return (uint32_t)(w >> (8 * i)) & 0xFFu; }
     static OC_RH void s32(uint32_t& w, int i, uint32_t v) { w = (w & ~(0xFFu << (8 * i))) | (v << (8 * i)); }
     static OC_RH void s64(uint64_t& w, int i, uint32_t v) {
         w = (w & ~(0xFFull << (8 * i))) | ((uint64_t)v << (8 * i));
     }
+    static OC_RH uint64_t word(const uint64_t (&w)[NW], int j) {
+        if constexpr (NW == 1) {
+            return w[0];
+        } else {
+            uint64_t w0 = w[0], w1 = w[1];
+#if defined(__HIP_DEVICE_COMPILE__)
+            // keep the select on register values: folded into a select of addresses it turns
+            // the two words into a scratch array with a run-time offset
+            asm("" : "+v"(w0), "+v"(w1));
+#endif
+            return j < 8 ? w0 : w1;
+        }
+    }
+    static OC_RH void set(uint64_t (&w)[NW], int j, uint32_t v) {
+        if constexpr (NW == 1) {
+            s64(w[0], j, v);
+        } else {
+            if (j < 8) s64(w[0], j, v);
+            else s64(w[1], j - 8, v);
+        }
+    }
     OC_RH int ax(int a) const { return (int)b32(x, a); }
     OC_RH int ay(int a) const { return (int)b32(y, a); }
     OC_RH int ah(int a) const { return (int)b32(h, a); }
-    OC_RH int il(int j) const { return (int)b64(loc, j); }
-    OC_RH int im(int j) const { return (int)b64(mask, j); }
+    OC_RH int il(int j) const { return (int)b64(word(loc, j), j & 7); }
+    OC_RH int im(int j) const { return (int)b64(word(mask, j), j & 7); }
+    OC_RH void set_loc(int j, uint32_t v) { set(loc, j, v); }
+    OC_RH void set_mask(int j, uint32_t v) { set(mask, j, v); }
 };
 
 // byte v occurs in one of the four bytes of w
@@ -189,6 +215,7 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
 // ---- row logic ----------------------------------------------------------------------------
 template <int A, int K>
 struct RowOps {
+    using Row = RowT<K>;
     const RollLevel& L;
     const uint8_t* T;       // the level's table blob (LDS on the device)
     uint32_t ac = 0xFFFFFFFFu;  // AgentCounter cells of this row's Level-0 view, one per byte (0xFF none)
@@ -219,8 +246,8 @@ struct RowOps {
             if ((active >> a) & 1u) continue;
             const int hh = r.ah(a);
             if (hh != kNone) {
-                Row::s64(r.loc, hh, kNone);
-                Row::s64(r.mask, hh, 0);
+                r.set_loc(hh, kNone);
+                r.set_mask(hh, 0);
                 Row::s32(r.h, a, kNone);
             }
             const uint32_t c = (uint32_t)agent_cell(r, a);
@@ -268,26 +295,26 @@ struct RowOps {
         if (t == kFloor) {  // move_to: the held item follows
             Row::s32(r.x, a, (uint32_t)tx);
             Row::s32(r.y, a, (uint32_t)ty);
-            if (h != kNone) Row::s64(r.loc, h, (uint32_t)tc);
+            if (h != kNone) r.set_loc(h, (uint32_t)tc);
         } else if (h != kNone) {
             const int hm = r.im(h);
             if (t == kDelivery) {
                 if (deliverable(hm)) {
-                    Row::s64(r.loc, h, (uint32_t)tc);
+                    r.set_loc(h, (uint32_t)tc);
                     Row::s32(r.h, a, kNone);
                 }
             } else {
                 const int o = item_at(r, tc);
                 if (o >= 0) {
                     if (mergeable(hm, r.im(o))) {  // the holder's item absorbs o
-                        Row::s64(r.mask, h, (uint32_t)merged(hm, r.im(o)));
-                        Row::s64(r.loc, o, kNone);
-                        Row::s64(r.mask, o, 0);
+                        r.set_mask(h, (uint32_t)merged(hm, r.im(o)));
+                        r.set_loc(o, kNone);
+                        r.set_mask(o, 0);
                     }
                 } else if (t == kCutboard && needs_chopped(hm)) {
-                    Row::s64(r.mask, h, (uint32_t)chopped(hm));
+                    r.set_mask(h, (uint32_t)chopped(hm));
                 } else {  // put down
-                    Row::s64(r.loc, h, (uint32_t)tc);
+                    r.set_loc(h, (uint32_t)tc);
                     Row::s32(r.h, a, kNone);
                 }
             }
@@ -295,7 +322,7 @@ struct RowOps {
             const int o = item_at(r, tc);
             if (o >= 0) {  // pick up: the item moves onto the agent
                 Row::s32(r.h, a, (uint32_t)o);
-                Row::s64(r.loc, o, (uint32_t)agent_cell(r, a));
+                r.set_loc(o, (uint32_t)agent_cell(r, a));
             }
         }
     }

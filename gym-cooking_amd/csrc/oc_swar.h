@@ -72,7 +72,7 @@ struct SwarLevel {
     uint32_t goals_rep[4];   // Deliver goal masks, replicated
     int32_t ngoals;
     uint32_t maxT_rep;       // max_T replicated to both u16 halves (0 = no limit)
-    uint32_t tmpl_x[4], tmpl_y[4], tmpl_l[8], tmpl_m[8];  // reset template, replicated
+    uint32_t tmpl_x[4], tmpl_y[4], tmpl_l[16], tmpl_m[16];  // reset template, replicated
     int32_t tall;            // H > 8: y*W by multiply instead of the 8-entry LUT
     int32_t big;             // W*H > 128: cell ids reach bit 7, so cell compares use all 8 bits
                              // and the move delta is added as (positive part) - (negative part)
@@ -120,7 +120,7 @@ __host__ __device__ inline void build_swar_level(SwarLevel& S, int W, int H, int
         S.tmpl_x[a] = (uint32_t)(a < num_agents ? spawn_x[a] : 0) * 0x01010101u;
         S.tmpl_y[a] = (uint32_t)(a < num_agents ? spawn_y[a] : 0) * 0x01010101u;
     }
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 16; ++j) {  // cell / mask: 16 slots (OC_LOC_DEAD / 0 past the level's items)
         S.tmpl_l[j] = (uint32_t)cell[j] * 0x01010101u;
         S.tmpl_m[j] = (uint32_t)mask[j] * 0x01010101u;
     }
@@ -136,18 +136,28 @@ __host__ __device__ inline uint8_t tile_class(int tile) {
 constexpr uint32_t kDXlo = 0x02000101u, kDXhi = 0x01010101u;  // codes 0..3 | 4..7
 constexpr uint32_t kDYlo = 0x01010002u, kDYhi = 0x01010101u;
 
-// Gather V[idx] per byte lane from K slot words; idx bits given as h80 masks b0, b1, b2.
+// Gather V[idx] per byte lane from K slot words; idx bits 1, 2, 3 given as full masks f1, f2, f3.
 template <int K>
-OC_SW uint32_t gather(const uint32_t (&V)[K], uint32_t s, uint32_t f1, uint32_t f2) {
+OC_SW uint32_t gather(const uint32_t (&V)[K], uint32_t s, uint32_t f1, uint32_t f2, uint32_t f3 = 0u) {
     // s: v_perm selector picking byte q of the even (bit0 = 0) or odd slot of a pair
     const uint32_t g01 = perm(V[1], V[0], s), g23 = perm(V[3], V[2], s);
     const uint32_t lo = sel(f1, g23, g01);
     if constexpr (K == 4) {
         (void)f2;
+        (void)f3;
         return lo;
     } else {
         const uint32_t g45 = perm(V[5], V[4], s), g67 = perm(V[7], V[6], s);
-        return sel(f2, sel(f1, g67, g45), lo);
+        const uint32_t lo8 = sel(f2, sel(f1, g67, g45), lo);
+        if constexpr (K == 8) {
+            (void)f3;
+            return lo8;
+        } else {
+            const uint32_t g89 = perm(V[9], V[8], s), gAB = perm(V[11], V[10], s);
+            const uint32_t gCD = perm(V[13], V[12], s), gEF = perm(V[15], V[14], s);
+            const uint32_t hi8 = sel(f2, sel(f1, gEF, gCD), sel(f1, gAB, g89));
+            return sel(f3, hi8, lo8);
+        }
     }
 }
 
@@ -251,7 +261,7 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         const uint32_t h = H[k];
         const uint32_t hold80 = andn(k80, h);  // slot index < 0x80, none = 0xFF
         // un-held items at tc (a non-Delivery cell holds at most one; held items sit on Floor)
-        uint32_t at80[K], seen = 0u, ob0 = 0u, ob1 = 0u, ob2 = 0u;
+        uint32_t at80[K], seen = 0u, ob0 = 0u, ob1 = 0u, ob2 = 0u, ob3 = 0u;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             at80[j] = big ? zf80(Lc[j] ^ tc) : eq80(Lc[j], tc);
@@ -259,6 +269,7 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
             if (j & 1) ob0 |= at80[j];
             if (j & 2) ob1 |= at80[j];
             if (j & 4) ob2 |= at80[j];
+            if (j & 8) ob3 |= at80[j];
         }
         const uint32_t so1 = (ob0 >> 5) | kLanes;                            // (o & 1) * 4 + q
         const uint32_t sh = bop3<OC_LUT((a & b) | c)>(h << 2, k04, kLanes);  // (h & 1) * 4 + q
@@ -269,11 +280,12 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
             hm = perm(perm(M[3], M[2], sh), perm(M[1], M[0], sh), sh2);
             hl = perm(perm(Lc[3], Lc[2], sh), perm(Lc[1], Lc[0], sh), sh2);
         } else {
-            const uint32_t fo1 = full80(ob1), fo2 = full80(ob2);
+            const uint32_t fo1 = full80(ob1), fo2 = full80(ob2), fo3 = K == 16 ? full80(ob3) : 0u;
             const uint32_t fh1 = full80((h << 6) & k80), fh2 = full80((h << 5) & k80);
-            om = gather<K>(M, so1, fo1, fo2);
-            hm = gather<K>(M, sh, fh1, fh2);
-            hl = gather<K>(Lc, sh, fh1, fh2);
+            const uint32_t fh3 = K == 16 ? full80((h << 4) & k80) : 0u;
+            om = gather<K>(M, so1, fo1, fo2, fo3);
+            hm = gather<K>(M, sh, fh1, fh2, fh3);
+            hl = gather<K>(Lc, sh, fh1, fh2, fh3);
         }
 
         const uint32_t nf = andn(go80, isF80), mv = go80 & isF80;
@@ -329,15 +341,27 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         // select masks are one v_perm each: selector byte = slot index (h, or the target slot
         // oidx), table byte j = 0xFF.  Envs that write no slot get selector 0x0C, which v_perm
         // turns into a zero byte (a holding-none h = 0xFF never writes: fwh includes hold80).
-        const uint32_t oidx = (ob0 >> 7) | (ob1 >> 6) | (ob2 >> 5);
+        const uint32_t oidx = (ob0 >> 7) | (ob1 >> 6) | (ob2 >> 5) | (ob3 >> 4);
         const uint32_t fwo = full80(merge | pick);
         const uint32_t fwh = full80(and3(hold80, or3(reloc, merge, chop), k80));
         const uint32_t so = sel(fwo, oidx, 0x0C0C0C0Cu), shw = sel(fwh, h, 0x0C0C0C0Cu);
+        // K = 16: slots 8..15 use the same tables on index - 8; each half's selector turns the
+        // other half's indices into 0x0C (v_perm selectors >= 8 are not byte selects)
+        uint32_t so_lo = so, shw_lo = shw, so_hi = 0x0C0C0C0Cu, shw_hi = 0x0C0C0C0Cu;
+        if constexpr (K == 16) {
+            // index bit 3 of the slots written (the no-write code 0x0C has bit 3 set too)
+            const uint32_t o8 = full80(and3(oidx << 4, k80, fwo)), h8 = full80(and3(h << 4, k80, fwh));
+            so_lo = sel(o8, 0x0C0C0C0Cu, so);
+            shw_lo = sel(h8, 0x0C0C0C0Cu, shw);
+            so_hi = sel(o8, oidx ^ 0x08080808u, 0x0C0C0C0Cu);
+            shw_hi = sel(h8, h ^ 0x08080808u, 0x0C0C0C0Cu);
+        }
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const uint32_t lut_lo = j < 4 ? 0xFFu << (8 * j) : 0u, lut_hi = j < 4 ? 0u : 0xFFu << (8 * (j - 4));
-            const uint32_t eo = perm(lut_hi, lut_lo, so);
-            const uint32_t eh = perm(lut_hi, lut_lo, shw);
+            const int jj = j & 7;
+            const uint32_t lut_lo = jj < 4 ? 0xFFu << (8 * jj) : 0u, lut_hi = jj < 4 ? 0u : 0xFFu << (8 * (jj - 4));
+            const uint32_t eo = perm(lut_hi, lut_lo, j < 8 ? so_lo : so_hi);
+            const uint32_t eh = perm(lut_hi, lut_lo, j < 8 ? shw_lo : shw_hi);
             Lc[j] = sel(eh, newHl, sel(eo, newOl, Lc[j]));
             M[j] = sel(eh, newHm, sel(eo, newOm, M[j]));
         }

@@ -15,12 +15,12 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "liboc_engine.so")
 
 OC_MAX_AGENTS = 4
-OC_MAX_ITEMS = 8
+OC_MAX_ITEMS = 16
 OC_MAX_CELLS = 255
 OC_MAX_GOALS = 4
 OC_PITCH_ALIGN = 4096
 OC_NSTATS = 5
-OC_ABI_VERSION = 4  # include/oc_engine.h
+OC_ABI_VERSION = 5  # include/oc_engine.h
 OC_EINVAL, OC_EHIP, OC_ELEVEL = -1, -2, -3
 
 OC_FLAG_DONE = 0x01
@@ -132,8 +132,9 @@ def level_desc(level: "_lv.Level", num_agents: int) -> OcLevelDesc:
 
 
 def item_slots(level: "_lv.Level") -> int:
-    """K: item slots of the state layout (level items rounded up to 4 or 8)."""
-    return 4 if len(level.items) <= 4 else 8
+    """K: item slots of the state layout (level items rounded up to 4, 8 or 16)."""
+    n = len(level.items)
+    return 4 if n <= 4 else (8 if n <= 8 else 16)
 
 
 def layout_planes(A: int, K: int) -> dict:

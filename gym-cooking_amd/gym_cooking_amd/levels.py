@@ -68,7 +68,7 @@ MAX_PER_FOOD = 3   # ENC_COUNTS: 2-bit counts
 
 # Engine limits (include/oc_engine.h).
 MAX_AGENTS = 4
-MAX_ITEMS = 8
+MAX_ITEMS = 16
 MAX_CELLS = 255
 MAX_GOALS = 4
 LOC_DEAD = 0xFF

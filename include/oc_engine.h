@@ -35,10 +35,10 @@
 extern "C" {
 #endif
 
-#define OC_ABI_VERSION 4
+#define OC_ABI_VERSION 5
 
 #define OC_MAX_AGENTS 4
-#define OC_MAX_ITEMS 8
+#define OC_MAX_ITEMS 16  /* item slots: K = 4, 8 or 16 per level */
 #define OC_MAX_CELLS 255  /* cell ids are bytes; 0xFF is OC_LOC_DEAD */
 #define OC_MAX_GOALS 4
 #define OC_PITCH_ALIGN 4096

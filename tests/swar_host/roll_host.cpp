@@ -19,15 +19,15 @@ static void run(const oc_level_desc* lv, const uint8_t* sin, uint8_t* sout, cons
     if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
     for (int64_t e = 0; e < B; ++e) {
-        ocro::Row r;
+        ocro::RowT<K> r;
         for (int a = 0; a < A; ++a) {
             r.x |= (uint32_t)sin[a * P + e] << (8 * a);
             r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
             r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
         }
         for (int j = 0; j < K; ++j) {
-            r.loc |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
-            r.mask |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
+            r.loc[j >> 3] |= (uint64_t)sin[(kPL + j) * P + e] << (8 * (j & 7));
+            r.mask[j >> 3] |= (uint64_t)sin[(kPM + j) * P + e] << (8 * (j & 7));
         }
         const int ai = alloc ? alloc[e] : 0;
         float bound = 0.0f;
@@ -70,15 +70,15 @@ static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* take
         double v = 0.0;
         int f = OC_LIK_BADALLOC;
         if (ai < nsub) {
-            ocro::Row r;
+            ocro::RowT<K> r;
             for (int a = 0; a < A; ++a) {
                 r.x |= (uint32_t)sin[a * P + e] << (8 * a);
                 r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
                 r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
             }
             for (int j = 0; j < K; ++j) {
-                r.loc |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
-                r.mask |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
+                r.loc[j >> 3] |= (uint64_t)sin[(kPL + j) * P + e] << (8 * (j & 7));
+                r.mask[j >> 3] |= (uint64_t)sin[(kPM + j) * P + e] << (8 * (j & 7));
             }
             uint32_t taken = 0;
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
@@ -98,7 +98,7 @@ extern "C" int lik_host(const oc_level_desc* lv, int A, int K, const uint8_t* si
                         double* out, uint8_t* flags, int64_t B, int64_t P) {
 #define L_(a, k) \
     if (A == a && K == k) { lik<a, k>(lv, sin, taken, alloc, subs, nsub, self_agent, beta, nap, out, flags, B, P); return 0; }
-    L_(1, 4) L_(2, 4) L_(3, 4) L_(4, 4) L_(1, 8) L_(2, 8) L_(3, 8) L_(4, 8)
+    L_(1, 4) L_(2, 4) L_(3, 4) L_(4, 4) L_(1, 8) L_(2, 8) L_(3, 8) L_(4, 8) L_(1, 16) L_(2, 16) L_(3, 16) L_(4, 16)
 #undef L_
     return -1;
 }
@@ -108,7 +108,7 @@ extern "C" int roll_host(const oc_level_desc* lv, int A, int K, const uint8_t* s
                          int64_t P) {
 #define R_(a, k) \
     if (A == a && K == k) { run<a, k>(lv, sin, sout, act, alloc, subs, nsub, flags, lb, B, P); return 0; }
-    R_(1, 4) R_(2, 4) R_(3, 4) R_(4, 4) R_(1, 8) R_(2, 8) R_(3, 8) R_(4, 8)
+    R_(1, 4) R_(2, 4) R_(3, 4) R_(4, 4) R_(1, 8) R_(2, 8) R_(3, 8) R_(4, 8) R_(1, 16) R_(2, 16) R_(3, 16) R_(4, 16)
 #undef R_
     return -1;
 }
@@ -122,15 +122,15 @@ static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask
     if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
     for (int64_t e = 0; e < B; ++e) {
-        ocro::Row r;
+        ocro::RowT<K> r;
         for (int a = 0; a < A; ++a) {
             r.x |= (uint32_t)sin[a * P + e] << (8 * a);
             r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
             r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
         }
         for (int j = 0; j < K; ++j) {
-            r.loc |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
-            r.mask |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
+            r.loc[j >> 3] |= (uint64_t)sin[(kPL + j) * P + e] << (8 * (j & 7));
+            r.mask[j >> 3] |= (uint64_t)sin[(kPM + j) * P + e] << (8 * (j & 7));
         }
         ocro::RowOps<A, K> ops(L, blob);
         for (int i = 0; i < nsub; ++i) {
@@ -148,7 +148,7 @@ extern "C" int bounds_host(const oc_level_desc* lv, int A, int K, const uint8_t*
                            float* lb, uint8_t* doable, int64_t B, int64_t P) {
 #define B_(a, k) \
     if (A == a && K == k) { bounds<a, k>(lv, sin, subs, nsub, lb, doable, B, P); return 0; }
-    B_(1, 4) B_(2, 4) B_(3, 4) B_(4, 4) B_(1, 8) B_(2, 8) B_(3, 8) B_(4, 8)
+    B_(1, 4) B_(2, 4) B_(3, 4) B_(4, 4) B_(1, 8) B_(2, 8) B_(3, 8) B_(4, 8) B_(1, 16) B_(2, 16) B_(3, 16) B_(4, 16)
 #undef B_
     return -1;
 }

@@ -48,8 +48,8 @@ static void run(const oc_level_desc* lv, int max_T, const uint8_t* sin, uint8_t*
         tbl[c] = ocsw::tile_class(lv->tiles[c]);
         if (lv->tiles[c] == OC_TILE_DELIVERY && done_cell < 0) done_cell = c;
     }
-    uint8_t cell[8], mask[8];
-    for (int j = 0; j < 8; ++j) { cell[j] = j < lv->num_items ? lv->item_cell[j] : 0xFF; mask[j] = j < lv->num_items ? lv->item_mask[j] : 0; }
+    uint8_t cell[16], mask[16];
+    for (int j = 0; j < 16; ++j) { cell[j] = j < lv->num_items ? lv->item_cell[j] : 0xFF; mask[j] = j < lv->num_items ? lv->item_mask[j] : 0; }
     ocsw::SwarLevel S;
     ocsw::build_swar_level(S, W, H, done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y, A, cell, mask,
                            lv->encoding);
@@ -92,13 +92,13 @@ static void run(const oc_level_desc* lv, int max_T, const uint8_t* sin, uint8_t*
 extern "C" int swar_host_step_n(const oc_level_desc* lv, int A, int K, int max_T, const uint8_t* sin, uint8_t* traj,
                                 const uint8_t* act, uint8_t* exo, uint8_t* coll, int64_t B, int64_t P, int n) {
 #define RN(a, k) if (A == a && K == k) { run<a, k>(lv, max_T, sin, traj, act, exo, coll, B, P, n); return 0; }
-    RN(1, 4) RN(2, 4) RN(3, 4) RN(4, 4) RN(1, 8) RN(2, 8) RN(3, 8) RN(4, 8)
+    RN(1, 4) RN(2, 4) RN(3, 4) RN(4, 4) RN(1, 8) RN(2, 8) RN(3, 8) RN(4, 8) RN(1, 16) RN(2, 16) RN(3, 16) RN(4, 16)
     return -1;
 }
 
 extern "C" int swar_host_step(const oc_level_desc* lv, int A, int K, int max_T, const uint8_t* sin, uint8_t* sout,
                               const uint8_t* act, uint8_t* exo, uint8_t* coll, int64_t B, int64_t P) {
 #define R(a, k) if (A == a && K == k) { run<a, k>(lv, max_T, sin, sout, act, exo, coll, B, P); return 0; }
-    R(1, 4) R(2, 4) R(3, 4) R(4, 4) R(1, 8) R(2, 8) R(3, 8) R(4, 8)
+    R(1, 4) R(2, 4) R(3, 4) R(4, 4) R(1, 8) R(2, 8) R(3, 8) R(4, 8) R(1, 16) R(2, 16) R(3, 16) R(4, 16)
     return -1;
 }

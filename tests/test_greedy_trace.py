@@ -61,6 +61,28 @@ def test_all_subtasks_match_reference():
         assert ours == ep["all_subtasks"], ep["level"]
 
 
+def test_parallel_action_choice_matches_reference_set_order():
+    """Of two actions with one transition the reference's generate_graph keeps the one its
+    recipe.actions set iterates last (stripsworld.py:50-70); recipes._HASH0_KEPT must be that
+    choice in the PYTHONHASHSEED=0 orders tests/golden/gen_recipe_order.py recorded."""
+    with open(os.path.join(tl.GOLDEN, "recipe_order.json")) as f:
+        orders = json.load(f)["orders"]
+    for recipe in ("SimpleTomato", "SimpleLettuce", "Salad", "OnionSalad"):
+        order = orders["0"][recipe]
+        acts, _ = recipes.recipe_actions(recipe)
+        assert sorted(order) == sorted(str(a) for a in acts), recipe
+        kept = set()
+        for a in acts:
+            for b in acts:
+                if a is not b and a.name == b.name == "Merge" and sorted(a.pre) == sorted(b.pre) and \
+                        sorted(a.post_add) == sorted(b.post_add):
+                    kept.add(max(str(a), str(b), key=order.index))
+        assert kept == set(recipes._HASH0_KEPT.get(recipe, ())), recipe
+    # other seeds keep other members of the same pairs (the variants subtasks.json records)
+    assert any(orders[s]["OnionSalad"].index("Merge(Onion, Tomato)") < orders[s]["OnionSalad"].index(
+        "Merge(Tomato, Onion)") for s in orders)
+
+
 def test_subtask_masks_match_planner_table():
     """subtask_masks == the oc_subtask masks nav_utils.get_subtask_obj implies (the Salad
     table the rollout fixtures were recorded with, tests/golden/gen_rollout.py)."""
