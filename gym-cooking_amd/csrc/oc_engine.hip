@@ -697,7 +697,8 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
 // Image observation (oc_render, GameImage.get_image_obs: gym_cooking/misc/game/gameimage.py:31-51,
 // Game.on_render / draw_*: game.py:56-186).  Two blocks per (env, cell row), each taking half
 // of the row's pixel groups in whole waves.  In each block the first W lanes
-// build each cell's ordered draw list in LDS (items not held in slot order, then every agent
+// build each cell's ordered draw list in LDS (items not held in slot order or the caller's
+// draw rank, then every agent
 // in order followed by its held item).  The block then writes the row's tile*W*tile*3 output
 // bytes in iterations of 16 pixels per lane (48 output bytes), consecutive lanes on consecutive
 // pixels, so a wave's 64 lanes cover 1,024 pixels that span every cell of one to three image
@@ -743,6 +744,7 @@ __device__ __forceinline__ int div_small(int n, int d, float rcp) {
 
 template <int A, int K>
 __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const uint8_t* __restrict__ state,
+                                                           const uint8_t* __restrict__ rank,
                                                            const uint32_t* __restrict__ atlas,
                                                            const uint32_t* __restrict__ bg,
                                                            uint8_t* __restrict__ out) {
@@ -788,10 +790,27 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
             if (f != 0u && R.food_sprite[f] != 0xFFu)
                 push(R.food_base[cls] + (int32_t)R.food_sprite[f] * R.size[cls] * R.size[cls], cls);
         };
-        // Game.on_render: objects not held (draw_object, game.py:138-160) ...
+        // Game.on_render: objects not held (draw_object, game.py:138-160), in world.objects order
+        // when the caller gives ranks (render.DrawOrder), else in slot order ...
+        uint32_t here = 0u;
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            if (s[(kPL + j) * P] == (uint8_t)cell && !((held >> j) & 1u)) push_item(s[(kPM + j) * P], 0, 1, 0);
+            if (s[(kPL + j) * P] == (uint8_t)cell) here |= 1u << j;
+        here &= ~held;
+        while (here != 0u) {
+            int j = __builtin_ctz(here);
+            if (rank != nullptr && (here & (here - 1u)) != 0u) {  // several objects on this square
+                uint32_t best = 0xFFFFFFFFu;
+                for (uint32_t m = here; m != 0u; m &= m - 1u) {
+                    const int k = __builtin_ctz(m);
+                    const uint32_t key = ((uint32_t)rank[(int64_t)k * P + e] << 5) | (uint32_t)k;
+                    if (key < best) best = key;
+                }
+                j = (int)(best & 31u);
+            }
+            here &= ~(1u << j);
+            push_item(s[(kPM + j) * P], 0, 1, 0);
+        }
         // ... then the agents in order, each with its held object (draw_agent / draw_agent_object, :98-136)
 #pragma unroll
         for (int a = 0; a < A; ++a) {
@@ -1478,6 +1497,12 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
 
 int oc_render(const oc_handle* h, const void* state, const uint32_t* atlas, const uint32_t* background,
               const oc_render_desc* desc, uint8_t* out, int64_t B, void* stream) {
+    return oc_render_ordered(h, state, nullptr, atlas, background, desc, out, B, stream);
+}
+
+int oc_render_ordered(const oc_handle* h, const void* state, const uint8_t* draw_rank, const uint32_t* atlas,
+                      const uint32_t* background, const oc_render_desc* desc, uint8_t* out, int64_t B,
+                      void* stream) {
     if (h == nullptr || state == nullptr || atlas == nullptr || background == nullptr || desc == nullptr ||
         out == nullptr || B < 0)
         return fail(OC_EINVAL, "bad argument");
@@ -1514,8 +1539,8 @@ int oc_render(const oc_handle* h, const void* state, const uint32_t* atlas, cons
     const dim3 grid((unsigned)(B * H * R.parts));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_RENDER(A, K)                                                                               \
-    hipLaunchKernelGGL((oc_render_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state, atlas, \
-                       background, out)
+    hipLaunchKernelGGL((oc_render_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state, draw_rank, \
+                       atlas, background, out)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_RENDER)
     return hip_check("oc_render launch");
 }

@@ -32,7 +32,7 @@ OC_STAT_NAMES = ("episodes", "successes", "steps", "collisions", "errors")
 # Every symbol include/oc_engine.h declares (tests check the library exports them all).
 EXPORTED_SYMBOLS = (
     "oc_abi_version", "oc_last_error", "oc_create", "oc_destroy", "oc_get_layout", "oc_reset",
-    "oc_step", "oc_step_n", "oc_rollout", "oc_nav_likelihood", "oc_subtask_bounds", "oc_reachability", "oc_render",
+    "oc_step", "oc_step_n", "oc_rollout", "oc_nav_likelihood", "oc_subtask_bounds", "oc_reachability", "oc_render", "oc_render_ordered",
     "oc_gen_actions", "oc_state_checksum", "oc_stats_size", "oc_stats_reduce",
 )
 
@@ -185,6 +185,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.oc_reachability.restype = ctypes.c_int
     lib.oc_reachability.argtypes = [vp, ctypes.POINTER(i32), vp, i64, vp, i64]
     lib.oc_render.argtypes = [vp, vp, vp, vp, ctypes.POINTER(OcRenderDesc), vp, i64, vp]
+    lib.oc_render_ordered.restype = ctypes.c_int
+    lib.oc_render_ordered.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(OcRenderDesc), vp, i64, vp]
     lib.oc_step_n.restype = ctypes.c_int
     lib.oc_step_n.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]
     lib.oc_gen_actions.restype = ctypes.c_int

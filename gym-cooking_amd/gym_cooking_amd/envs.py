@@ -445,6 +445,7 @@ class OvercookedEnvironment:
         self._host = None
         self._group_names = frozenset()
         self._step_raises = False
+        self._draw = None  # render.DrawOrder: world.objects order for get_image_obs
         self.game = None
 
     # -- reference bookkeeping ------------------------------------------------------------
@@ -489,6 +490,8 @@ class OvercookedEnvironment:
         self._group_names = frozenset()
         self._host = eng.reset()
         self._refresh()
+        from .render import DrawOrder
+        self._draw = DrawOrder(self.level, eng.K)
         if getattr(self.arglist, "record", False) or getattr(self.arglist, "with_image_obs", False):
             self.game = _GameImage(self)  # GameImage(filename, world, sim_agents) (:232-240)
         self.obs_tm1 = _copy.copy(self)
@@ -522,6 +525,7 @@ class OvercookedEnvironment:
         for a, act in zip(self.obs_tm1.sim_agents, executed):
             a.action = act
         self._host = new
+        self._draw.update(_object_planes(pre, eng.A, eng.K), _object_planes(new, eng.A, eng.K))
         self._refresh(executed)
         self.agent_actions = {n: act for n, act in zip(names, executed)}
         if self._step_raises:
@@ -653,16 +657,27 @@ class OvercookedEnvironment:
             raise ValueError("expected %d state bytes, got %s" % (self._engine.NP, b.shape))
         self._host = b
         self._group_names = frozenset()
+        from .render import DrawOrder
+        self._draw = DrawOrder(self.level, self._engine.K)
+        self._draw.sync(_object_planes(b, self._engine.A, self._engine.K))
         self._refresh()
+
+
+def _object_planes(env_bytes: np.ndarray, A: int, K: int) -> Dict[str, np.ndarray]:
+    """The held-slot, location and mask planes of one env's state bytes (render.DrawOrder);
+    the shim steps a finished env again (it clears DONE), so no auto-reset is implied."""
+    return {"ah": env_bytes[2 * A:3 * A], "loc": env_bytes[3 * A:3 * A + K], "mask": env_bytes[3 * A + K:3 * A + 2 * K]}
 
 
 class _GameImage:
     """``env.game`` (misc/game/gameimage.py:10-51): ``get_image_obs()`` renders the env's
-    current state on the GPU (oc_render) and returns the reference's u8 [H*80, W*80, 3] array."""
+    current state on the GPU (oc_render_ordered, objects of one square in the reference's
+    world.objects order) and returns the reference's u8 [H*80, W*80, 3] array."""
 
     def __init__(self, env):
         self._env = env
         self._renderer = None
+        self._rank = None
 
     def get_image_obs(self) -> np.ndarray:
         env = self._env
@@ -670,8 +685,10 @@ class _GameImage:
         if self._renderer is None:
             from .render import Renderer
             self._renderer = Renderer(single.b)
+            self._rank = torch.zeros((single.K, single.P), dtype=torch.uint8, device=single.b.device)
         single._upload(env._host, single.s_in)
-        return self._renderer.render(single.s_in)[0].cpu().numpy()
+        self._rank[:, 0] = torch.from_numpy(env._draw.ranks())
+        return self._renderer.render(single.s_in, draw_rank=self._rank)[0].cpu().numpy()
 
 
 class _Single:
@@ -777,12 +794,13 @@ class OvercookedVecEnv:
                 "error": (fl & FLAG_ERR) != 0}
         return dst, reward, done, info
 
-    def render(self, channels: str = "reference") -> torch.Tensor:
-        """u8 [B, H*80, W*80, 3] image observations of the current states (oc_render)."""
+    def render(self, channels: str = "reference", draw_rank: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """u8 [B, H*80, W*80, 3] image observations of the current states (oc_render_ordered;
+        `draw_rank`: optional u8 [K, pitch] per-slot draw ranks, see render.DrawOrder)."""
         if getattr(self, "_renderer", None) is None:
             from .render import Renderer
             self._renderer = Renderer(self.batch)
-        return self._renderer.render(self.state, channels=channels)
+        return self._renderer.render(self.state, channels=channels, draw_rank=draw_rank)
 
     def episode_stats(self) -> torch.Tensor:
         """int64 [episodes, successes, steps, collisions, errors] since construction."""

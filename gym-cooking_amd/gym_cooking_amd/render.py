@@ -22,9 +22,19 @@ which parses ``0xRRGGBBAA``, and stores ``(color.g, color.b, color.r)``.  That y
 ``(R, G, 0)``, which ``channels="reference"`` reproduces.  ``channels="rgb"`` gives the drawn
 RGB image instead.
 
-Parity is unpinned: pygame and SDL are not installed here, so no reference image could be
-produced.  tests/ checks the kernel against an independent numpy restatement
-(oracle/render_oracle.py) of the same rules.
+Draw order of objects that share a square.  ``on_render`` draws the objects that are not held
+in ``world.objects`` order (game.py:62-74): the groups in the order their names were first
+inserted, each group's list in insertion order (``World.insert``, utils/world.py:304-305).  A
+merge re-inserts the merged object under its new name (utils/interact.py:46-52), so the order
+is episode history the state does not hold.  Only dishes delivered to one Delivery square
+share a square (they stay there, interact.py:35-40).  ``DrawOrder`` replays that history from
+consecutive states and gives ``oc_render_ordered`` a per-slot draw rank; without ranks the
+kernel draws a square's objects in slot order.
+
+Parity: the kernel and an independent numpy restatement (oracle/render_oracle.py) reproduce
+the reference's screenshots and recorded GIF frames (tests/test_render.py); the draw order is
+pinned to the reference's world.objects order along recorded episodes
+(tests/golden/gen_draw_order.py, tests/test_draw_order.py).
 """
 from __future__ import annotations
 
@@ -147,6 +157,69 @@ class RenderTables:
         return d
 
 
+def _group_name(mask: int, enc: int) -> str:
+    """``Object.name``: the contents' names, sorted, without their states (core.py:161-171)."""
+    return "-".join(n for n, _ in _levels.mask_contents(mask, enc))
+
+
+class DrawOrder:
+    """The reference's ``world.objects`` order of one env's objects, replayed from its
+    consecutive states.  ``load_level`` inserts the objects in map scan order
+    (overcooked_environment.py:158-165), which is slot order; a merge removes the object it
+    absorbed and the holder's object, and re-inserts the holder's (the engine keeps the
+    holder's slot) at the end of its new name's group, creating the group if the name is new
+    (utils/interact.py:46-52, world.py:304-315).  Groups stay when emptied, as dict keys do."""
+
+    def __init__(self, level: "_levels.Level", K: int):
+        self.level, self.K = level, K
+        self.reset()
+
+    def reset(self) -> None:
+        enc = self.level.encoding
+        self.groups: Dict[str, list] = {}
+        for j, (_cell, m) in enumerate(self.level.items):
+            self.groups.setdefault(_group_name(m, enc), []).append(j)
+
+    def update(self, prev: Dict[str, np.ndarray], nxt: Dict[str, np.ndarray]) -> None:
+        """Advance over one step.  `prev` / `nxt` hold one env's planes: ``ah`` [A], ``loc``
+        [K], ``mask`` [K], ``t`` (and ``fl``); a state with DONE set is followed by a reset."""
+        if int(prev.get("fl", 0)) & 1:  # auto-reset (DESIGN.md §1): the next state is the template
+            self.reset()
+            return
+        enc = self.level.encoding
+        gone = {j for j in range(self.K) if prev["loc"][j] != 0xFF and nxt["loc"][j] == 0xFF}
+        if gone:
+            for g in self.groups.values():
+                g[:] = [j for j in g if j not in gone]
+        for a, h in enumerate(nxt["ah"]):
+            h = int(h)
+            if h >= self.K or int(prev["ah"][a]) != h:
+                continue
+            old, new = _group_name(int(prev["mask"][h]), enc), _group_name(int(nxt["mask"][h]), enc)
+            if old != new:  # a merge into the object this agent holds
+                self.groups[old].remove(h)
+                self.groups.setdefault(new, []).append(h)
+
+    def sync(self, planes: Dict[str, np.ndarray]) -> None:
+        """Start from a state of unknown history (a loaded state): each live object in the
+        group of its current name, groups and objects in slot order."""
+        enc = self.level.encoding
+        self.groups = {}
+        for j in range(self.K):
+            if planes["loc"][j] != 0xFF:
+                self.groups.setdefault(_group_name(int(planes["mask"][j]), enc), []).append(j)
+
+    def ranks(self) -> np.ndarray:
+        """u8 [K]: each slot's position in world.objects order (0xFF: merged away)."""
+        r = np.full(self.K, 0xFF, np.uint8)
+        i = 0
+        for g in self.groups.values():
+            for j in g:
+                r[j] = i
+                i += 1
+        return r
+
+
 class Renderer:
     """Image observations of an :class:`engine.OvercookedBatch`'s states on its GPU."""
 
@@ -163,18 +236,25 @@ class Renderer:
         import torch
         return torch.empty((self.batch.B,) + self.shape, dtype=torch.uint8, device=self.batch.device)
 
-    def render(self, state, out=None, channels: str = "reference"):
-        """u8 [B, H*80, W*80, 3] images of all B envs of `state`."""
+    def render(self, state, out=None, channels: str = "reference", draw_rank=None):
+        """u8 [B, H*80, W*80, 3] images of all B envs of `state`.  `draw_rank` (optional u8
+        [K, pitch] device tensor, e.g. stacked ``DrawOrder.ranks()``): the objects of one
+        square are drawn in ascending rank, ties in slot order; without it, in slot order."""
         self.batch._check(state, self.batch.layout.state_bytes)
         shape = (self.batch.B,) + self.shape
         out = self.new_images() if out is None else out
         if tuple(out.shape) != shape or not out.is_contiguous() or out.device != self.batch.device:
             raise ValueError("out must be a contiguous u8 %s tensor on %s" % (shape, self.batch.device))
+        rank_ptr = None
+        if draw_rank is not None:
+            self.batch._check(draw_rank, self.batch.K * self.batch.pitch)
+            rank_ptr = ctypes.c_void_p(draw_rank.data_ptr())
         desc = self.tables.desc_with(channels)
-        capi.check(self.batch.lib.oc_render(self.batch._h, ctypes.c_void_p(state.data_ptr()),
-                                            ctypes.c_void_p(self.atlas.data_ptr()),
-                                            ctypes.c_void_p(self.background.data_ptr()), ctypes.byref(desc),
-                                            ctypes.c_void_p(out.data_ptr()), self.batch.B, self.batch._stream()))
+        capi.check(self.batch.lib.oc_render_ordered(self.batch._h, ctypes.c_void_p(state.data_ptr()), rank_ptr,
+                                                    ctypes.c_void_p(self.atlas.data_ptr()),
+                                                    ctypes.c_void_p(self.background.data_ptr()), ctypes.byref(desc),
+                                                    ctypes.c_void_p(out.data_ptr()), self.batch.B,
+                                                    self.batch._stream()))
         return out
 
 

@@ -372,6 +372,16 @@ typedef struct {
 int oc_render(const oc_handle* h, const void* state, const uint32_t* atlas, const uint32_t* background,
               const oc_render_desc* desc, uint8_t* out, int64_t B, void* stream);
 
+/* oc_render with the draw order of objects that share a square (Game.on_render draws the
+ * objects not held in world.objects order, game.py:62-74: name groups in first-insertion
+ * order, each in insertion order -- episode history, world.py:304-315, interact.py:46-52).
+ *   draw_rank : device u8 [K][pitch] or NULL; objects of one square are drawn in ascending
+ *               rank, ties in slot order.  NULL: slot order (oc_render).  The host side's
+ *               render.DrawOrder replays the reference's order from consecutive states. */
+int oc_render_ordered(const oc_handle* h, const void* state, const uint8_t* draw_rank, const uint32_t* atlas,
+                      const uint32_t* background, const oc_render_desc* desc, uint8_t* out, int64_t B,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -85,8 +85,10 @@ def _draw_obj(screen, spr, mask, x, y, held, enc=0):
               y * SCALE + off_plain)
 
 
-def render_env(level, env_bytes, A, K, spr=None, channels="reference"):
-    """One env's image from its state bytes (ax[A] ay[A] ah[A] loc[K] mask[K] t_lo t_hi flags)."""
+def render_env(level, env_bytes, A, K, spr=None, channels="reference", order=None):
+    """One env's image from its state bytes (ax[A] ay[A] ah[A] loc[K] mask[K] t_lo t_hi flags).
+    `order`: the slots in the order the objects are drawn (the reference's world.objects
+    order, game.py:62-74); default slot order."""
     spr = _sprites() if spr is None else spr
     W, H = level.width, level.height
     b = [int(v) for v in env_bytes]
@@ -111,7 +113,7 @@ def render_env(level, env_bytes, A, K, spr=None, channels="reference"):
         if kind == 2:
             _blit(screen, spr["cutboard@80"], x * SCALE, y * SCALE)
     held = {h for h in ah if h < K}
-    for j in range(K):
+    for j in (range(K) if order is None else order):
         if loc[j] != 0xFF and j not in held:
             _draw_obj(screen, spr, mask[j], loc[j] % W, loc[j] // W, False, level.encoding)
     for a in range(A):

@@ -144,7 +144,9 @@ def test_render_random_batch_and_errors():
 @pytest.mark.gpu
 def test_shim_image_obs():
     """OvercookedEnvironment(with_image_obs=True): info['image_obs'] and game.get_image_obs()
-    are the current state's image (step :290-300)."""
+    are the current state's image (step :290-300), the objects of one square drawn in the
+    world.objects order render.DrawOrder replays (pinned in tests/test_draw_order.py; this
+    episode's two deliveries share a Delivery square from step 30 on)."""
     import types
     from gym_cooking_amd.envs import OvercookedEnvironment
     fx, A = tl.load_fixture("greedy.npz"), 2
@@ -158,7 +160,9 @@ def test_shim_image_obs():
         codes = fx["act"][fx["ep_act_off"][e] + step][:A]
         _, _, _, info = env.step({"agent-%d" % (a + 1): levels.ACTIONS[int(codes[a])] for a in range(A)})
         if step % 5 == 4 or step == int(fx["ep_T"][e]) - 1:
-            exp = render_oracle.render_env(lv, env.state_bytes(), A, capi.item_slots(lv))
+            r = env._draw.ranks()
+            order = sorted(range(len(r)), key=lambda j: (r[j], j))
+            exp = render_oracle.render_env(lv, env.state_bytes(), A, capi.item_slots(lv), order=order)
             assert info["image_obs"].shape == (lv.height * 80, lv.width * 80, 3)
             assert np.array_equal(info["image_obs"], exp), step
             assert np.array_equal(env.game.get_image_obs(), exp)
