@@ -255,12 +255,39 @@ def measure_bayes(dev, world, n_updates: int = 256, n_seq: int = 8) -> dict:
     set_priors and their probabilities), replicated to `n_updates` delegators with their own
     planners, all updated in ONE bayes_update_batch call; `n_seq` of them are also updated one
     at a time (bayes_update) for comparison."""
+    from gym_cooking_amd.delegation import bayes_update_batch
+    make, calls, fx = bayes_jobs(dev)
+    warm = [make(c) for c in calls]  # first use of the level: expander, library, caches
+    bayes_update_batch([w[0] for w in warm], [w[1] for w in warm], [w[2] for w in warm], fx["beta"])
+    jobs = [make(calls[i % len(calls)]) for i in range(n_updates)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    errs = bayes_update_batch([j[0] for j in jobs], [j[1] for j in jobs], [j[2] for j in jobs], fx["beta"])
+    torch.cuda.synchronize()
+    dt = ocdist.max_over_ranks(time.perf_counter() - t0, dev)
+    seq = [make(calls[i % len(calls)]) for i in range(n_seq)]
+    t1 = time.perf_counter()
+    for d, env, acts in seq:
+        d.bayes_update(obs_tm1=env, actions_tm1=acts, beta=fx["beta"])
+    dts = time.perf_counter() - t1
+    exp = jobs[0][0].planner._exp
+    return {"value": world * n_updates / dt, "unit": "belief updates/s", "updates_per_gpu": n_updates,
+            "seconds": dt, "raised": sum(e is not None for e in errs),
+            "sequential": {"updates": n_seq, "value": n_seq / dts, "unit": "belief updates/s"},
+            "rollout_launches_per_batch": None if exp is None else exp.launches,
+            "workload": "C5 layout: full-divider_salad 4 agents, the reference's recorded 4-agent bayes_update "
+                        "calls (18 allocations each, Level-1 inverse planning) replicated, one batched call"}
+
+
+def bayes_jobs(dev, **planner_kw):
+    """(make, calls, fixture) of the bayes line: make(call) -> (delegator, PlanEnv, executed
+    actions) of one recorded 4-agent update (tests/golden/bayes.json) with a fresh planner;
+    `planner_kw` goes to E2E_BRTDP (tools/prof_host_search.py passes a CPU expander)."""
     import random as _random
     import re
     import numpy as np
     from gym_cooking_amd import capi, levels as _lv, recipes
-    from gym_cooking_amd.delegation import (BayesianDelegator, SubtaskAllocation, SubtaskAllocDistribution,
-                                            bayes_update_batch)
+    from gym_cooking_amd.delegation import BayesianDelegator, SubtaskAllocation, SubtaskAllocDistribution
     from gym_cooking_amd.planner import E2E_BRTDP, PlanEnv
     with open(os.path.join(ROOT, "tests", "golden", "bayes.json")) as f:
         fx = json.load(f)
@@ -298,7 +325,7 @@ def measure_bayes(dev, world, n_updates: int = 256, n_seq: int = 8) -> dict:
                 i = next(i for i, (_, ix, iy, m) in enumerate(held) if (ix, iy, m) == (x, y, hm))
                 s[L["agent_hold"] + q] = held.pop(i)[0]
         env = PlanEnv(lv, A, s, [g for g in c["groups"] if g not in static], device=dev)
-        planner = E2E_BRTDP(**fx["params"], rng=np.random.RandomState(c["np_seed"]))
+        planner = E2E_BRTDP(**fx["params"], rng=np.random.RandomState(c["np_seed"]), **planner_kw)
         d = BayesianDelegator(c["self"], env.get_agent_names(), "bd", planner, fx["none_action_prob"],
                               rng=_random.Random(c["random_seed"]))
         allocs = [tuple(SubtaskAllocation(None if st is None else subtask(st), tuple(a)) for st, a in rec)
@@ -308,26 +335,7 @@ def measure_bayes(dev, world, n_updates: int = 256, n_seq: int = 8) -> dict:
             d.probs.probs[k] = p
         return d, env, {n: tuple(a) for n, a in c["actions"].items()}
 
-    warm = [make(c) for c in calls]  # first use of the level: expander, library, caches
-    bayes_update_batch([w[0] for w in warm], [w[1] for w in warm], [w[2] for w in warm], fx["beta"])
-    jobs = [make(calls[i % len(calls)]) for i in range(n_updates)]
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    errs = bayes_update_batch([j[0] for j in jobs], [j[1] for j in jobs], [j[2] for j in jobs], fx["beta"])
-    torch.cuda.synchronize()
-    dt = ocdist.max_over_ranks(time.perf_counter() - t0, dev)
-    seq = [make(calls[i % len(calls)]) for i in range(n_seq)]
-    t1 = time.perf_counter()
-    for d, env, acts in seq:
-        d.bayes_update(obs_tm1=env, actions_tm1=acts, beta=fx["beta"])
-    dts = time.perf_counter() - t1
-    exp = jobs[0][0].planner._exp
-    return {"value": world * n_updates / dt, "unit": "belief updates/s", "updates_per_gpu": n_updates,
-            "seconds": dt, "raised": sum(e is not None for e in errs),
-            "sequential": {"updates": n_seq, "value": n_seq / dts, "unit": "belief updates/s"},
-            "rollout_launches_per_batch": None if exp is None else exp.launches,
-            "workload": "C5 layout: full-divider_salad 4 agents, the reference's recorded 4-agent bayes_update "
-                        "calls (18 allocations each, Level-1 inverse planning) replicated, one batched call"}
+    return make, calls, fx
 
 
 def measure_planner(dev, world) -> dict:

@@ -44,6 +44,11 @@ from . import levels as _levels
 from .engine import _ptr
 from . import recipes as _recipes
 
+try:  # the sample trial's loop in C (csrc/brtdp_host.c, built in-tree by csrc/Makefile)
+    from . import _brtdp as _native
+except ImportError:  # not built: the same loop in Python (tests/test_planner_host.py compares the two)
+    _native = None
+
 _NAV = [(0, 1), (0, -1), (-1, 0), (1, 0), (0, 0)]  # action codes 0..4 (World.NAV_ACTIONS + no-op)
 _NOOP = 4
 
@@ -121,6 +126,8 @@ def argmin(vector, rng=np.random):
         if i != len(vector) - 1:
             rng.random_sample()
         return i
+    if _native is not None:  # the same draw, restated over rng's uniforms (csrc/brtdp_host.c tie_pick)
+        return _native.tie_pick([v == m for v in vector], rng.random_sample)
     e_x = np.array(vector) == m
     return np.where(rng.multinomial(1, e_x / e_x.sum()))[0][0]
 
@@ -280,6 +287,7 @@ class E2E_BRTDP:
         host search without a GPU.  `rng`: the tie-breaking generator (default numpy's global
         one, as the reference)."""
         self.alpha, self.tau, self.cap, self.main_cap = alpha, tau, cap, main_cap
+        self.use_native = True  # the C sample-trial loop when built (False: the Python loop)
         self._make_expander = expander or _Expander
         self._rng = rng if rng is not None else np.random
         self.v_l: Dict = {}
@@ -312,31 +320,58 @@ class E2E_BRTDP:
             raise NotImplementedError("the reference agents do not plan the None subtask")
         assert len(subtask_agent_names) <= 2, "Cannot have more than 2 agents! Hm... {}".format(subtask_agent_names)
         names = env.get_agent_names()
-        self.subtask = subtask
-        self.subtask_agent_names = tuple(subtask_agent_names)
-        self.is_joint = len(subtask_agent_names) == 2
-        agents = [names.index(n) for n in subtask_agent_names]
-        assert agents == sorted(agents), "subtask agent names are not in order"
-        self._agents = agents
         level, A = env.level, len(names)
         key = expander_key(env, self.device)
         if self._exp is None or self._exp_key != key:
             self._exp = self._make_expander(level, A, self.device or env._device)
             self._exp_key = key
+        fast = getattr(env, "planner_bytes", None)
+        if fast is not None:
+            full = fast(self._exp.t_plane)
+        else:
+            b = env.state_bytes()
+            b[self._exp.t_plane:] = 0
+            full = b.tobytes()
+        return self._configure_raw(level, A, self.device or env._device, full, _groups(env), subtask,
+                                   subtask_agent_names)
+
+    def _configure_raw(self, level, A, dev, full: bytes, groups, subtask, subtask_agent_names):
+        """The set-up of _configure from a state's bytes (t and flags zeroed) and group names,
+        once the expander is chosen.  What it derives from (state, Level, agents, subtask) --
+        the planner's start bytes, cur_obj_count, the subtask row -- is a pure function of
+        those, kept per expander (many planners set up on the same states: the delegators'
+        other-agent planners at every state a Level-1 search visits)."""
         exp = self._exp
-        kind, starts, goal = _recipes.subtask_masks(subtask, exp.enc)
-        self._sub_key = str(subtask)
-        self._kind, self._goal_mask = kind, goal
-        full = env.state_bytes()
-        groups = _groups(env)
-        start = full.copy() if self._level else self._level0(full, exp)
-        start[exp.t_plane:] = 0
-        start = np.frombuffer(_canon(start.tobytes(), exp.A, exp.K, exp.enc), np.uint8).copy()
-        self.cur_obj_count = self._obj_count(start, exp, env.level)  # _define_goal_state on the Level-0 env
-        self._sub = capi.subtask(kind, agents, list(starts), goal, self.cur_obj_count, self._level)
-        self._level_name = env.level
+        names = _agent_names(A)
+        self.subtask = subtask
+        self.subtask_agent_names = tuple(subtask_agent_names)
+        self.is_joint = len(subtask_agent_names) == 2
+        agents = tuple(names.index(n) for n in subtask_agent_names)
+        assert list(agents) == sorted(agents), "subtask agent names are not in order"
+        self._agents = list(agents)
+        sk = str(subtask)
+        self._sub_key = sk
+        ck = (full, self._level, agents, sk)
+        hit = exp.__dict__.setdefault("_conf_cache", {}).get(ck)
+        if hit is None:
+            kind, starts, goal = _recipes.subtask_masks(subtask, exp.enc)
+            self._kind, self._goal_mask = kind, goal  # _obj_count reads them
+            start = np.frombuffer(full, np.uint8).copy()
+            if not self._level:
+                start = self._level0(start, exp)
+            start = np.frombuffer(_canon(start.tobytes(), exp.A, exp.K, exp.enc), np.uint8).copy()
+            count = self._obj_count(start, exp, level)  # _define_goal_state on the Level-0 env
+            # [start, kind, goal mask, cur_obj_count, subtask row, (goal, bound) of the no-op row]
+            hit = [start, kind, goal, count, capi.subtask(kind, list(agents), list(starts), goal, count, self._level),
+                   None]
+            if len(exp._conf_cache) > 1 << 18:
+                exp._conf_cache.clear()
+            exp._conf_cache[ck] = hit
+        start, self._kind, self._goal_mask, self.cur_obj_count, self._sub, _ = hit
+        self._conf = hit
+        self._level_name = level
         self._A = A
-        self._dev = self.device or env._device
+        self._dev = dev
         self.start = self._key(start, groups)
         # the start state: a no-op row gives its goal flag and lower bound
         return (start, [(_NOOP,) * len(agents)], self._sub)
@@ -346,11 +381,22 @@ class E2E_BRTDP:
         self._start_goal = bool(fl[0] & capi.ROLL_GOAL)  # is_goal_state with this call's cur_obj_count
         self._value_init(self.start, self._start_goal, float(lb[0]))
 
+    def _configure_gen(self, req):
+        """Finish a set-up whose request `req` _configure / _configure_raw made: the start's goal
+        flag and lower bound come from one no-op row, a pure function of the set-up, so a set-up
+        seen before (its cache entry) needs no row."""
+        hit = self._conf
+        if hit[5] is None:
+            _, fl, lb = yield req
+            hit[5] = (bool(fl[0] & capi.ROLL_GOAL), float(lb[0]))
+        self._start_goal = hit[5][0]
+        self._value_init(self.start, hit[5][0], hit[5][1])
+
     def set_settings(self, env, subtask, subtask_agent_names, other_agent_planners=None):
         self._drive(self._set_settings_gen(env, subtask, subtask_agent_names, other_agent_planners))
 
     def _set_settings_gen(self, env, subtask, subtask_agent_names, other_agent_planners=None):
-        self._configured((yield self._configure(env, subtask, subtask_agent_names, other_agent_planners)))
+        yield from self._configure_gen(self._configure(env, subtask, subtask_agent_names, other_agent_planners))
 
     def _exp_run(self, req):
         return self._exp.run([req])[0]
@@ -576,7 +622,10 @@ class E2E_BRTDP:
     # ---- search (e2e_brtdp.py:208-331, 842-878), as generators --------------------------------
     def _sample_trial(self):  # runSampleTrial
         """runSampleTrial; _q_all / _expected_diff / _need inlined (the same float64 operations
-        in the same order)."""
+        in the same order).  At Level 0 the loop runs in C (_brtdp.forward / backprop) and comes
+        back here only to expand a state or initialise its successors."""
+        if _native is not None and not self._level and self.use_native:
+            return (yield from self._sample_trial_native())
         x = self.start
         traj = []
         counter = 0
@@ -615,6 +664,27 @@ class E2E_BRTDP:
             v_u[rx] = min([c + v_u[vk] for c, vk in zip(costs, vks)])
             v_l[rx] = min([c + v_l[vk] for c, vk in zip(costs, vks)])
 
+    def _sample_trial_native(self):
+        sk = self._sub_key
+        succ, v_u, v_l, rng = self._succ, self.v_u, self.v_l, self._rng
+        rs = (self._repr(self.start), sk)
+        traj = []
+        x, counter, resume = self.start, 0, False
+        while True:
+            st, x, counter, i = _native.forward(succ, v_u, v_l, x, sk, rs, self.cap, counter, self.tau, traj,
+                                                rng.random_sample, resume)
+            if st == 0:
+                break
+            if st == 2:  # get_expected_diff's T raises
+                _raise_copy_crash(succ[(x, sk)][0][i])
+            if (x, sk) not in succ:
+                yield from self._need(x)
+            got = succ[(x, sk)]
+            if not got[6]:
+                self._init_succ(got)
+            resume = True
+        _native.backprop(succ, v_u, v_l, traj, sk)
+
     def _main(self):  # main
         main_counter = 0
         sk = (self._repr(self.start), self._sub_key)
@@ -625,7 +695,7 @@ class E2E_BRTDP:
             yield from self._sample_trial()
 
     def _next_action(self, env, subtask, subtask_agent_names, other_agent_planners):
-        self._configured((yield self._configure(env, subtask, subtask_agent_names, other_agent_planners)))
+        yield from self._configure_gen(self._configure(env, subtask, subtask_agent_names, other_agent_planners))
         cur = self.start
         self.cur_state = cur
         yield from self._modified_state(cur)
@@ -705,9 +775,10 @@ class E2E_BRTDP:
             return
         groups = key[1]
         for name, op in self.other_agent_planners.items():
-            env = PlanEnv(self._level_name, self._A, np.frombuffer(key[0], np.uint8), groups, device=self._dev)
             op._exp, op._exp_key, op._rng = self._exp, self._exp_key, self._rng
-            op._configured((yield op._configure(env, op.subtask, op.subtask_agent_names)))
+            op.other_agent_planners, op._level = {}, 0  # _configure without other planners: Level 0
+            yield from op._configure_gen(op._configure_raw(self._level_name, self._A, self._dev, key[0], groups,
+                                                           op.subtask, op.subtask_agent_names))
             yield from op._need(op.start)
             acts = op._succ[(op.start, op._sub_key)][0]
             argmin(op._q_all(op.start, op.v_l), op._rng)
@@ -735,6 +806,8 @@ class PlanEnv:
         self._world = None
         self._group_names = frozenset(group_names)
         self._enc = _encoding(level)
+        self._names = None
+        self._zero = None
 
     @property
     def world(self):
@@ -745,13 +818,33 @@ class PlanEnv:
 
     def item_names(self) -> FrozenSet[str]:
         """The current items' object-group names (ItemView.name of every item not merged away)."""
-        return frozenset(_envs.item_name(m, self._enc) for _, m in self._live)
+        if self._names is None:
+            self._names = frozenset(_envs.item_name(m, self._enc) for _, m in self._live)
+        return self._names
 
     def get_agent_names(self) -> List[str]:
-        return ["agent-%d" % (a + 1) for a in range(self._A)]
+        return list(_agent_names(self._A))
+
+    def planner_bytes(self, t_plane: int) -> bytes:
+        """The state bytes with t and flags zeroed (what a planner set-up reads), kept."""
+        if self._zero is None or self._zero[0] != t_plane:
+            b = self._bytes.copy()
+            b[t_plane:] = 0
+            self._zero = (t_plane, b.tobytes())
+        return self._zero[1]
 
     def state_bytes(self) -> np.ndarray:
         return self._bytes.copy()
+
+
+_AGENT_NAMES: Dict[int, List[str]] = {}
+
+
+def _agent_names(A: int) -> List[str]:
+    n = _AGENT_NAMES.get(A)
+    if n is None:
+        n = _AGENT_NAMES[A] = ["agent-%d" % (a + 1) for a in range(A)]
+    return n
 
 
 def _level_tables(level):

@@ -13,7 +13,7 @@ import pytest
 
 import oc_testlib as tl
 import test_planner_gpu as tg
-from gym_cooking_amd import capi, envs, levels
+from gym_cooking_amd import capi, envs, levels, recipes
 
 from oracle import oracle
 
@@ -251,3 +251,40 @@ def test_argmin_matches_multinomial_draws():
     assert a == b and np.random.random_sample() == (np.random.seed(7), [ref([1.0, 0.5, 2.0, 0.5][:k], np.random)
                                                                         for k in (1, 2, 3, 4)],
                                                     np.random.random_sample())[2]
+
+
+def test_native_sample_trial_matches_python_loop():
+    """The sample trial's C loop (csrc/brtdp_host.c, planner._sample_trial_native) and the Python
+    loop give the same searches: the same actions, bit-identical value tables, the same
+    generator state, on 40 random-play states of 2 kitchens with single and joint subtasks
+    (ties included: the multinomial path runs inside the C loop)."""
+    from gym_cooking_amd import planner as pl
+    from gym_cooking_amd.planner import E2E_BRTDP, PlanEnv, plan_batch
+    assert pl._native is not None, "the _brtdp extension is not built (make -C gym-cooking_amd/csrc)"
+    for level, sub, agn, names in (("open-divider_salad", recipes.Chop("Tomato"), ("agent-1",), ["Tomato", "Lettuce", "Plate"]),
+                                   ("partial-divider_salad", recipes.Chop("Lettuce"), ("agent-1", "agent-2"),
+                                    ["Tomato", "Lettuce", "Plate"])):
+        lv = levels.load_level(level)
+        ob = oracle.OracleBatch(lv, 2, 0, 20)
+        s, s2, a = ob.new_state(), ob.new_state(), ob.new_actions()
+        ob.reset(s)
+        for t in range(9):
+            ob.gen_actions(a, 0, t, 5)
+            ob.step(s, s2, a)
+            s, s2 = s2, s
+        ev = tl.env_view(s, 2, ob.K, ob.pitch, 20)
+        runs = []
+        for native in (True, False):
+            envs_, ps = [], []
+            for b in range(20):
+                envs_.append(PlanEnv(lv, 2, ev[:, b], names, device="cpu"))
+                p = E2E_BRTDP(alpha=0.01, tau=2, cap=75, main_cap=100, device="cpu", expander=OracleExpander,
+                              rng=np.random.RandomState(b))
+                p.use_native = native
+                ps.append(p)
+            acts = plan_batch(ps, envs_, [sub] * 20, [agn] * 20)
+            runs.append((acts, [(p.v_l, p.v_u, p._rng.get_state()[2]) for p in ps]))
+        (a1, t1), (a2, t2) = runs
+        assert a1 == a2
+        for (l1, u1, g1), (l2, u2, g2) in zip(t1, t2):
+            assert l1 == l2 and u1 == u2 and g1 == g2

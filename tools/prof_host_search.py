@@ -42,7 +42,16 @@ class BatchOracleExpander:
             self._obs[pitch] = oracle.OracleBatch(self.level, self.A, 0, pitch)
         return self._obs[pitch]
 
+    busy = 0.0  # seconds inside run() over all instances: the stand-in for the GPU's share
+
     def run(self, requests):
+        t0 = time.perf_counter()
+        try:
+            return self._run(requests)
+        finally:
+            BatchOracleExpander.busy += time.perf_counter() - t0
+
+    def _run(self, requests):
         subs, sub_id, rows = [], {}, []
         for state, codes, sub in requests:
             key = bytes(sub)
@@ -117,13 +126,35 @@ def plan_workload(B=256, steps=12):
     return lambda: plan_batch(planners, envs_, [recipes.Chop("Tomato")] * B, [("agent-1",)] * B), planners
 
 
+def bayes_workload(B=128):
+    import bench
+    from gym_cooking_amd.delegation import bayes_update_batch
+    make, calls, fx = bench.bayes_jobs("cpu", expander=BatchOracleExpander)
+    warm = [make(c) for c in calls]
+    bayes_update_batch([w[0] for w in warm], [w[1] for w in warm], [w[2] for w in warm], fx["beta"])
+    jobs = [make(calls[i % len(calls)]) for i in range(B)]
+    return (lambda: bayes_update_batch([j[0] for j in jobs], [j[1] for j in jobs], [j[2] for j in jobs],
+                                       fx["beta"])), [j[0].planner for j in jobs]
+
+
 def main():
     what = sys.argv[1]
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     if what == "plan":
         run, planners = plan_workload(B)
+    elif what == "bayes":
+        run, planners = bayes_workload(B)
     else:
         raise SystemExit("unknown workload")
+    if len(sys.argv) > 3 and sys.argv[3] == "time":  # no profiler: host seconds outside the expander
+        t0 = time.perf_counter()
+        run()
+        dt = time.perf_counter() - t0
+        exp = planners[0]._exp
+        print("%s: %d in %.2f s, host %.2f s (%.1f per s), %d rounds, %d rows" % (
+            what, B, dt, dt - BatchOracleExpander.busy, B / (dt - BatchOracleExpander.busy), exp.launches,
+            exp.rows_done))
+        return
     pr = cProfile.Profile()
     t0 = time.perf_counter()
     pr.enable()
@@ -135,6 +166,7 @@ def main():
     s = io.StringIO()
     st = pstats.Stats(pr, stream=s)
     st.sort_stats("tottime").print_stats(35)
+    st.sort_stats("cumulative").print_stats(40)
     print(s.getvalue())
 
 
