@@ -263,7 +263,169 @@ fail:
     return NULL;
 }
 
+/* expand(rows, fl, lb, cand, key, sk, m0, K, A, cost, changed) -> entry, illegal
+ * planner.E2E_BRTDP._expanded over one expansion's rollout rows (e2e_brtdp.py:103-206: T,
+ * get_actions; value_init's inputs): rows = the successors' state bytes [n][NP] (a buffer),
+ * fl = their u8 flags, lb = their f32 bounds, cand = the candidate joint actions in get_actions
+ * order, key = (state bytes, group names, agents, Level).  A row whose item masks changed (a
+ * chop or a merge) goes through changed(bytes) -> (canonical bytes, group names) in Python.
+ * Returns the _succ entry (without its initialised flag set) and {action: row} of the illegal
+ * candidates (or None). */
+static PyObject* expand(PyObject* self, PyObject* args) {
+    PyObject *rows_o, *fl_o, *lb_o, *cand, *key, *sk, *cost, *changed;
+    Py_ssize_t m0, K, A;
+    if (!PyArg_ParseTuple(args, "OOOO!O!OnnnO!O", &rows_o, &fl_o, &lb_o, &PyList_Type, &cand, &PyTuple_Type, &key, &sk,
+                          &m0, &K, &A, &PyDict_Type, &cost, &changed))
+        return NULL;
+    Py_buffer rb, fb, lbb;
+    if (PyObject_GetBuffer(rows_o, &rb, PyBUF_C_CONTIGUOUS) < 0) return NULL;
+    if (PyObject_GetBuffer(fl_o, &fb, PyBUF_C_CONTIGUOUS) < 0) {
+        PyBuffer_Release(&rb);
+        return NULL;
+    }
+    if (PyObject_GetBuffer(lb_o, &lbb, PyBUF_C_CONTIGUOUS) < 0) {
+        PyBuffer_Release(&rb);
+        PyBuffer_Release(&fb);
+        return NULL;
+    }
+    PyObject *actions = NULL, *succ = NULL, *costs = NULL, *vks = NULL, *goals = NULL, *lbs = NULL, *crash = NULL,
+             *illegal = NULL, *out = NULL, *ra = NULL, *self_vk = NULL, *self_r = NULL;
+    PyObject *sb = PyTuple_GET_ITEM(key, 0), *groups = PyTuple_GET_ITEM(key, 1), *agents = PyTuple_GET_ITEM(key, 2),
+             *lvl_o = PyTuple_GET_ITEM(key, 3);
+    const Py_ssize_t n = PyList_GET_SIZE(cand);
+    const Py_ssize_t NP = PyBytes_GET_SIZE(sb);
+    const int lvl = PyObject_IsTrue(lvl_o);
+    const unsigned char* raw = (const unsigned char*)rb.buf;
+    const unsigned char* fl = (const unsigned char*)fb.buf;
+    const float* lbv = (const float*)lbb.buf;
+    const unsigned char* pm = (const unsigned char*)PyBytes_AS_STRING(sb) + m0;
+    if (rb.len < n * NP || fb.len < n || lbb.len < n * (Py_ssize_t)sizeof(float)) {
+        PyErr_SetString(PyExc_ValueError, "expand: row buffers shorter than the candidates");
+        goto done;
+    }
+    actions = PyList_New(0);
+    succ = PyList_New(0);
+    costs = PyList_New(0);
+    vks = PyList_New(0);
+    goals = PyList_New(0);
+    lbs = PyList_New(0);
+    if (!actions || !succ || !costs || !vks || !goals || !lbs) goto done;
+    ra = (lvl || PyTuple_GET_SIZE(agents) == A) ? Py_None : agents;  /* _repr's agents entry */
+    Py_INCREF(ra);
+    for (Py_ssize_t r = 0; r < n; ++r) {
+        PyObject* c = PyList_GET_ITEM(cand, r);
+        const unsigned f = fl[r];
+        if (!(f & 1u)) {  /* OC_ROLL_LEGAL */
+            if (illegal == NULL && (illegal = PyDict_New()) == NULL) goto done;
+            PyObject* ri = PyLong_FromSsize_t(r);
+            if (ri == NULL || PyDict_SetItem(illegal, c, ri) < 0) {
+                Py_XDECREF(ri);
+                goto done;
+            }
+            Py_DECREF(ri);
+            continue;
+        }
+        if (f & 4u) {  /* OC_ROLL_ASSERT: T raises (e2e_brtdp.py:143) */
+            PyErr_Format(PyExc_AssertionError, "action %S led to co-located subtask agents", c);
+            goto done;
+        }
+        const unsigned char* row = raw + r * NP;
+        PyObject *ns, *ng;
+        if (memcmp(row + m0, pm, (size_t)K) != 0) {  /* a chop or a merge */
+            PyObject* b = PyBytes_FromStringAndSize((const char*)row, NP);
+            if (b == NULL) goto done;
+            PyObject* t = PyObject_CallOneArg(changed, b);
+            Py_DECREF(b);
+            if (t == NULL) goto done;
+            ns = PyTuple_GetItem(t, 0);
+            ng = PyTuple_GetItem(t, 1);
+            if (ns == NULL || ng == NULL) {
+                Py_DECREF(t);
+                goto done;
+            }
+            Py_INCREF(ns);
+            Py_INCREF(ng);
+            Py_DECREF(t);
+        } else {
+            ns = PyBytes_FromStringAndSize((const char*)row, NP);
+            if (ns == NULL) goto done;
+            ng = groups;
+            Py_INCREF(ng);
+        }
+        PyObject* nk = PyTuple_Pack(4, ns, ng, agents, lvl_o);
+        PyObject* rep = PyTuple_Pack(3, ns, ng, ra);
+        PyObject* vk = rep ? PyTuple_Pack(2, rep, sk) : NULL;
+        Py_XDECREF(rep);
+        if (nk == NULL || vk == NULL) {
+            Py_XDECREF(nk);
+            Py_XDECREF(vk);
+            Py_DECREF(ns);
+            Py_DECREF(ng);
+            goto done;
+        }
+        if (lvl) {  /* _copy_crashes: two co-located agents that both hold */
+            const unsigned char* q = (const unsigned char*)PyBytes_AS_STRING(ns);
+            int hit = 0;
+            for (Py_ssize_t i = 0; i < A && !hit; ++i) {
+                if (q[2 * A + i] == 0xFF) continue;
+                for (Py_ssize_t j = i + 1; j < A; ++j)
+                    if (q[2 * A + j] != 0xFF && q[i] == q[j] && q[A + i] == q[A + j]) {
+                        hit = 1;
+                        break;
+                    }
+            }
+            if (hit) {
+                PyObject* ai = PyLong_FromSsize_t(PyList_GET_SIZE(actions));
+                if (crash == NULL) crash = PySet_New(NULL);
+                if (ai == NULL || crash == NULL || PySet_Add(crash, ai) < 0) {
+                    Py_XDECREF(ai);
+                    Py_DECREF(nk);
+                    Py_DECREF(vk);
+                    Py_DECREF(ns);
+                    Py_DECREF(ng);
+                    goto done;
+                }
+                Py_DECREF(ai);
+            }
+        }
+        Py_DECREF(ns);
+        Py_DECREF(ng);
+        PyObject* cst = PyDict_GetItemWithError(cost, c);
+        PyObject* lbf = PyFloat_FromDouble((double)lbv[r]);
+        int bad = cst == NULL || lbf == NULL;
+        if (cst == NULL && !PyErr_Occurred()) PyErr_SetObject(PyExc_KeyError, c);
+        bad = bad || PyList_Append(actions, c) < 0 || PyList_Append(succ, nk) < 0 || PyList_Append(costs, cst) < 0 ||
+              PyList_Append(vks, vk) < 0 || PyList_Append(goals, (f & 2u) ? Py_True : Py_False) < 0 ||
+              PyList_Append(lbs, lbf) < 0;
+        Py_DECREF(nk);
+        Py_DECREF(vk);
+        Py_XDECREF(lbf);
+        if (bad) goto done;
+    }
+    self_r = PyTuple_Pack(3, sb, groups, ra);
+    if (self_r == NULL || (self_vk = PyTuple_Pack(2, self_r, sk)) == NULL) goto done;
+    out = Py_BuildValue("([OOOOOOOOO]O)", actions, succ, costs, vks, goals, lbs, Py_False, crash ? crash : Py_None,
+                        self_vk, illegal ? illegal : Py_None);
+done:
+    Py_XDECREF(actions);
+    Py_XDECREF(succ);
+    Py_XDECREF(costs);
+    Py_XDECREF(vks);
+    Py_XDECREF(goals);
+    Py_XDECREF(lbs);
+    Py_XDECREF(crash);
+    Py_XDECREF(illegal);
+    Py_XDECREF(ra);
+    Py_XDECREF(self_r);
+    Py_XDECREF(self_vk);
+    PyBuffer_Release(&rb);
+    PyBuffer_Release(&fb);
+    PyBuffer_Release(&lbb);
+    return out;
+}
+
 static PyMethodDef methods[] = {
+    {"expand", expand, METH_VARARGS, "_expanded's successor lists from one expansion's rollout rows"},
     {"forward", forward, METH_VARARGS, "runSampleTrial's forward loop over expanded, initialised states"},
     {"backprop", backprop, METH_VARARGS, "runSampleTrial's backward pass"},
     {"tie_pick", tie_pick, METH_VARARGS, "argmin's multinomial tie-break over a list of minima flags"},

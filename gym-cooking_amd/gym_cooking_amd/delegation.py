@@ -258,8 +258,9 @@ class BayesianDelegator:
         self.probs.normalize()
 
     def bayes_update(self, obs_tm1, actions_tm1, beta) -> None:  # :1026-1072
-        doable = self._doability(obs_tm1, self._doability_pairs())
-        self.planner._drive(self._bayes_update_gen(obs_tm1, actions_tm1, beta, doable))
+        with _planner.searching():
+            doable = self._doability(obs_tm1, self._doability_pairs())
+            self.planner._drive(self._bayes_update_gen(obs_tm1, actions_tm1, beta, doable))
 
 
 def bayes_update_batch(delegators: Sequence[BayesianDelegator], obs_list, actions_list, beta) -> list:
@@ -271,6 +272,11 @@ def bayes_update_batch(delegators: Sequence[BayesianDelegator], obs_list, action
     shared oc_rollout launches.  Returns, per delegator, None or the exception its update
     raised (the reference's bayes_update raises AssertionError / AttributeError on some
     states; the others still complete)."""
+    with _planner.searching():
+        return _bayes_update_batch(delegators, obs_list, actions_list, beta)
+
+
+def _bayes_update_batch(delegators, obs_list, actions_list, beta) -> list:
     n = len(delegators)
     assert len(obs_list) == len(actions_list) == n
     groups: Dict[tuple, List[int]] = {}

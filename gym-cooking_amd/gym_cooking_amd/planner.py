@@ -31,6 +31,8 @@ e2e_brtdp.py:842-878), drawing the same random numbers as the reference.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import itertools
 import types
 from typing import Dict, FrozenSet, List, Optional, Sequence, Tuple
@@ -50,6 +52,22 @@ except ImportError:  # not built: the same loop in Python (tests/test_planner_ho
     _native = None
 
 _NAV = [(0, 1), (0, -1), (-1, 0), (1, 0), (0, 0)]  # action codes 0..4 (World.NAV_ACTIONS + no-op)
+
+
+@contextlib.contextmanager
+def searching():
+    """The cyclic garbage collector paused for a search call.  A search allocates millions of
+    small tuples (its table keys and successor lists) that form no reference cycles; CPython's
+    collector would walk them over and over as they accumulate -- 40 % of plan_batch's host
+    time (tools/prof_host_search.py).  Nothing is collected late but cycles, and collection
+    resumes, in its previous state, when the call returns."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 _NOOP = 4
 
 
@@ -97,6 +115,20 @@ def _canon(sb: bytes, A: int, K: int, enc: int = 0) -> bytes:
         if h != 0xFF:
             b[2 * A + a] = new_of[h]
     return bytes(b)
+
+
+_CODES: Dict[int, np.ndarray] = {}
+
+
+def _codes_array(codes) -> np.ndarray:
+    """u8 [len, agents] of a candidate list; kept for the fixed get_actions lists (_CAND)."""
+    c = _CODES.get(id(codes))
+    if c is not None and c.shape[0] == len(codes):
+        return c
+    c = np.array(codes, np.uint8).reshape(len(codes), -1)
+    if any(codes is v for v in _CAND.values()):
+        _CODES[id(codes)] = c
+    return c
 
 
 def _cost(action) -> float:  # E2E_BRTDP.cost (e2e_brtdp.py:816-826): 1.0, + 0.1 per moving agent, in order
@@ -203,34 +235,52 @@ class _Expander:
 
     def run(self, requests):
         out, chunk, nrows, subs = [], [], 0, {}
+        key_of = {}  # id(sub) -> its bytes: the requests hold their subtask rows alive for this call
         for req in requests:
             n = len(req[1])
-            key = bytes(req[2])
+            sub = req[2]
+            key = key_of.get(id(sub))
+            if key is None:
+                key = key_of[id(sub)] = bytes(sub)
             if chunk and (nrows + n > self.ROWS or (key not in subs and len(subs) == capi.MAX_SUBTASKS)):
                 out += self._launch(chunk, subs)
                 chunk, nrows, subs = [], 0, {}
-            subs.setdefault(key, (len(subs), req[2]))
-            chunk.append(req)
+            if key not in subs:
+                subs[key] = (len(subs), sub)
+            chunk.append((req, subs[key][0]))
             nrows += n
         if chunk:
             out += self._launch(chunk, subs)
         return out
 
-    def _launch(self, reqs, subs):
+    def _launch(self, chunk, subs):
+        """One oc_rollout launch over the chunk's requests, packed with whole-array copies: the
+        states repeated per candidate row, each (candidate list, agents) group's action codes
+        scattered at once."""
         hi, ha, hal = self._hi, self._ha, self._hal
-        r0, spans = 0, []
-        for state, codes, sub in reqs:
-            n = len(codes)
-            hi[:, r0:r0 + n] = state[:, None]
-            ha[:, r0:r0 + n] = _NOOP
-            for r, c in enumerate(codes):
-                for q in range(sub.num_agents):
-                    ha[sub.agent[q], r0 + r] = c[q]
-            hal[r0:r0 + n] = subs[bytes(sub)][0]
-            spans.append((r0, n))
-            r0 += n
-        n = r0
+        counts = np.fromiter((len(req[1]) for req, _ in chunk), np.int64, len(chunk))
+        starts = np.zeros(len(chunk), np.int64)
+        np.cumsum(counts[:-1], out=starts[1:])
+        n = int(counts.sum())
+        hi[:, :n] = np.repeat(np.stack([req[0] for req, _ in chunk]), counts, axis=0).T
         hi[self.t_plane:, :n] = 0  # t and flags: copied through by the kernel, not part of a planner state
+        ha[:, :n] = _NOOP
+        hal[:n] = np.repeat(np.fromiter((si for _, si in chunk), np.uint8, len(chunk)), counts)
+        groups, agents_of = {}, {}
+        for (req, _), s0 in zip(chunk, starts.tolist()):
+            codes, sub = req[1], req[2]
+            ag = agents_of.get(id(sub))
+            if ag is None:
+                ag = agents_of[id(sub)] = tuple(sub.agent[:sub.num_agents])
+            g = groups.get((id(codes), ag))
+            if g is None:
+                g = groups[(id(codes), ag)] = (codes, ag, [])
+            g[2].append(s0)
+        for codes, ag, s0s in groups.values():
+            c = _codes_array(codes)
+            rows = (np.asarray(s0s)[:, None] + np.arange(len(codes))[None, :]).ravel()
+            for q, a in enumerate(ag):
+                ha[a, rows] = np.tile(c[:, q], len(s0s))
         table = [sub for _, sub in sorted(subs.values(), key=lambda v: v[0])]
         self._d_in.copy_(self._h_in_all, non_blocking=True)  # one H2D
         lib, eb = self.eb.lib, self.eb
@@ -241,13 +291,10 @@ class _Expander:
         self.rows_done += n
         self._h_out_all.copy_(self._d_out, non_blocking=True)  # one D2H
         torch.cuda.current_stream(eb.device).synchronize()
-        ho, hf, hl = self._ho, self._hf, self._hl
-        res = []
-        for r0, n in spans:
-            nxt = ho[:, r0:r0 + n].T.copy()
-            nxt[:, self.t_plane:] = 0
-            res.append((nxt, hf[r0:r0 + n].copy(), hl[r0:r0 + n].copy()))
-        return res
+        nxt = self._ho[:, :n].T.copy()  # [n, NP]: each request's rows are a contiguous slice
+        nxt[:, self.t_plane:] = 0
+        fl, lb = self._hf[:n].copy(), self._hl[:n].copy()
+        return [(nxt[s0:s0 + c], fl[s0:s0 + c], lb[s0:s0 + c]) for s0, c in zip(starts.tolist(), counts.tolist())]
 
 
 def _copy_crashes(sb: bytes, A: int) -> bool:
@@ -300,7 +347,6 @@ class E2E_BRTDP:
         self._exp = None
         self._exp_key = None
         self._succ: Dict = {}  # (state key, subtask key) -> [actions, successors, costs, value keys, goal flags, lower bounds, initialised]
-        self._reprs: Dict = {}  # state key -> the reference's env repr of that state (value-table key)
         self._tmemo: Dict = {}  # this object's T memo: (repr, action) -> successor (bytes, groups)
         self._illegal: Dict = {}  # (state key, subtask key) -> {action outside get_actions: (next bytes, flags)}
 
@@ -451,12 +497,8 @@ class E2E_BRTDP:
         tables are keyed by (repr, subtask) as the reference's are, so that planners of
         different agent sets or levels meet in them exactly where the reference's do (the
         delegator's planner and its copies share one table pair)."""
-        r = self._reprs.get(key)
-        if r is None:
-            sb, groups, agents, lvl = key
-            r = (sb, groups, None if lvl or len(agents) == self._exp.A else agents)
-            self._reprs[key] = r
-        return r
+        sb, groups, agents, lvl = key
+        return (sb, groups, None if lvl or len(agents) == self._exp.A else agents)
 
     # ---- values (value_init, e2e_brtdp.py:678-729) --------------------------------------------
     def _value_init(self, key, goal: bool, lb: float) -> None:
@@ -483,6 +525,8 @@ class E2E_BRTDP:
     def _expanded(self, key, cand, res) -> None:
         nxt, fl, lb = res
         sb, groups, agents, lvl = key
+        if _native is not None and self.use_native and fl.dtype == np.uint8 and lb.dtype == np.float32:
+            return self._expanded_native(key, cand, nxt, fl, lb)
         NP, K, A, enc = len(sb), self._exp.K, self._exp.A, self._exp.enc
         l0, m0 = 3 * A, 3 * A + K
         raw = nxt.tobytes()
@@ -492,12 +536,13 @@ class E2E_BRTDP:
         illegal = {}
         crash = None
         fl, lb = fl.tolist(), lb.tolist()  # Python ints / floats (the f32 bounds exactly)
+        LEGAL, ASSERT, GOAL = capi.ROLL_LEGAL, capi.ROLL_ASSERT, capi.ROLL_GOAL
         for r, c in enumerate(cand):
             f = fl[r]
-            if not f & capi.ROLL_LEGAL:
+            if not f & LEGAL:
                 illegal[c] = r
                 continue
-            if f & capi.ROLL_ASSERT:  # T raises (e2e_brtdp.py:143)
+            if f & ASSERT:  # T raises (e2e_brtdp.py:143)
                 raise AssertionError("action {} led to co-located subtask agents".format(c))
             ns = raw[r * NP:(r + 1) * NP]
             ng = groups
@@ -510,18 +555,35 @@ class E2E_BRTDP:
                 crash.add(len(actions))
             actions.append(c)
             succ.append(nk)
-            goals.append(bool(f & capi.ROLL_GOAL))
+            goals.append(bool(f & GOAL))
             lbs.append(lb[r])
         # T's value_init of a successor runs when T is first asked for it (e2e_brtdp.py:145-148):
         # all of them by _init_succ on the first full Q pass, one by T / _expected_diff before
         # that, so that value tables shared between planners fill in the reference's order.
         # [actions, successor keys, costs, successor value keys, goal flags, bounds,
         #  successors initialised, copy-crash action indices, this state's value key]
-        rep = self._repr
-        self._succ[(key, sk)] = [actions, succ, [_COST[c] for c in actions], [(rep(nk), sk) for nk in succ],
-                                 goals, lbs, False, crash, (rep(key), sk)]
-        if illegal:  # what T would do with them (only asked for by taken_action_error)
-            self._illegal[(key, sk)] = {c: (raw[r * NP:(r + 1) * NP], int(fl[r])) for c, r in illegal.items()}
+        ra = None if lvl or len(agents) == A else agents  # _repr's agents entry, the same for every successor
+        self._succ[(key, sk)] = [actions, succ, [_COST[c] for c in actions], [((nk[0], nk[1], ra), sk) for nk in succ],
+                                 goals, lbs, False, crash, ((sb, groups, ra), sk)]
+        if illegal:  # what T would do with them (only asked for by taken_action_error): decoded there
+            self._illegal[(key, sk)] = (illegal, raw, NP, fl)
+
+    def _expanded_native(self, key, cand, nxt, fl, lb) -> None:
+        """_expanded with the row loop in C (_brtdp.expand): the same entry, field for field."""
+        groups = key[1]
+        A, K, enc = self._exp.A, self._exp.K, self._exp.enc
+        l0, m0 = 3 * A, 3 * A + K
+
+        def changed(ns):  # a chop or a merge: canonical slot order, a merge's new object group
+            ns = _canon(ns, A, K, enc)
+            return ns, groups | frozenset(_group_name(m, enc) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
+        sk = self._sub_key
+        nxt = np.ascontiguousarray(nxt)
+        entry, illegal = _native.expand(nxt, np.ascontiguousarray(fl), np.ascontiguousarray(lb), cand, key, sk, m0, K,
+                                        A, _COST, changed)
+        self._succ[(key, sk)] = entry
+        if illegal:
+            self._illegal[(key, sk)] = (illegal, nxt.reshape(-1), len(key[0]), fl)
 
     def _drive(self, gen):
         """Run a search generator to completion, one launch per request."""
@@ -545,9 +607,18 @@ class E2E_BRTDP:
         if got[7]:
             _raise_copy_crash(got[0][min(got[7])])
         v_l, v_u = self.v_l, self.v_u
-        for nk, vk, g, lb in zip(got[1], got[3], got[4], got[5]):
-            if vk not in v_l or vk not in v_u:
-                self._value_init(nk, g, lb)
+        tc = self.time_cost + self.action_cost
+        for vk, g, lb in zip(got[3], got[4], got[5]):  # _value_init of each, inlined (same arithmetic)
+            if vk in v_l and vk in v_u:
+                continue
+            if g:
+                v_l[vk] = 0.0
+                v_u[vk] = 0.0
+                continue
+            lower = lb * tc
+            assert lower > 0, "lower: {}".format(lower)
+            v_l[vk] = lower - 1.09
+            v_u[vk] = lower * 5 * tc
         got[6] = True
 
     def T(self, key, action):  # e2e_brtdp.py:103-149
@@ -724,7 +795,8 @@ class E2E_BRTDP:
         """The next (joint) action for the subtask agents, as the reference's
         ``get_next_action`` returns it: a (dx, dy) tuple for one agent, a pair of them for two,
         ``None`` when the start state already satisfies the subtask."""
-        return self._drive(self._next_action(env, subtask, subtask_agent_names, other_agent_planners))
+        with searching():
+            return self._drive(self._next_action(env, subtask, subtask_agent_names, other_agent_planners))
 
     def taken_action_error(self, key, action) -> Optional[type]:
         """For an action outside get_actions(key): the exception the reference raises on
@@ -736,9 +808,11 @@ class E2E_BRTDP:
 
     def _taken_action_error_gen(self, key, action):
         yield from self._need(key)
-        got = self._illegal.get((key, self._sub_key), {})
-        if action not in got:
+        ill = self._illegal.get((key, self._sub_key))
+        if ill is None or action not in ill[0]:
             return None
+        r, raw, NP, fl = ill[0][action], ill[1], ill[2], ill[3]
+        got = {action: (bytes(raw[r * NP:(r + 1) * NP]), int(fl[r]))}
         if (self._repr(key), action) in self._tmemo:  # T answers from its memo; the assert raises
             return AssertionError
         ns, f = got[action]
@@ -892,6 +966,11 @@ def plan_batch(planners: Sequence[E2E_BRTDP], envs_, subtasks, agent_names, othe
     if len(keys) != 1:
         raise ValueError("plan_batch: the searches must share one level, agent count and device "
                          "(they share one expander); got %d different ones" % len(keys))
+    with searching():
+        return _plan_batch(planners, envs_, subtasks, agent_names, others)
+
+
+def _plan_batch(planners, envs_, subtasks, agent_names, others) -> list:
     gens = [p._next_action(e, st, an, o) for p, e, st, an, o in zip(planners, envs_, subtasks, agent_names, others)]
     out = [None] * len(gens)
     pending = {}
