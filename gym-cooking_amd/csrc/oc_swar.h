@@ -52,9 +52,11 @@ OC_SW uint32_t or3(uint32_t a, uint32_t b, uint32_t c) { return bop3<OC_LUT(a | 
 OC_SW uint32_t andn(uint32_t a, uint32_t b) { return bop3<OC_LUT(a & !b)>(a, b, 0u); }  // a & ~b
 OC_SW uint32_t perm(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_perm(hi, lo, s); }
 
-// h80 -> full mask per byte: 0x80 -> 0xFF, carry-free.  Written as h | (h - (h >> 7)):
-// the equivalent (s << 8) - s is turned into a quarter-rate v_mul_lo_u32 by the compiler.
-OC_SW uint32_t full80(uint32_t h) { return h | (h - (h >> 7)); }
+// h80 -> full mask per byte: 0x80 -> 0xFF, 0x00 -> 0x00.  One v_perm_b32 with h as the
+// selector: a selector byte >= 13 (0x80) yields 0xFF, and 0 picks byte 0 of the zero source
+// (h | (h - (h >> 7)), the carry-free arithmetic form, takes three instructions).  Every h
+// passed here has only bit 7 of a byte set.
+OC_SW uint32_t full80(uint32_t h) { return perm(0u, 0u, h); }
 // bytes <= 0x7F: h80 of (byte != 0) / (byte == 0)
 OC_SW uint32_t nz80(uint32_t x) { return (x + k7F) & k80; }
 OC_SW uint32_t z80(uint32_t x) { return andn(k80, x + k7F); }
