@@ -262,17 +262,30 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         const uint32_t isC80 = (cls[k] << 2) & k80;
         const uint32_t h = H[k];
         const uint32_t hold80 = andn(k80, h);  // slot index < 0x80, none = 0xFF
-        // un-held items at tc (a non-Delivery cell holds at most one; held items sit on Floor)
-        uint32_t at80[K], seen = 0u, ob0 = 0u, ob1 = 0u, ob2 = 0u, ob3 = 0u;
+        // un-held items at tc (a non-Delivery cell holds at most one; held items sit on Floor).
+        // ne[j] has bit 7 set where slot j is NOT at tc, so the ORs over slots are ANDs of ne
+        // (one bitop3 per three slots) and each slot costs two instructions, not three.
+        uint32_t ne[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            at80[j] = big ? zf80(Lc[j] ^ tc) : eq80(Lc[j], tc);
-            seen |= at80[j];
-            if (j & 1) ob0 |= at80[j];
-            if (j & 2) ob1 |= at80[j];
-            if (j & 4) ob2 |= at80[j];
-            if (j & 8) ob3 |= at80[j];
+            if (big)
+                ne[j] = ~zf80(Lc[j] ^ tc);
+            else
+                ne[j] = bop3<OC_LUT((a ^ b) & c)>(Lc[j], tc, k7F) + k7F;  // bit 7: low 7 bits differ
         }
+        // h80 of "some slot of the set is at tc": bit 7 of ~AND(ne over the set)
+        auto any_at = [&](auto pick) -> uint32_t {
+            uint32_t all = 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                if (pick(j)) all &= ne[j];
+            return andn(k80, all);
+        };
+        const uint32_t seen = any_at([](int) { return true; });
+        const uint32_t ob0 = any_at([](int j) { return (j & 1) != 0; });
+        const uint32_t ob1 = any_at([](int j) { return (j & 2) != 0; });
+        const uint32_t ob2 = K > 4 ? any_at([](int j) { return (j & 4) != 0; }) : 0u;
+        const uint32_t ob3 = K > 8 ? any_at([](int j) { return (j & 8) != 0; }) : 0u;
         const uint32_t so1 = (ob0 >> 5) | kLanes;                            // (o & 1) * 4 + q
         const uint32_t sh = bop3<OC_LUT((a & b) | c)>(h << 2, k04, kLanes);  // (h & 1) * 4 + q
         uint32_t om, hm, hl;
@@ -291,38 +304,41 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         }
 
         const uint32_t nf = andn(go80, isF80), mv = go80 & isF80;
-        uint32_t two, allch, plate_ok, food_ok, nch, cu, chopped;
+        // Content predicates as "raw" words: only bit 7 of each byte carries the predicate (or
+        // its negation, n*_r); the other bits are don't-care, because every use ANDs it with a
+        // clean h80 word (nfh, cnt, empty), which saves the per-predicate & 0x80.
+        uint32_t two_r, nallch_r, nplate_r, nfood_r, nch_r, cu, chopped;
         if (counts) {  // wave-uniform: OC_ENC_COUNTS masks (T/L/O 2-bit counts, 0x40 Plate, 0x80 Fresh)
             const uint32_t x = hm & k7F;
             // >= 2 contents: the count bits are not a single unit (0x01, 0x04, 0x10, 0x40) nor zero;
             // ((x | 0x80) - 1) & x clears the lowest set bit without a borrow into the next env
-            two = nz80(bop3<OC_LUT((a & b) | c)>((x | k80) - k01, x, x & 0x2A2A2A2Au));
-            allch = k80;  // a merged object is all-Chopped (mergeable admits last-state foods only)
-            plate_ok = z80(and3(hm, om, 0x40404040u));
-            food_ok = andn(k80, hm | om);  // no Fresh food on either side
-            nch = hm & k80;                // Object.needs_chopped: a single fresh food
-            cu = x + (om & k7F);           // contents add up; every field sum stays in its bits
-            chopped = x;                   // Object.chop: the Fresh bit goes
+            two_r = bop3<OC_LUT((a & b) | c)>((x | k80) - k01, x, x & 0x2A2A2A2Au) + k7F;
+            nallch_r = 0u;  // a merged object is all-Chopped (mergeable admits last-state foods only)
+            nplate_r = and3(hm, om, 0x40404040u) + k7F;
+            nfood_r = hm | om;  // a Fresh food on either side
+            nch_r = hm;         // Object.needs_chopped: a single fresh food (bit 7 = Fresh)
+            cu = x + (om & k7F);  // contents add up; every field sum stays in its bits
+            chopped = x;          // Object.chop: the Fresh bit goes
         } else {
             // Object.is_deliverable (core.py:214-219): >= 2 contents, all foods chopped
             const uint32_t c4 = hm & k0F;
-            two = nz80(((c4 | k80) - k01) & c4);
-            allch = z80(bop3<OC_LUT((!a) & b & c)>(hm >> 4, hm, k07));
+            two_r = (((c4 | k80) - k01) & c4) + k7F;
+            nallch_r = bop3<OC_LUT((!a) & b & c)>(hm >> 4, hm, k07) + k7F;
             // mergeable (core.py:222-241): <= 1 plate, every food chopped
             cu = hm | om;
-            plate_ok = z80(and3(hm, om, k08));
-            food_ok = z80(bop3<OC_LUT((!a) & b & c)>(cu >> 4, cu, k07));
+            nplate_r = and3(hm, om, k08) + k7F;
+            nfood_r = bop3<OC_LUT((!a) & b & c)>(cu >> 4, cu, k07) + k7F;
             // Object.needs_chopped (core.py:176-178): exactly one content, a fresh food
-            nch = bop3<OC_LUT(a & !b & c)>(nz80(c4), two, z80(hm & k78));
+            nch_r = bop3<OC_LUT(a & !b & !c)>(c4 + k7F, two_r, (hm & k78) + k7F);
             // Object.chop (core.py:187-192): the single food's chopped bit (bits 4..6, no cross-byte spill)
             chopped = bop3<OC_LUT((a & b) | c)>(hm << 4, 0x70707070u, hm);
         }
         const uint32_t nfh = nf & hold80;
-        const uint32_t deliver = and3(nfh & isD80, two, allch);                  // :35-40
+        const uint32_t deliver = bop3<OC_LUT(a & b & !c)>(nfh & isD80, two_r, nallch_r);  // :35-40
         const uint32_t cnt = andn(nfh, isD80);
-        const uint32_t merge = and3(cnt, seen, plate_ok & food_ok);              // :43-56
-        const uint32_t empty = andn(cnt, seen);                                  // :60-70
-        const uint32_t chop = and3(empty, isC80, nch);
+        const uint32_t merge = bop3<OC_LUT(a & b & !c)>(cnt, seen, nplate_r | nfood_r);    // :43-56
+        const uint32_t empty = andn(cnt, seen);                                              // :60-70
+        const uint32_t chop = and3(empty, isC80, nch_r);
         const uint32_t put = andn(empty, chop);
         const uint32_t pick = andn(bop3<OC_LUT(a & !b & c)>(nf, hold80, seen), isD80);  // :73-84
         const uint32_t reloc = or3(mv, deliver, put);  // the held item ends on tc
