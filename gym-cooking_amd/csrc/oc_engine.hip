@@ -1103,9 +1103,6 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     for (int c = 0; c < W * H; ++c) {
         const int t = lv->tiles[c];
         if (t < OC_TILE_FLOOR || t > OC_TILE_DELIVERY) return fail(OC_ELEVEL, "tile %d at cell %d", t, c);
-        const int x = c % W, y = c / W;
-        if (t == OC_TILE_FLOOR && (x == 0 || y == 0 || x == W - 1 || y == H - 1))
-            return fail(OC_ELEVEL, "Floor on the border at (%d,%d)", x, y);
         L.cls4[c >> 2] |= (uint32_t)ocsw::tile_class(t) << (8 * (c & 3));
         if (t == OC_TILE_DELIVERY && L.done_cell < 0) L.done_cell = c;
     }
@@ -1157,7 +1154,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     for (int c = 0; c < 5; ++c) L.dcell_lut |= (uint64_t)((dcell[c] + 128) & 0xFF) << (8 * c);
     if (max_T > 0x7FFF) return fail(OC_EINVAL, "max_T %d > 32767", max_T);
     ocsw::build_swar_level(L.sw, W, H, L.done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y,
-                           num_agents, cell, mask, lv->encoding);
+                           num_agents, cell, mask, lv->encoding, lv->tiles);
     oc_handle* h = new oc_handle;
     h->level = *lv;
     h->A = num_agents;
@@ -1255,7 +1252,8 @@ int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
 // The step kernels: 4-slot levels of the common class (H <= 8, W*H <= 128, presence masks:
 // every shipped kitchen) take the MODE 0 build of the SWAR step, everything else MODE 1.
 #define OC_DISPATCH_STEP(h_, LAUNCH)                                                        \
-    if ((h_)->K == 4 && !(h_)->args.sw.tall && !(h_)->args.sw.big && !(h_)->args.sw.counts) {  \
+    if ((h_)->K == 4 && !(h_)->args.sw.tall && !(h_)->args.sw.big && !(h_)->args.sw.counts &&  \
+        !(h_)->args.sw.edge) {                                                              \
         switch ((h_)->A) {                                                                  \
             case 1: LAUNCH(1, 4, 0); break;                                                 \
             case 2: LAUNCH(2, 4, 0); break;                                                 \

@@ -82,16 +82,25 @@ struct SwarLevel {
     uint32_t dp_lo, dp_hi, dn_lo, dn_hi;  // big: v_perm LUTs action code -> max(delta, 0), max(-delta, 0)
     int32_t counts;          // item masks in OC_ENC_COUNTS (a food type repeats on the map): the
                              // content predicates below read 2-bit counts, a plate bit and a Fresh bit
+    int32_t edge;            // a Floor square on the grid's border: an action can point off the grid
+    uint32_t wm1_rep, hm1_rep;  // W - 1, H - 1 replicated (the off-grid test)
 };
 
 // Host-side construction of the SwarLevel constants (called by oc_create after validation).
 // cell/mask: item slot templates (OC_LOC_DEAD / 0 past the level's items).
 __host__ __device__ inline void build_swar_level(SwarLevel& S, int W, int H, int done_cell, const uint8_t* goal_mask,
                              int ngoals, int max_T, const uint8_t* spawn_x, const uint8_t* spawn_y,
-                             int num_agents, const uint8_t* cell, const uint8_t* mask, int encoding) {
+                             int num_agents, const uint8_t* cell, const uint8_t* mask, int encoding,
+                             const uint8_t* tiles) {
     S = SwarLevel{};
     S.W = (uint32_t)W;
     S.counts = encoding != 0;
+    for (int c = 0; c < W * H; ++c) {
+        const int x = c % W, y = c / W;
+        if (tiles[c] == 0 && (x == 0 || y == 0 || x == W - 1 || y == H - 1)) S.edge = 1;  // OC_TILE_FLOOR
+    }
+    S.wm1_rep = (uint32_t)(W - 1) * 0x01010101u;
+    S.hm1_rep = (uint32_t)(H - 1) * 0x01010101u;
     S.tall = H > 8;
     S.big = W * H > 128;
     const int dcell[5] = {W, -W, -1, 1, 0};
@@ -198,16 +207,44 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
                  uint32_t& pending) {
     const bool tall = MODE ? (bool)L.tall : false, big = MODE ? (bool)L.big : false;
     const bool counts = MODE ? (bool)L.counts : false;
+    const bool edge = MODE ? (bool)L.edge : false;
     const uint32_t rst = full80((F << 7) & k80);  // input DONE => next-step auto-reset
 
     // ---- positions, next squares, collidability (is_collision :692-700) ----
-    uint32_t act[A], loc[A], nraw[A], cls[A], nn80[A], bump80[A], nxt[A], blk80[A];
+    uint32_t act[A], loc[A], nraw[A], cls[A], nn80[A], bump80[A], nxt[A], blk80[A], out80[A];
 #pragma unroll
     for (int a = 0; a < A; ++a) {
         uint32_t c = ACT[a];
         const uint32_t ge5 = bop3<OC_LUT((a | b) & c)>((c & k7F) + 0x7B7B7B7Bu, c, k80);
-        c = sel(full80(ge5), k04, c);  // codes > 4 act as (0, 0)
-        act[a] = c;
+        act[a] = sel(full80(ge5), k04, c);  // codes > 4 act as (0, 0)
+        out80[a] = 0u;
+    }
+    // A Floor on the border (wave-uniform): an action can point off the grid.  is_collision
+    // looks the unclamped square up (get_gridsquare_at asserts there is exactly one: it
+    // raises, :692-700), so with two or more agents such a step raises in check_collisions
+    // before anything moves: the env gets DONE | ERR with its state unchanged but t (as the
+    // copy crash), every action a no-op.  With one agent there is no pair
+    // to check, and interact's World.inbounds clamps the square to the agent's own (no move).
+    uint32_t raise80 = 0u;
+    if (edge) {
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            const uint32_t c = act[a];
+            out80[a] = or3(and3(z80(c), z80(Y[a] ^ L.hm1_rep), k80), and3(z80(c ^ k01), z80(Y[a]), k80),
+                           and3(z80(c ^ 0x02020202u), z80(X[a]), k80) | and3(z80(c ^ 0x03030303u), z80(X[a] ^ L.wm1_rep), k80));
+            if (A >= 2) raise80 |= out80[a];
+        }
+        if (A >= 2) {
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                act[a] = sel(full80(raise80), k04, act[a]);
+                out80[a] = 0u;
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        const uint32_t c = act[a];
         nn80[a] = nz80(c ^ k04);
         uint32_t yw;
         if (tall)  // wave-uniform: H > 8 rows
@@ -219,6 +256,7 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
             nraw[a] = loc[a] + perm(L.dp_hi, L.dp_lo, c) - perm(L.dn_hi, L.dn_lo, c);
         else  // cells < 128: loc + (delta + 0x80) stays in its byte, bias removed
             nraw[a] = (loc[a] + perm(L.dc_hi, L.dc_lo, c)) ^ k80;
+        if (edge) nraw[a] = sel(full80(out80[a]), loc[a], nraw[a]);  // World.inbounds (one agent)
         cls[a] = cls_of(nraw[a]);
         const uint32_t onF80 = cls[a] & k80;
         nxt[a] = sel(full80(onF80), nraw[a], loc[a]);
@@ -249,6 +287,8 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
             cm |= (bi | bj) >> (7 - p);
         }
     }
+
+    if (edge && A >= 2) cm = andn(cm, full80(raise80));  // a raising step logs no collision (build-defined)
 
     // ---- execute_navigation: interact per agent, in order (:767-770, interact.py:4-89) ----
     uint32_t dlv = 0u;  // h80: some agent delivered
@@ -303,7 +343,7 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
             hl = gather<K>(Lc, sh, fh1, fh2, fh3);
         }
 
-        const uint32_t nf = andn(go80, isF80), mv = go80 & isF80;
+        const uint32_t nf = andn(go80, isF80), mv = andn(go80 & isF80, out80[k]);  // clamped: no move
         // Content predicates as "raw" words: only bit 7 of each byte carries the predicate (or
         // its negation, n*_r); the other bits are don't-care, because every use ANDs it with a
         // clean h80 word (nfh, cnt, empty), which saves the per-predicate & 0x80.
@@ -396,6 +436,7 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
             const uint32_t same = z80(bop3<OC_LUT((a ^ b) | c)>(X[i], X[j], Y[i] ^ Y[j]));
             err |= and3(same, andn(k80, H[i]), andn(k80, H[j]));
         }
+    err |= raise80;
 
     // ---- done() (:316-363) and reward() (:365-376) ----
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));

@@ -506,6 +506,13 @@ class OvercookedEnvironment:
             raise RuntimeError("call reset() before step()")
         names = self.get_agent_names()
         codes = [action_code(action_dict[n]) for n in names]
+        if eng.A >= 2 and self.level.edge:  # check_collisions' unclamped lookup (:692-700)
+            for a in self.sim_agents:
+                x, y = a.location
+                if self.level.off_grid(x, y, codes[names.index(a.name)]):
+                    self.t += 1  # step increments t before it raises (:257)
+                    dx, dy = _levels.ACTIONS[codes[names.index(a.name)]]
+                    raise AssertionError("0 gridsquares at {}: []".format((x + dx, y + dy)))  # world.py:429
         pre = self._host
         new, ex, coll = eng.step(pre, codes)
         t_now = self.t + 1

@@ -244,6 +244,17 @@ class Level:
                     out[name] += 1
         return out
 
+    @property
+    def edge(self) -> bool:
+        """Some Floor square lies on the grid's border (an action there can point off it)."""
+        W, H = self.width, self.height
+        return any(t == TILE_FLOOR and (c % W in (0, W - 1) or c // W in (0, H - 1)) for c, t in enumerate(self.tiles))
+
+    def off_grid(self, x: int, y: int, code: int) -> bool:
+        """Action `code` from (x, y) points outside the grid (World.NAV_ACTIONS order + no-op)."""
+        dx, dy = ((0, 1), (0, -1), (-1, 0), (1, 0), (0, 0))[min(code, 4)]
+        return not (0 <= x + dx < self.width and 0 <= y + dy < self.height)
+
     def tile_at(self, x: int, y: int) -> int:
         return self.tiles[y * self.width + x]
 
@@ -301,18 +312,10 @@ class Level:
         if len(self.goals) > MAX_GOALS:
             raise ValueError("too many goals")
         self.delivery_cell  # noqa: B018 -- raises if absent
-        # is_collision indexes loc+action without clamping (overcooked_environment.py:692-700):
-        # a Floor on the border would let an agent look outside the grid, where the
-        # reference raises.  Every reference level has a non-Floor border.
+        # A Floor on the border is allowed: is_collision looks the unclamped next square up
+        # (overcooked_environment.py:692-700), so with 2+ agents an action off the grid makes
+        # step raise (the engine's ERR, include/oc_engine.h), and interact clamps it for one.
         W, H = self.width, self.height
-        for x in range(W):
-            for y in (0, H - 1):
-                if self.tile_at(x, y) == TILE_FLOOR:
-                    raise ValueError("level %s: Floor on border at (%d,%d)" % (self.name, x, y))
-        for y in range(H):
-            for x in (0, W - 1):
-                if self.tile_at(x, y) == TILE_FLOOR:
-                    raise ValueError("level %s: Floor on border at (%d,%d)" % (self.name, x, y))
         for (x, y) in self.spawns[:num_agents]:
             if not (0 <= x < W and 0 <= y < H) or self.tile_at(x, y) != TILE_FLOOR:
                 raise ValueError("level %s: spawn (%d,%d) is not a Floor" % (self.name, x, y))

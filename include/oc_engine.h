@@ -93,9 +93,13 @@ extern "C" {
 /* flags plane bits */
 #define OC_FLAG_DONE 0x01u    /* done() returned True (overcooked_environment.py:316-363) */
 #define OC_FLAG_SUCCESS 0x02u /* reward() == 1 (overcooked_environment.py:365-376) */
-#define OC_FLAG_ERR 0x04u     /* the reference raises at new_obs = copy.copy(self)
-                                 (overcooked_environment.py:289 -> :108-113 -> world.py:417):
-                                 two co-located agents both holding.  ERR implies DONE. */
+#define OC_FLAG_ERR 0x04u     /* the reference's step raises: at new_obs = copy.copy(self)
+                                 (overcooked_environment.py:289 -> world.py:417) when two
+                                 co-located agents both hold, or, on a level with a Floor on its
+                                 border and two or more agents, in check_collisions when an action
+                                 points off the grid (is_collision :692-700 -> get_gridsquare_at
+                                 asserts, world.py:429; the state is then unchanged but t, the
+                                 executed actions no-ops).  ERR implies DONE. */
 
 /* per-GPU episode statistics (oc_stats_reduce output, uint64 each) */
 #define OC_STAT_EPISODES 0   /* envs whose episode ended this window (DONE newly set) */
@@ -106,7 +110,7 @@ extern "C" {
 #define OC_NSTATS 5
 
 typedef struct oc_level_desc {
-    int32_t width, height;           /* 3..; width*height <= OC_MAX_CELLS; non-Floor border */
+    int32_t width, height;           /* 3..; width*height <= OC_MAX_CELLS */
     int32_t num_items;               /* <= OC_MAX_ITEMS; OC_ENC_PRESENCE: at most one of each food
                                         type, OC_ENC_COUNTS: at most OC_MC_MAX_PER_FOOD */
     int32_t num_spawns;              /* >= num_agents */

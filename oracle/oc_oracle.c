@@ -69,7 +69,7 @@ static int action_code(Loc a) {
 }
 
 /* World.get_gridsquare_at (world.py:421-430): the unique GridSquare at location. The
- * reference asserts when there is none (off-grid); level validation excludes that. */
+ * reference asserts when there is none (off-grid); step_one catches that case first. */
 static int gridsquare_at(const Env* e, Loc l) {
     if (l.x < 0 || l.y < 0 || l.x >= e->L->width || l.y >= e->L->height) abort();
     const int c = l.y * e->L->width + l.x;
@@ -454,6 +454,20 @@ static void step_one(const Cfg* c, const uint8_t* sin, uint8_t* sout, const uint
     for (int a = 0; a < c->A; ++a) { /* :263-264 */
         int code = act[a * P + e];
         env.agents[a].action = NAV[code > OC_ACT_NOOP ? OC_ACT_NOOP : code];
+    }
+    if (c->A >= 2) { /* check_collisions -> is_collision looks up the unclamped next square */
+        int off = 0;
+        for (int a = 0; a < c->A; ++a) {
+            Loc n = loc_add(env.agents[a].location, env.agents[a].action);
+            off |= n.x < 0 || n.y < 0 || n.x >= c->L->width || n.y >= c->L->height;
+        }
+        if (off) { /* get_gridsquare_at asserts (world.py:429): step raises before anything moves */
+            pack(c, &env, OC_FLAG_DONE | OC_FLAG_ERR, sout, e); /* t advanced (:257), nothing else */
+            for (int a = 0; a < c->A; ++a)
+                if (exec_out) exec_out[a * P + e] = OC_ACT_NOOP;
+            if (coll_out) coll_out[e] = 0;
+            return;
+        }
     }
     int cmask = check_collisions(&env); /* :267 */
     int ex[OC_MAX_AGENTS];

@@ -52,7 +52,7 @@ static void run(const oc_level_desc* lv, int max_T, const uint8_t* sin, uint8_t*
     for (int j = 0; j < 16; ++j) { cell[j] = j < lv->num_items ? lv->item_cell[j] : 0xFF; mask[j] = j < lv->num_items ? lv->item_mask[j] : 0; }
     ocsw::SwarLevel S;
     ocsw::build_swar_level(S, W, H, done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y, A, cell, mask,
-                           lv->encoding);
+                           lv->encoding, lv->tiles);
     auto cls_of = [&](uint32_t cells) -> uint32_t {
         return (uint32_t)tbl[cells & 0xFF] | ((uint32_t)tbl[(cells >> 8) & 0xFF] << 8) |
                ((uint32_t)tbl[(cells >> 16) & 0xFF] << 16) | ((uint32_t)tbl[cells >> 24] << 24);
@@ -72,7 +72,7 @@ static void run(const oc_level_desc* lv, int max_T, const uint8_t* sin, uint8_t*
         for (int r = 0; r < n; ++r) {
             for (int a = 0; a < A; ++a) AC[a] = rd(act + (int64_t)r * A * P, a, g);
             // the device's dispatch: 4-slot levels of the common class take the MODE 0 build
-            if (K == 4 && !S.tall && !S.big && !S.counts)
+            if (K == 4 && !S.tall && !S.big && !S.counts && !S.edge)
                 ocsw::step4<A, K, 0>(S, X, Y, Hh, Lc, M, T0, T1, F, AC, EX, CM, cls_of,
                                      [](uint32_t v) { return v != 0u; }, pending);
             else

@@ -56,9 +56,13 @@ def test_create_layout_and_validation_without_gpu():
     assert lib.oc_destroy(h) == 0
     # bad levels are rejected with a message
     bad = capi.level_desc(lv, 2)
-    bad.tiles[0] = 0  # Floor on the border
+    bad.tiles[bad.item_cell[0]] = 0  # an item on a Floor square
     assert lib.oc_create(ctypes.byref(bad), 2, 100, 0, ctypes.byref(h)) == capi_err("ELEVEL")
-    assert b"border" in lib.oc_last_error()
+    assert b"not on a counter" in lib.oc_last_error()
+    edge = capi.level_desc(lv, 2)
+    edge.tiles[0] = 0  # a Floor on the border loads (an off-grid action raises in step: ERR)
+    assert lib.oc_create(ctypes.byref(edge), 2, 100, 0, ctypes.byref(h)) == 0
+    assert lib.oc_destroy(h) == 0
     assert lib.oc_create(ctypes.byref(d), 5, 100, 0, ctypes.byref(h)) == capi_err("EINVAL")
 
 
