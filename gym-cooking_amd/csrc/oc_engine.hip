@@ -112,7 +112,7 @@ __device__ __forceinline__ void bst32(__amdgpu_buffer_rsrc_t r, uint32_t v, uint
     __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, CP);
 }
 
-template <int A, int K>
+template <int A, int K, bool kActs = true>
 __device__ __forceinline__ void load_chunk(Chunk<A, K>& c, const Bufs& b, uint32_t P, uint32_t g) {
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
     const uint32_t vo = g * 4u;
@@ -121,7 +121,7 @@ __device__ __forceinline__ void load_chunk(Chunk<A, K>& c, const Bufs& b, uint32
         c.wx[a] = bld32(b.sin, vo, a * P);
         c.wy[a] = bld32(b.sin, vo, (kPY + a) * P);
         c.wh[a] = bld32(b.sin, vo, (kPH + a) * P);
-        c.wa[a] = bld32(b.act, vo, a * P);
+        if (kActs) c.wa[a] = bld32(b.act, vo, a * P);
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -265,6 +265,16 @@ __host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
     return (stat_rows * OC_NSTATS + kTicketStride - 1) / kTicketStride * kTicketStride;
 }
 
+// oc_step_n takes its action words in batches of kActBatch steps: each lane loads a batch's
+// words into registers one batch ahead and parks them in LDS when the batch starts; a step
+// reads its words from LDS.  The compiler waits vmcnt(0) before it consumes a loaded word while
+// stores are outstanding (loads and stores share the counter, and it does not assume they
+// complete in order), i.e. for every store the wave has issued.  With one load per step that was
+// each wave waiting, every step, for the previous step's stores to drain (C3: 6.4 us/step, 5.1
+// with the loads taken out of the loop); with batches it waits once per batch.
+template <int A>
+constexpr int act_batch() { return A >= 4 ? 4 : 8; }  // 2 * A * batch registers <= 32
+
 template <int A, int K, int CP, int LCP, int MODE>
 __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
                                                            uint8_t* __restrict__ sout,
@@ -276,6 +286,8 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
     __shared__ uint32_t tbl4[64];
     __shared__ uint32_t waves_done;
     __shared__ unsigned long long fold[OC_NSTATS][64 + 8];  // the folding wave's partial sums
+    constexpr int kS = act_batch<A>();
+    __shared__ uint32_t actbuf[kBlock / 64][kS * A][64];  // each wave's current action batch
     if (threadIdx.x < 64u) tbl4[threadIdx.x] = L.cls4[threadIdx.x];
     if (threadIdx.x == 0u) waves_done = 0u;
     __syncthreads();
@@ -300,25 +312,39 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
     typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
     for (uint32_t g = blockIdx.x * (uint32_t)kBlock + threadIdx.x; g < nlanes; g += stride) {  // block-uniform
         Chunk<A, K> c;
-        load_chunk<A, K>(c, b, P, g);
+        load_chunk<A, K, false>(c, b, P, g);
         const uint32_t vo = g * 4u;
-        uint32_t T0 = c.wt.x, T1 = c.wt.y, nxt[A];
+        uint32_t T0 = c.wt.x, T1 = c.wt.y;
         uint32_t pending = ocsw::at_done80<K, MODE>(L.sw, c.wl);  // the loaded state: the full path once
         const int64_t rem = L.B - (int64_t)g * kEPL;
         const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (rem <= 0 ? 0u : (1u << (8 * (uint32_t)rem)) - 1u);
+        // action batches: word i of the batch starting at step r0 is agent i % A of step r0 + i / A;
+        // the step offset is in the VGPR offset, so words past step n fall outside the
+        // descriptor's range and read 0 without a memory access
+        uint32_t* const ab = &actbuf[threadIdx.x >> 6][0][threadIdx.x & 63u];
+        uint32_t areg[kS * A];
+        auto load_batch = [&](int r0) {
+            const uint32_t vb = vo + (uint32_t)(r0 * A) * P;
 #pragma unroll
-        for (int a = 0; a < A; ++a) nxt[a] = n > 1 ? bld32<LCP>(b.act, vo, (uint32_t)(A + a) * P) : 0u;
+            for (int i = 0; i < kS * A; ++i)
+                areg[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(b.act, (int)(vb + (uint32_t)i * P), 0, LCP);
+        };
+        auto park_batch = [&]() {
+#pragma unroll
+            for (int i = 0; i < kS * A; ++i) ab[i * 64] = areg[i];
+        };
+        load_batch(0);
+        park_batch();
+        if (n > kS) load_batch(kS);
         for (int r = 0; r < n; ++r) {
+            const int sb = r % kS;
+            if (sb == 0 && r > 0) {  // wave-uniform: a new batch
+                park_batch();
+                if (r + kS < n) load_batch(r + kS);
+            }
             uint32_t act[A], ex[A], cm;
 #pragma unroll
-            for (int a = 0; a < A; ++a) {
-                act[a] = c.wa[a];
-                c.wa[a] = nxt[a];
-            }
-            if (r + 2 < n) {
-#pragma unroll
-                for (int a = 0; a < A; ++a) nxt[a] = bld32<LCP>(b.act, vo, (uint32_t)((r + 2) * A + a) * P);
-            }
+            for (int a = 0; a < A; ++a) act[a] = ab[(sb * A + a) * 64];
             const uint32_t f_in = c.wf;
             const bool full = ocsw::step4<A, K, MODE>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, act, ex,
                                                       cm, cls_of, WaveAny{}, pending);
@@ -1191,15 +1217,16 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     return OC_OK;
 }
 
-int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint8_t* node_of, int64_t node_of_len, uint8_t* dist,
+int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, int64_t node_of_len, uint8_t* dist,
                     int64_t dist_len) {
     if (h == nullptr || num_nodes == nullptr) return fail(OC_EINVAL, "bad argument");
-    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes", ocro::kMaxNodes);
+    if (h->roll.nnodes < 0)
+        return fail(OC_ELEVEL, "reachability graph exceeds %d nodes or a distance of 254", ocro::kMaxNodes);
     const int n = h->roll.nnodes, cells = h->level.width * h->level.height;
     *num_nodes = n;
     if (node_of != nullptr) {
-        if (node_of_len < (int64_t)cells * 5) return fail(OC_EINVAL, "node_of needs %d bytes", cells * 5);
-        for (int i = 0; i < cells * 5; ++i) node_of[i] = h->roll_blob_host[ocro::kNodeOff + i];
+        if (node_of_len < (int64_t)cells * 5) return fail(OC_EINVAL, "node_of needs %d entries", cells * 5);
+        memcpy(node_of, h->roll_blob_host + ocro::kNodeOff, (size_t)cells * 5 * sizeof(uint16_t));
     }
     if (dist != nullptr) {
         if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %d bytes", n * n);
@@ -1381,7 +1408,7 @@ static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num
         if (subtasks[i].level != OC_LEVEL0 && !level1_ok)
             return fail(OC_EINVAL, "subtask %d: only oc_rollout takes OC_LEVEL1", i);
     if (num_subtasks < 1 || num_subtasks > OC_MAX_SUBTASKS) return fail(OC_EINVAL, "num_subtasks %d", num_subtasks);
-    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes", ocro::kMaxNodes);
+    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes or a distance of 254", ocro::kMaxNodes);
     if (h->roll_blob == nullptr) return fail(OC_EHIP, "rollout tables not on the device");
     R.L = h->roll;
     R.nsub = num_subtasks;
@@ -1411,6 +1438,22 @@ static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num
     return OC_OK;
 }
 
+// The planner kernels stage the level's table blob in dynamic LDS.  Past the 64 KB a launch gets
+// by default (graphs of more than ~245 nodes) the kernel must be allowed more, up to the CU's
+// 160 KB; the kernel's static LDS counts against the same limit.
+constexpr int kLdsPerCu = 160 * 1024;
+static int allow_dyn_lds(const void* kernel, int dyn) {
+    if (dyn <= 48 * 1024) return OC_OK;
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, kernel) != hipSuccess) return hip_check("hipFuncGetAttributes");
+    if ((int64_t)fa.sharedSizeBytes + dyn > kLdsPerCu)
+        return fail(OC_ELEVEL, "level tables (%d B) and the kernel's LDS (%d B) exceed %d B", dyn,
+                    (int)fa.sharedSizeBytes, kLdsPerCu);
+    if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, dyn) != hipSuccess)
+        return hip_check("hipFuncSetAttribute");
+    return OC_OK;
+}
+
 int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
                const uint8_t* alloc, const oc_subtask* subtasks, int32_t num_subtasks, uint8_t* out_flags,
                float* lower_bound, int64_t B, void* stream) {
@@ -1427,6 +1470,7 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_ROLL(A, K)                                                                                 \
+    if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K>, h->roll_blob_bytes)) return rc;                 \
     hipLaunchKernelGGL((oc_rollout_kernel<A, K>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,                \
                        (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags,    \
                        lower_bound)
@@ -1454,6 +1498,10 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_LIK(A, K)                                                                                          \
+    if (const int rc = allow_dyn_lds(any_joint ? (const void*)oc_likelihood_kernel<A, K, 32>                          \
+                                               : (const void*)oc_likelihood_kernel<A, K, 8>,                    \
+                                     h->roll_blob_bytes))                                                            \
+        return rc;                                                                                                   \
     if (any_joint)                                                                                                   \
         hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 32>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,          \
                            (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,   \
@@ -1487,6 +1535,7 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
     const dim3 grid((unsigned)bx, (unsigned)chunks);
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_BOUNDS(A, K)                                                                             \
+    if (const int rc = allow_dyn_lds((const void*)oc_bounds_kernel<A, K>, h->roll_blob_bytes)) return rc;                 \
     hipLaunchKernelGGL((oc_bounds_kernel<A, K>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,            \
                        (const uint8_t*)state, h->roll_blob, lower_bound, doable)
     OC_DISPATCH(h->A, h->K, OC_LAUNCH_BOUNDS)

@@ -12,8 +12,9 @@
 // build_roll_level() as a compact all-pairs distance table (u8, 0xFF = no path).  The static
 // tables of a level (tile classes, graph node ids, Cutboard / Delivery lists, distances) form
 // one byte blob that the kernels stage in LDS, sized per level (kBlob*Off + nnodes^2 bytes):
-// a 7x7 kitchen's blob is ~6 KB, the largest (248 nodes) ~63 KB.  Distances and
-// bounds are exact in fp32 (integers and halves < 2^9).
+// a 7x7 kitchen's blob is ~7 KB, the largest (kMaxNodes nodes) ~152 KB, which the kernels get
+// as dynamic LDS past the default 64 KB (gfx950 has 160 KB per CU).  Distances and bounds are
+// exact in fp32 (integers and halves < 2^9).
 //
 // The includer defines __host__ / __device__ (HIP, or empty for the host test harness).
 #pragma once
@@ -28,10 +29,12 @@
 namespace ocro {
 
 constexpr int kMaxCells = 255;  // cell ids are bytes, 0xFF = dead / none
-// compact reachability-graph node ids are bytes (0xFF = none); at most 248 nodes keep a block's
-// LDS (blob + 64 configurations) within the 64 KB a launch gets without a function attribute
-constexpr int kMaxNodes = 248;
+// compact reachability-graph node ids are u16 (kNoNode = none); at most kMaxNodes nodes keep a
+// block's LDS (blob + 64 configurations + the kernels' own) within the 160 KB of a gfx950 CU;
+// distances are bytes (0xFF = no path), so a graph whose BFS distances reach 255 is refused too
+constexpr int kMaxNodes = 390;
 constexpr uint8_t kNone = 0xFF;
+constexpr uint16_t kNoNode = 0xFFFF;
 constexpr int kFloor = 0, kCounter = 1, kCutboard = 2, kDelivery = 3;  // OC_TILE_*
 constexpr int kNoop = 4;
 constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NAV_ACTIONS + (0, 0)
@@ -39,8 +42,8 @@ constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NA
 // Static level tables, one byte blob: tile class per cell, node id per (cell, approach),
 // Cutboard and Delivery cells in scan order, then the nnodes x nnodes distance table.
 constexpr int kTileOff = 0;                        // [256] tile class (cells >= W*H: Counter)
-constexpr int kNodeOff = 256;                      // [256 * 5] cell * 5 + approach (4 = (0, 0))
-constexpr int kCutOff = kNodeOff + 256 * 5;        // [256] Cutboard cells, L.ncut of them
+constexpr int kNodeOff = 256;                      // u16 [256 * 5] cell * 5 + approach (4 = (0, 0))
+constexpr int kCutOff = kNodeOff + 2 * 256 * 5;    // [256] Cutboard cells, L.ncut of them
 constexpr int kDelivOff = kCutOff + 256;           // [256] Delivery cells, L.ndeliv of them
 constexpr int kDistOff = kDelivOff + 256;          // [nnodes][nnodes] BFS distances
 // after the distances, at dmin_off: [2][nnodes] the distance from a node to the nearest
@@ -113,7 +116,7 @@ OC_RH bool has_byte(uint32_t w, uint32_t v) {
 // ---- host: level tables --------------------------------------------------------------------
 // Builds the reachability graph of make_reachability_graph (world.py:67-108) and its BFS
 // distances into `blob` (kBlobMax bytes).  Returns the node count, or -1 when the level has
-// more than kMaxCells cells or the graph more than kMaxNodes nodes.
+// more than kMaxCells cells, the graph more than kMaxNodes nodes, or a BFS distance past 254.
 inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uint8_t* tiles, int enc) {
     L.W = W;
     L.enc = enc;
@@ -122,13 +125,13 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
     L.ncut = L.ndeliv = 0;
     if (W * H > kMaxCells) return -1;
     uint8_t* tile = blob + kTileOff;
-    uint8_t* node = blob + kNodeOff;
+    uint16_t* node = (uint16_t*)(blob + kNodeOff);
     for (int c = 0; c < 256; ++c) {
         tile[c] = c < W * H ? tiles[c] : (uint8_t)kCounter;
         if (c < W * H && tiles[c] == kCutboard) blob[kCutOff + L.ncut++] = (uint8_t)c;
         if (c < W * H && tiles[c] == kDelivery) blob[kDelivOff + L.ndeliv++] = (uint8_t)c;
     }
-    for (int i = 0; i < 256 * 5; ++i) node[i] = kNone;
+    for (int i = 0; i < 256 * 5; ++i) node[i] = kNoNode;
     int n = 0;
     auto clampx = [&](int v) { return v < 0 ? 0 : (v > W - 1 ? W - 1 : v); };
     auto clampy = [&](int v) { return v < 0 ? 0 : (v > H - 1 ? H - 1 : v); };
@@ -137,13 +140,13 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
         const bool coll = tiles[c] != kFloor;
         if (!coll) {
             if (n >= kMaxNodes) return -1;
-            node[c * 5 + 4] = (uint8_t)n++;
+            node[c * 5 + 4] = (uint16_t)n++;
         }
         for (int d = 0; d < 4; ++d) {
             const int nc = clampy(y + kDY[d]) * W + clampx(x + kDX[d]);
             if (coll && tiles[nc] == kFloor) {
                 if (n >= kMaxNodes) return -1;
-                node[c * 5 + d] = (uint8_t)n++;
+                node[c * 5 + d] = (uint16_t)n++;
             }
         }
     }
@@ -151,14 +154,14 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
     // adjacency (undirected): floor-floor, and a collidable square's approach node with the
     // floor it is approached from
     static const int opp[4] = {1, 0, 3, 2};
-    static uint8_t adj[kMaxNodes][8];
+    static uint16_t adj[kMaxNodes][8];
     int deg[kMaxNodes] = {0};
     auto link = [&](int u, int v) {
-        if (u == kNone || v == kNone || u == v) return;
+        if (u == kNoNode || v == kNoNode || u == v) return;
         for (int k = 0; k < deg[u]; ++k)
             if (adj[u][k] == v) return;
-        adj[u][deg[u]++] = (uint8_t)v;
-        adj[v][deg[v]++] = (uint8_t)u;
+        adj[u][deg[u]++] = (uint16_t)v;
+        adj[v][deg[v]++] = (uint16_t)u;
     };
     for (int c = 0; c < W * H; ++c) {
         const int x = c % W, y = c / W;
@@ -183,6 +186,7 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
             for (int k = 0; k < deg[u]; ++k) {
                 const int v = adj[u][k];
                 if (row[v] == kNone) {
+                    if (row[u] + 1 >= kNone) return -1;  // a distance the byte table cannot hold
                     row[v] = (uint8_t)(row[u] + 1);
                     q[qt++] = v;
                 }
@@ -202,7 +206,7 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
             for (int i = 0; i < nc; ++i)
                 for (int d = 0; d < 4; ++d) {
                     const int b = node[cells[i] * 5 + d];
-                    if (b == kNone) continue;
+                    if (b == kNoNode) continue;
                     const int dd = dist[v * n + b];
                     if (dd != kNone && dd < best) best = dd;
                 }
@@ -380,9 +384,11 @@ struct RowOps {
         return count > s.count;
     }
 
-    OC_RH int nid(int c, int d) const { return T[kNodeOff + c * 5 + d]; }  // graph node of (cell, approach)
+    OC_RH int nid(int c, int d) const {  // graph node of (cell, approach)
+        return ((const uint16_t*)(T + kNodeOff))[c * 5 + d];
+    }
     OC_RH int dn(int u, int v) const {  // nx.shortest_path_length between node ids, or -1
-        if (u == kNone || v == kNone) return -1;
+        if (u == kNoNode || v == kNoNode) return -1;
         const int d = T[kDistOff + u * L.nnodes + v];
         return d == kNone ? -1 : d;
     }

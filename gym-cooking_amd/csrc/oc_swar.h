@@ -52,6 +52,19 @@ OC_SW uint32_t or3(uint32_t a, uint32_t b, uint32_t c) { return bop3<OC_LUT(a | 
 OC_SW uint32_t andn(uint32_t a, uint32_t b) { return bop3<OC_LUT(a & !b)>(a, b, 0u); }  // a & ~b
 OC_SW uint32_t perm(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_perm(hi, lo, s); }
 
+// In-place updates for the rare path of step4: x = m ? a : x, x &= ~m, x |= m, with the result
+// in x's own register.  The device build (oc_engine.hip) defines them as inline asm whose
+// output is tied to x: the rare path then rewrites the common path's registers, and the
+// common path, where x passes through unchanged, needs no copy per state word at the join
+// (with plain selects the compiler gave the join the rare path's registers and copied 25
+// words on every common-path step).  `a` is wave-uniform (a level constant).  Other
+// includers (the host test harness) get plain C.
+#ifndef OC_TIED_SEL
+#define OC_TIED_SEL(x, m, a) ((x) = ::ocsw::sel((m), (a), (x)))
+#define OC_TIED_ANDN(x, m) ((x) = ::ocsw::andn((x), (m)))
+#define OC_TIED_OR(x, m) ((x) |= (m))
+#endif
+
 // h80 -> full mask per byte: 0x80 -> 0xFF, 0x00 -> 0x00.  One v_perm_b32 with h as the
 // selector: a selector byte >= 13 (0x80) yields 0xFF, and 0 picks byte 0 of the zero source
 // (h | (h - (h >> 7)), the carry-free arithmetic form, takes three instructions).  Every h
@@ -328,19 +341,20 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         const uint32_t ob3 = K > 8 ? any_at([](int j) { return (j & 8) != 0; }) : 0u;
         const uint32_t so1 = (ob0 >> 5) | kLanes;                            // (o & 1) * 4 + q
         const uint32_t sh = bop3<OC_LUT((a & b) | c)>(h << 2, k04, kLanes);  // (h & 1) * 4 + q
-        uint32_t om, hm, hl;
+        // A held item lies on its holder's square: acquire sets its location to the agent's,
+        // move_to moves it along, and a merge keeps the holder's object (agent.py:408-423,
+        // core.py merge), so the held slot's location is loc[k] and needs no gather.
+        uint32_t om, hm;
         if constexpr (K == 4) {  // the pair select is a second v_perm on the index's bit 1
             const uint32_t so2 = (ob1 >> 5) | kLanes, sh2 = bop3<OC_LUT(a | (b & c))>(kLanes, h << 1, k04);
             om = perm(perm(M[3], M[2], so1), perm(M[1], M[0], so1), so2);
             hm = perm(perm(M[3], M[2], sh), perm(M[1], M[0], sh), sh2);
-            hl = perm(perm(Lc[3], Lc[2], sh), perm(Lc[1], Lc[0], sh), sh2);
         } else {
             const uint32_t fo1 = full80(ob1), fo2 = full80(ob2), fo3 = K == 16 ? full80(ob3) : 0u;
             const uint32_t fh1 = full80((h << 6) & k80), fh2 = full80((h << 5) & k80);
             const uint32_t fh3 = K == 16 ? full80((h << 4) & k80) : 0u;
             om = gather<K>(M, so1, fo1, fo2, fo3);
             hm = gather<K>(M, sh, fh1, fh2, fh3);
-            hl = gather<K>(Lc, sh, fh1, fh2, fh3);
         }
 
         const uint32_t nf = andn(go80, isF80), mv = andn(go80 & isF80, out80[k]);  // clamped: no move
@@ -393,7 +407,7 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         const uint32_t fmg = full80(merge), fpk = full80(pick);
         const uint32_t newOl = fmg | sel(fpk, loc[k], tc);  // merged away: dead (0xFF)
         const uint32_t newOm = andn(om, fmg);
-        const uint32_t newHl = sel(full80(reloc), tc, hl);
+        const uint32_t newHl = sel(full80(reloc), tc, loc[k]);
         const uint32_t newHm = sel(fmg, cu, sel(full80(chop), chopped, hm));
         // scatter: target slot on merge / pick, held slot on reloc / merge / chop.  The per-slot
         // select masks are one v_perm each: selector byte = slot index (h, or the target slot
@@ -451,13 +465,11 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
         const uint32_t z1 = andn(0x80008000u, ((d1 & 0x7FFF7FFFu) + 0x7FFF7FFFu) | d1);
         tout = perm(z1, z0, 0x07050301u);  // high byte of each u16 half -> env byte
     }
-    if (!any_of(or3(rst, tout | err, dlv | pending))) {  // wave-uniform: no rare event
-        T0 = __builtin_bit_cast(uint32_t, t0);
-        T1 = __builtin_bit_cast(uint32_t, t1);
-        F = 0u;
-        CM = cm;
-        return false;
-    }
+    T0 = __builtin_bit_cast(uint32_t, t0);
+    T1 = __builtin_bit_cast(uint32_t, t1);
+    F = 0u;
+    CM = cm;
+    if (!any_of(or3(rst, tout | err, dlv | pending))) return false;  // wave-uniform: no rare event
     pending = 0u;
     uint32_t ok = k80;
     for (int g = 0; g < L.ngoals; ++g) {  // every Deliver goal: an item == goal at the delivery cell
@@ -479,20 +491,20 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
     // ---- auto-reset of envs that were done at the input: the level template ----
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-        X[a] = sel(rst, L.tmpl_x[a], X[a]);
-        Y[a] = sel(rst, L.tmpl_y[a], Y[a]);
-        H[a] = H[a] | rst;
-        EX[a] = sel(rst, k04, EX[a]);
+        OC_TIED_SEL(X[a], rst, L.tmpl_x[a]);
+        OC_TIED_SEL(Y[a], rst, L.tmpl_y[a]);
+        OC_TIED_OR(H[a], rst);
+        OC_TIED_SEL(EX[a], rst, k04);
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        Lc[j] = sel(rst, L.tmpl_l[j], Lc[j]);
-        M[j] = sel(rst, L.tmpl_m[j], M[j]);
+        OC_TIED_SEL(Lc[j], rst, L.tmpl_l[j]);
+        OC_TIED_SEL(M[j], rst, L.tmpl_m[j]);
     }
-    T0 = andn(__builtin_bit_cast(uint32_t, t0), perm(rst, rst, 0x01010000u));
-    T1 = andn(__builtin_bit_cast(uint32_t, t1), perm(rst, rst, 0x03030202u));
-    F = andn(fl, rst);
-    CM = andn(cm, rst);
+    OC_TIED_ANDN(T0, perm(rst, rst, 0x01010000u));
+    OC_TIED_ANDN(T1, perm(rst, rst, 0x03030202u));
+    OC_TIED_OR(F, andn(fl, rst));
+    OC_TIED_ANDN(CM, rst);
     return true;
 }
 

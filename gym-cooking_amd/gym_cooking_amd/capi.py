@@ -20,7 +20,7 @@ OC_MAX_CELLS = 255
 OC_MAX_GOALS = 4
 OC_PITCH_ALIGN = 4096
 OC_NSTATS = 5
-OC_ABI_VERSION = 5  # include/oc_engine.h
+OC_ABI_VERSION = 6  # include/oc_engine.h
 OC_EINVAL, OC_EHIP, OC_ELEVEL = -1, -2, -3
 
 OC_FLAG_DONE = 0x01
@@ -205,7 +205,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 
 class LevelError(RuntimeError):
     """OC_ELEVEL: the level is outside an entry point's envelope (e.g. a reachability graph of
-    more than 248 nodes for the planner entry points)."""
+    more than 390 nodes for the planner entry points)."""
 
 
 def check(rc: int) -> None:

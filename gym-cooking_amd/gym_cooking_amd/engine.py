@@ -220,13 +220,13 @@ class OvercookedBatch:
         return lower_bound, doable
 
     def reachability(self):
-        """The level's static reachability graph (oc_reachability): (node_of u8 [W*H*5] with
-        0xFF = not a node, dist u8 [n][n] with 0xFF = no path)."""
+        """The level's static reachability graph (oc_reachability): (node_of u16 [W*H*5] with
+        0xFFFF = not a node, dist u8 [n][n] with 0xFF = no path)."""
         import ctypes
         n = ctypes.c_int32()
         capi.check(self.lib.oc_reachability(self._h, ctypes.byref(n), None, 0, None, 0))
         cells = self.level.width * self.level.height
-        node_of = np.zeros(cells * 5, np.uint8)
+        node_of = np.zeros(cells * 5, np.uint16)
         dist = np.zeros((n.value, n.value), np.uint8)
         capi.check(self.lib.oc_reachability(self._h, ctypes.byref(n), node_of.ctypes.data, node_of.size,
                                             dist.ctypes.data, dist.size))

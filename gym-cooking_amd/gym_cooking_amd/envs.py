@@ -176,7 +176,7 @@ class ReachabilityGraph:
         self.width = width
         self._id: Dict[tuple, int] = {}
         for key, n in enumerate(node_of.tolist()):
-            if n != 0xFF:
+            if n != 0xFFFF:
                 c, d = divmod(key, 5)
                 self._id[((c % width, c // width), self._APPROACH[d])] = n
         self._dist = dist
@@ -711,7 +711,7 @@ class _Single:
         try:
             node_of, dist = batch.reachability()
             self.reach = ReachabilityGraph(batch.level.width, node_of, dist)
-        except capi.LevelError:  # graph past the planner tables' 248 nodes: stepping still works
+        except capi.LevelError:  # graph past the planner tables' 390 nodes: stepping still works
             self.reach = None
 
     def _download(self, buf) -> np.ndarray:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define OC_ABI_VERSION 5
+#define OC_ABI_VERSION 6
 
 #define OC_MAX_AGENTS 4
 #define OC_MAX_ITEMS 16  /* item slots: K = 4, 8 or 16 per level */
@@ -314,10 +314,10 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
  * side a collidable square is reached from) and 4 = (0, 0) (a Floor square).  Host data; works
  * without a device.
  *   num_nodes : out, n
- *   node_of   : nullable u8 [W*H*5]: node id of (cell, approach), 0xFF = not a node
+ *   node_of   : nullable u16 [W*H*5]: node id of (cell, approach), 0xFFFF = not a node
  *   dist      : nullable u8 [n][n]: nx.shortest_path_length between nodes, 0xFF = no path
  * World.get_lower_bound_between(_helper) (world.py:115-283) evaluates over exactly this table. */
-int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint8_t* node_of, int64_t node_of_len, uint8_t* dist,
+int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, int64_t node_of_len, uint8_t* dist,
                     int64_t dist_len);
 
 /* ---------------------------------------------------------------------------------------

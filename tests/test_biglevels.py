@@ -101,7 +101,8 @@ def test_big_level_swar_matches_oracle_random(name, A):
 
 
 @pytest.mark.parametrize("fixture,cfg", [("bounds_big.npz", 0), ("bounds_big.npz", 1), ("bounds_big.npz", 2),
-                                         ("bounds_k8.npz", 0)])
+                                         ("bounds_k8.npz", 0), ("bounds_bignodes.npz", 0),
+                                         ("bounds_bignodes.npz", 1)])
 def test_big_level_bounds_match_reference_rows(fixture, cfg):
     rows = tl.BoundRows(tl.load_fixture(fixture), cfg)
     assert rows.level.ncells > 64 or rows.K == 8

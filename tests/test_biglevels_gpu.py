@@ -4,10 +4,12 @@
     on a 9x9 kitchen of 6 items (the 8-slot layout), bit for bit (tests/golden/biglevels*.npz),
     one oc_step launch per step;
   * oc_step_n (multi-step launches) against the CPU oracle on every step's full state;
-  * oc_subtask_bounds against the reference's bound rows (bounds_big.npz), oc_rollout and
+  * oc_subtask_bounds against the reference's bound rows (bounds_big.npz, bounds_bignodes.npz:
+    the 255-cell kitchen's 266-node graph), oc_rollout and
     oc_nav_likelihood against the oracle on random rows;
   * the gym shim replays recorded episodes, raises the reference's exceptions on ragged maps,
-    and steps the 255-cell kitchen whose reachability graph is past the planner tables;
+    and steps the 255-cell kitchen, whose 266-node reachability graph the planner tables hold
+    with u16 node ids;
   * oc_render against the numpy restatement on the 169-cell kitchen."""
 import json
 import os
@@ -96,7 +98,8 @@ def test_big_level_step_n_matches_oracle(name, A):
 
 
 @pytest.mark.parametrize("fixture,cfg", [("bounds_big.npz", 0), ("bounds_big.npz", 1), ("bounds_big.npz", 2),
-                                         ("bounds_k8.npz", 0)])
+                                         ("bounds_k8.npz", 0), ("bounds_bignodes.npz", 0),
+                                         ("bounds_bignodes.npz", 1)])
 def test_big_level_bounds_match_reference_rows(fixture, cfg):
     rows = tl.BoundRows(tl.load_fixture(fixture), cfg)
     P = capi.pitch_for(rows.B)
@@ -109,7 +112,7 @@ def test_big_level_bounds_match_reference_rows(fixture, cfg):
         assert not errs, "\n".join(errs[:20])
 
 
-@pytest.mark.parametrize("name", ["big-10x12_salad", "big-13x13_tl", K8])
+@pytest.mark.parametrize("name", ["big-10x12_salad", "big-13x13_tl", "big-15x17_salad", K8])
 @pytest.mark.parametrize("A", [2, 4])
 def test_big_level_rollout_and_likelihood_match_oracle(name, A):
     B = 6000
@@ -136,14 +139,15 @@ def test_big_level_rollout_and_likelihood_match_oracle(name, A):
     np.testing.assert_allclose(g_v[ok], o_v[ok], rtol=1e-12)
 
 
-def test_planner_tables_refuse_graphs_past_248_nodes():
+def test_planner_tables_of_a_266_node_graph():
+    """The 255-cell kitchen's graph (266 nodes: u16 node ids, a 75 KB table blob staged in
+    dynamic LDS past the default 64 KB) against the reference's graph (reach_big.json)."""
     eb = _batch(levels.load_level(_path("big-15x17_salad")), 2, 64)
-    s = eb.new_state()
-    eb.reset(s)
-    with pytest.raises(capi.LevelError):
-        eb.subtask_bounds(s, [capi.subtask(1, [0], [1, 0], 0x11, 0)])
-    with pytest.raises(capi.LevelError):
-        eb.reachability()
+    node_of, dist = eb.reachability()
+    ref = json.load(open(os.path.join(tl.GOLDEN, "reach_big.json")))["big-15x17_salad"]
+    assert dist.shape == (len(ref["nodes"]),) * 2 == (266, 266)
+    assert int((node_of != 0xFFFF).sum()) == 266 and int(node_of[node_of != 0xFFFF].max()) == 265
+    assert int((dist == 1).sum()) == 2 * len(ref["edges"])
 
 
 def _shim(level, A, max_T=100):
@@ -199,7 +203,7 @@ def test_shim_ragged_maps_raise_like_the_reference():
 def test_shim_steps_the_255_cell_kitchen():
     env = _shim(_path("big-15x17_salad"), 4)
     env.reset()
-    assert env.world.reachability_graph is None  # past the planner tables; stepping still works
+    assert len(env.world.reachability_graph) == 266  # u16 node ids
     for t in range(5):
         env.step({"agent-%d" % (a + 1): levels.ACTIONS[(t + a) % 5] for a in range(4)})
     assert env.t == 5

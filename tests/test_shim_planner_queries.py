@@ -27,7 +27,7 @@ def _reach(level_name):
     try:
         n = ctypes.c_int32()
         capi.check(lib.oc_reachability(h, ctypes.byref(n), None, 0, None, 0))
-        node_of = np.zeros(lv.width * lv.height * 5, np.uint8)
+        node_of = np.zeros(lv.width * lv.height * 5, np.uint16)
         dist = np.zeros((n.value, n.value), np.uint8)
         capi.check(lib.oc_reachability(h, ctypes.byref(n), node_of.ctypes.data, node_of.size, dist.ctypes.data,
                                        dist.size))
@@ -41,10 +41,17 @@ def _key(n):
     return (tuple(n[0]), tuple(n[1]))
 
 
-@pytest.mark.parametrize("level", sorted(json.load(open(os.path.join(tl.GOLDEN, "reach.json")))))
-def test_reachability_graph_matches_reference(level):
-    ref = json.load(open(os.path.join(tl.GOLDEN, "reach.json")))[level]
-    _, g = _reach(level)
+# builtin levels (reach.json) and the 255-cell kitchen, whose 266-node graph takes u16 node ids
+# (reach_big.json, tests/golden/gen_bignodes.py)
+_REACH = [("reach.json", lv) for lv in sorted(json.load(open(os.path.join(tl.GOLDEN, "reach.json"))))] + \
+    [("reach_big.json", lv) for lv in sorted(json.load(open(os.path.join(tl.GOLDEN, "reach_big.json"))))]
+
+
+@pytest.mark.parametrize("fixture,level", _REACH)
+def test_reachability_graph_matches_reference(fixture, level):
+    ref = json.load(open(os.path.join(tl.GOLDEN, fixture)))[level]
+    _, g = _reach(level if fixture == "reach.json" else os.path.join(tl.GOLDEN, "levels", level + ".txt"))
+    assert len(g) == len(ref["nodes"])
     assert sorted(g.nodes()) == sorted(_key(n) for n in ref["nodes"])
     assert sorted(tuple(sorted(e)) for e in g.edges()) == sorted(tuple(sorted(_key(n) for n in e))
                                                                   for e in ref["edges"])
