@@ -265,18 +265,28 @@ __host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
     return (stat_rows * OC_NSTATS + kTicketStride - 1) / kTicketStride * kTicketStride;
 }
 
-// oc_step_n takes its action words in batches of kActBatch steps: each lane loads a batch's
-// words into registers one batch ahead and parks them in LDS when the batch starts; a step
-// reads its words from LDS.  The compiler waits vmcnt(0) before it consumes a loaded word while
-// stores are outstanding (loads and stores share the counter, and it does not assume they
-// complete in order), i.e. for every store the wave has issued.  With one load per step that was
-// each wave waiting, every step, for the previous step's stores to drain (C3: 6.4 us/step, 5.1
-// with the loads taken out of the loop); with batches it waits once per batch.
-template <int A>
-constexpr int act_batch() { return A >= 4 ? 4 : 8; }  // 2 * A * batch registers <= 32
+// Loader wave (LW).  A wave that has stores outstanding and consumes a loaded word waits for
+// every one of those stores: the compiler emits vmcnt(0) there (loads and stores share the
+// counter on gfx950, and it does not take them to complete in order).  With each step's action
+// words loaded by the stepping wave, every wave waited at every step for the stores of the step
+// before to drain: C3 (3 agents) ran 6.4 us/step, and 5.1 with the action loads taken out of
+// the loop (tools/c3_floor.py, profiles/r03/lw/).  With LW, a block has a fifth wave that only
+// loads: it fetches the next kLwSteps steps' action words of the block's 256 lanes into one half
+// of an LDS ring while the four stepping waves read theirs from the other half, and an
+// LDS-only barrier per kLwSteps steps hands the halves over (no vmcnt wait; the stepping waves
+// issue no vector load after their state).  Only the loader waits on memory, for loads alone.
+constexpr int kLwSteps = 4;
+constexpr bool kLoaderWave = false;  // pending its GPU run
+template <int A, int K, int MODE>
+constexpr bool use_loader_wave() { return kLoaderWave && A <= 3 && K == 4; }
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
-template <int A, int K, int CP, int LCP, int MODE>
-__global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
+template <int A, int K, int CP, int LCP, int MODE, bool LW = use_loader_wave<A, K, MODE>()>
+__global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void oc_step_n_kernel(LevelArgs L, const uint8_t* __restrict__ sin,
                                                            uint8_t* __restrict__ sout,
                                                            const uint8_t* __restrict__ actions,
                                                            uint8_t* __restrict__ traj, uint8_t* __restrict__ exec_out,
@@ -286,11 +296,13 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
     __shared__ uint32_t tbl4[64];
     __shared__ uint32_t waves_done;
     __shared__ unsigned long long fold[OC_NSTATS][64 + 8];  // the folding wave's partial sums
-    constexpr int kS = act_batch<A>();
-    __shared__ uint32_t actbuf[kBlock / 64][kS * A][64];  // each wave's current action batch
+    // LW: [half][step of the batch][stepping wave][agent][lane] action words
+    __shared__ uint32_t ring[LW ? 2 * kLwSteps * (kBlock / 64) * A * 64 : 1];
     if (threadIdx.x < 64u) tbl4[threadIdx.x] = L.cls4[threadIdx.x];
     if (threadIdx.x == 0u) waves_done = 0u;
     __syncthreads();
+    const bool loader = LW && threadIdx.x >= (uint32_t)kBlock;  // wave-uniform
+    const uint32_t lane = threadIdx.x & 63u;
     const uint8_t* tbl = (const uint8_t*)tbl4;
     const uint32_t P = (uint32_t)L.pitch, nlanes = P / kEPL, stride = gridDim.x * (uint32_t)kBlock;
     constexpr int NP = 3 * A + 2 * K + 3;
@@ -310,41 +322,73 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
     b.coll = make_rsrc(has_coll ? (const void*)coll_out : (const void*)sin, has_coll ? (int64_t)n * P : 0);
     StepStats st;
     typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
-    for (uint32_t g = blockIdx.x * (uint32_t)kBlock + threadIdx.x; g < nlanes; g += stride) {  // block-uniform
+    for (uint32_t gb = blockIdx.x * (uint32_t)kBlock; gb < nlanes; gb += stride) {  // block-uniform
+        if (loader) {
+            // the action words of steps r0 .. r0 + kLwSteps - 1 (those < n) into ring half h;
+            // this wave issues no store, so its waits are for its own loads only
+            auto fill = [&](int r0, int h) {
+                uint32_t w[kLwSteps][kBlock / 64][A];
+#pragma unroll
+                for (int q = 0; q < kLwSteps; ++q)
+#pragma unroll
+                    for (int v = 0; v < kBlock / 64; ++v)
+#pragma unroll
+                        for (int a = 0; a < A; ++a)
+                            w[q][v][a] = r0 + q < n ? bld32<LCP>(b.act, (gb + 64u * v + lane) * 4u,
+                                                                 (uint32_t)((r0 + q) * A + a) * P)
+                                                    : 0u;
+#pragma unroll
+                for (int q = 0; q < kLwSteps; ++q)
+#pragma unroll
+                    for (int v = 0; v < kBlock / 64; ++v)
+#pragma unroll
+                        for (int a = 0; a < A; ++a)
+                            ring[(((h * kLwSteps + q) * (kBlock / 64) + v) * A + a) * 64 + lane] = w[q][v][a];
+            };
+            fill(0, 0);
+            for (int r0 = 0; r0 < n; r0 += kLwSteps) {
+                lds_barrier();  // half (r0 / kLwSteps) & 1 is full; the other one has been read
+                if (r0 + kLwSteps < n) fill(r0 + kLwSteps, ((r0 / kLwSteps) & 1) ^ 1);
+            }
+            lds_barrier();  // the chunk's last batch has been read: the next chunk may refill
+            continue;
+        }
+        const uint32_t g = gb + threadIdx.x;
         Chunk<A, K> c;
-        load_chunk<A, K, false>(c, b, P, g);
+        load_chunk<A, K, !LW>(c, b, P, g);
+        // the state words land before the step loop: waited for at their first use inside the
+        // loop, the wait (vmcnt(0) for the last of them) would stay in the loop body and drain
+        // every step's stores (an s_waitcnt the compiler's waitcnt pass sees and accounts for)
+        if (LW) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt untouched
         const uint32_t vo = g * 4u;
-        uint32_t T0 = c.wt.x, T1 = c.wt.y;
+        uint32_t T0 = c.wt.x, T1 = c.wt.y, nxt[A];
         uint32_t pending = ocsw::at_done80<K, MODE>(L.sw, c.wl);  // the loaded state: the full path once
         const int64_t rem = L.B - (int64_t)g * kEPL;
         const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (rem <= 0 ? 0u : (1u << (8 * (uint32_t)rem)) - 1u);
-        // action batches: word i of the batch starting at step r0 is agent i % A of step r0 + i / A;
-        // the step offset is in the VGPR offset, so words past step n fall outside the
-        // descriptor's range and read 0 without a memory access
-        uint32_t* const ab = &actbuf[threadIdx.x >> 6][0][threadIdx.x & 63u];
-        uint32_t areg[kS * A];
-        auto load_batch = [&](int r0) {
-            const uint32_t vb = vo + (uint32_t)(r0 * A) * P;
+        if (!LW) {
 #pragma unroll
-            for (int i = 0; i < kS * A; ++i)
-                areg[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(b.act, (int)(vb + (uint32_t)i * P), 0, LCP);
-        };
-        auto park_batch = [&]() {
-#pragma unroll
-            for (int i = 0; i < kS * A; ++i) ab[i * 64] = areg[i];
-        };
-        load_batch(0);
-        park_batch();
-        if (n > kS) load_batch(kS);
+            for (int a = 0; a < A; ++a) nxt[a] = n > 1 ? bld32<LCP>(b.act, vo, (uint32_t)(A + a) * P) : 0u;
+        }
         for (int r = 0; r < n; ++r) {
-            const int sb = r % kS;
-            if (sb == 0 && r > 0) {  // wave-uniform: a new batch
-                park_batch();
-                if (r + kS < n) load_batch(r + kS);
-            }
             uint32_t act[A], ex[A], cm;
+            if (LW) {
+                const int q = r % kLwSteps;
+                if (q == 0) lds_barrier();  // the loader has filled this batch's half
+                const int h = (r / kLwSteps) & 1;
 #pragma unroll
-            for (int a = 0; a < A; ++a) act[a] = ab[(sb * A + a) * 64];
+                for (int a = 0; a < A; ++a)
+                    act[a] = ring[(((h * kLwSteps + q) * (kBlock / 64) + (threadIdx.x >> 6)) * A + a) * 64 + lane];
+            } else {
+#pragma unroll
+                for (int a = 0; a < A; ++a) {
+                    act[a] = c.wa[a];
+                    c.wa[a] = nxt[a];
+                }
+                if (r + 2 < n) {
+#pragma unroll
+                    for (int a = 0; a < A; ++a) nxt[a] = bld32<LCP>(b.act, vo, (uint32_t)((r + 2) * A + a) * P);
+                }
+            }
             const uint32_t f_in = c.wf;
             const bool full = ocsw::step4<A, K, MODE>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, act, ex,
                                                       cm, cls_of, WaveAny{}, pending);
@@ -382,6 +426,7 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
             for (int a = 0; a < A; ++a) bst32<CP>(b.ex, ex[a], vo, (uint32_t)(r * A + a) * P);
             bst32<CP>(b.coll, cm, vo, (uint32_t)r * P);
         }
+        if (LW) lds_barrier();  // pairs with the loader's end-of-chunk barrier
 #pragma unroll
         for (int a = 0; a < A; ++a) {
             bst32<CP>(b.sout, c.wx[a], vo, a * P);
@@ -397,6 +442,7 @@ __global__ __launch_bounds__(kBlock) void oc_step_n_kernel(LevelArgs L, const ui
         __builtin_amdgcn_raw_buffer_store_b64(tw, b.sout, (int)(g * 8u), (int)(kPT * P), CP);
         bst32<CP>(b.sout, c.wf, vo, kPF * P);
     }
+    if (loader) return;  // the stepping waves count and fold the statistics
     if (stats != nullptr) {
         const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
                                        wave_sum(st.err)};
@@ -1374,8 +1420,8 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
     int64_t per = ((1ll << 31) - 1) / (NP * L.pitch);
     if (per > 4096) per = 4096;
     per = (n + (n + per - 1) / per - 1) / ((n + per - 1) / per);  // equal launches
-    const int64_t need = L.pitch / kEnvsPerBlock, cap = (int64_t)h->cus * 5;  // <= 5 waves/SIMD resident
-    const dim3 grid((unsigned)(need < cap ? need : cap));
+    // <= 5 waves per SIMD resident: 5 blocks of 4 waves per CU, or 4 of 5 with the loader wave
+    const int64_t need = L.pitch / kEnvsPerBlock;
     hipStream_t s = (hipStream_t)stream;
     const uint32_t rows = (uint32_t)stats_rows(h, B);
     const uint8_t* src = (const uint8_t*)state_in;
@@ -1392,8 +1438,13 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
         const bool last = r0 + m >= n;
         uint8_t* so = (traj != nullptr && !last) || (out_is_last && last) ? nullptr : (uint8_t*)state_out;
 #define OC_LAUNCH_STEPN(A, K, MODE)                                                                    \
-    hipLaunchKernelGGL((oc_step_n_kernel<A, K, kCPnt, 0, MODE>), grid, dim3(kBlock), 0, s, L, src, so, ac, tr, ex, \
-                       cm, stats, last ? totals : nullptr, rows, m)
+    {                                                                                                  \
+        constexpr bool kLW = use_loader_wave<A, K, MODE>();                                           \
+        const int64_t cap = (int64_t)h->cus * (kLW ? 4 : 5);                                           \
+        const dim3 grid((unsigned)(need < cap ? need : cap));                                          \
+        hipLaunchKernelGGL((oc_step_n_kernel<A, K, kCPnt, 0, MODE>), grid, dim3(kBlock + (kLW ? 64 : 0)), 0, s, L, \
+                           src, so, ac, tr, ex, cm, stats, last ? totals : nullptr, rows, m);                 \
+    }
         OC_DISPATCH_STEP(h, OC_LAUNCH_STEPN)
         src = traj != nullptr ? tr + (int64_t)(m - 1) * NP * L.pitch : (const uint8_t*)state_out;
         if (const int rc = hip_check("oc_step_n launch")) return rc;
