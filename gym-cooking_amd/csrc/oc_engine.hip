@@ -276,9 +276,13 @@ __host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
 // LDS-only barrier per kLwSteps steps hands the halves over (no vmcnt wait; the stepping waves
 // issue no vector load after their state).  Only the loader waits on memory, for loads alone.
 constexpr int kLwSteps = 4;
-constexpr bool kLoaderWave = false;  // pending its GPU run
+// A = 3 only: there the stepping waves' drains were a fifth of the time (C3, 100-step launches,
+// one box: 6.42 -> 6.07 us/step, outputs identical).  At A <= 2 the step is store-bound and the
+// block-wide barrier every kLwSteps steps costs more than the drains (2 agents, 20-step launch:
+// 4.60 -> 4.70 us/step; 100-step: 4.20 -> 4.22); A = 4 needs more than 102 VGPRs.
+constexpr bool kLoaderWave = true;
 template <int A, int K, int MODE>
-constexpr bool use_loader_wave() { return kLoaderWave && A <= 3 && K == 4; }
+constexpr bool use_loader_wave() { return kLoaderWave && A == 3 && K == 4; }
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
