@@ -79,7 +79,25 @@ SALAD_SUBTASKS = [(1, (0x01, 0), 0x11), (1, (0x02, 0), 0x22),
                   (3, (0x3B, 0), 0x3B)]
 
 
-def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 20) -> dict:
+def time_launches(launch, reps: int, dev) -> float:
+    """Mean duration (ms, max over ranks) of one kernel launch: `reps` launches of a pre-bound
+    launcher (engine.*_launcher: one ctypes call each, no per-call validation or table
+    packing) back to back between two HIP events on the launch stream.  The host enqueues a
+    launch in a few microseconds, faster than the kernels run, so the queue never drains and
+    the events bracket kernel time (rocprofv3's kernel-trace mean agrees: profiles/r04/c5/)."""
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    return ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
+
+
+def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 200) -> dict:
     """Secondary line, config C5: navigation-planner rollout rows (oc_rollout) on
     full-divider_salad with 4 agents.  Row states are mid-episode random-play states; each
     row gets a random (subtask, 1-2 agent) allocation out of the Salad subtasks x every agent
@@ -115,16 +133,7 @@ def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 20) -> dict:
     lb = torch.empty(eb.pitch, dtype=torch.float32, device=dev)
 
     def time_rollout(al):
-        for _ in range(2):
-            eb.rollout(s, out, a, table, al, flags, lb)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            eb.rollout(s, out, a, table, al, flags, lb)
-        e1.record()
-        torch.cuda.synchronize()
-        return ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
+        return time_launches(eb.rollout_launcher(s, out, a, table, al, flags, lb), reps, dev)
 
     ms_rnd = time_rollout(rnd)
     ms = time_rollout(alloc)
@@ -143,41 +152,27 @@ def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 20) -> dict:
             "random_order": {"ms_per_launch": ms_rnd, "value": world * rows / (ms_rnd * 1e-3)}}
 
 
-def measure_likelihood(eb, states, taken, table, alloc, dev, world, reps: int = 5) -> dict:
+def measure_likelihood(eb, states, taken, table, alloc, dev, world, reps: int = 40) -> dict:
     """C5's consumer: Bayesian-delegation likelihoods (oc_nav_likelihood, prob_nav_actions with
     value_init values) of the same rows -- every legal candidate action of a row is a rollout."""
     from gym_cooking_amd import capi
-    for _ in range(2):
-        v, f = eb.nav_likelihood(states, taken, table, 0, 1.3, 0.5, alloc)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        v, f = eb.nav_likelihood(states, taken, table, 0, 1.3, 0.5, alloc)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
+    v = torch.empty(eb.pitch, dtype=torch.float64, device=dev)
+    f = torch.empty(eb.pitch, dtype=torch.uint8, device=dev)
+    ms = time_launches(eb.nav_likelihood_launcher(states, taken, table, 0, 1.3, 0.5, alloc, v, f), reps, dev)
     ok = int((f[:eb.B] == capi.LIK_OK).sum())
     return {"value": world * eb.B / (ms * 1e-3), "unit": "likelihood rows/s", "ms_per_launch": ms,
             "kernel": "oc_likelihood_kernel<4,4>", "rows_computed": ok, "bound": "divergence + latency (a lane "
             "per candidate rollout, up to 25 per row; profiles/r02/c5_grouped/pmc_c5.json)"}
 
 
-def measure_bounds(eb, states, table, dev, world, reps: int = 10) -> dict:
+def measure_bounds(eb, states, table, dev, world, reps: int = 60) -> dict:
     """C5's prior setup: full-state subtask bounds + allocation feasibility (oc_subtask_bounds,
     get_lower_bound_for_subtask_given_objs / subtask_alloc_is_doable) of every env x every
     configuration of the table.  Algorithmic bytes per env: S(4) = 23 state bytes read + 5 B
     (f32 bound, u8 doable) written per configuration."""
-    for _ in range(2):
-        lb, ok = eb.subtask_bounds(states, table)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        eb.subtask_bounds(states, table, lb, ok)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) / reps * 1e-3, dev) * 1e3
+    lb = torch.empty((len(table), eb.pitch), dtype=torch.float32, device=dev)
+    ok = torch.empty((len(table), eb.pitch), dtype=torch.uint8, device=dev)
+    ms = time_launches(eb.subtask_bounds_launcher(states, table, lb, ok), reps, dev)
     cells = eb.B * len(table)
     nbytes = eb.B * (23 + 5 * len(table))
     return {"value": world * cells / (ms * 1e-3), "unit": "(env, configuration) bounds/s", "ms_per_launch": ms,
@@ -422,7 +417,7 @@ def measure_plan_batch(dev, B: int = 1024, steps: int = 12) -> dict:
             "workload": "B random-play states of open-divider_salad after %d steps, Chop(Tomato) by agent-1" % steps}
 
 
-def measure_c3(dev, world, B: int = 1 << 20, n: int = 100) -> dict:
+def measure_c3(dev, world, B: int = 1 << 20, n: int = 100, reps: int = 20) -> dict:
     """Secondary line, config C3: 3-agent full-divider_tl (the collision-heavy path), 2^20 envs
     per GPU, one oc_step_n launch of n steps with every step's outputs written."""
     from gym_cooking_amd.engine import OvercookedBatch
@@ -433,19 +428,17 @@ def measure_c3(dev, world, B: int = 1 << 20, n: int = 100) -> dict:
         eb.gen_actions(acts[i], step=i, seed=3)
     traj = torch.empty(n * S, dtype=torch.uint8, device=dev)
     ex, coll = torch.empty(n * A * P, dtype=torch.uint8, device=dev), torch.empty(n * P, dtype=torch.uint8, device=dev)
-    s, s2, stats = eb.new_state(), eb.new_state(), eb.new_stats()
+    s, stats = eb.new_state(), eb.new_stats()
+    tot = torch.zeros(5, dtype=torch.int64, device=dev)
     eb.reset(s)
-    eb.step_n(s, s2, acts.reshape(-1), n, traj, ex, coll, stats)
+    # as the headline launches it: state_out is the trajectory's last state, statistics folded
+    # in-launch; every replay starts from the same reset state
+    f = eb.step_n_launcher(s, traj[(n - 1) * S:], acts.reshape(-1), n, traj, ex, coll, stats, tot)
+    f()
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    eb.reset(s)
-    stats.zero_()
-    e0.record()
-    eb.step_n(s, s2, acts.reshape(-1), n, traj, ex, coll, stats)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = ocdist.max_over_ranks(e0.elapsed_time(e1) * 1e-3, dev) * 1e3
-    tot = eb.reduce_stats(stats).cpu().tolist()
+    first = tot.cpu().tolist()
+    ms = time_launches(f, reps, dev)
+    tot = first
     nS = eb.layout.num_planes
     bytes_step = (nS + n * (nS + 2 * A + 1)) / n
     return {"value": world * B * n / (ms * 1e-3), "unit": "env-steps/s", "envs_per_gpu": B, "steps": n,
@@ -627,7 +620,7 @@ def main() -> int:
     summary_row[5:] = ocdist.device_ident(dev).to(dev)
     totals = summary_row[:5]
 
-    def plan(n_steps_total):
+    def plan(n_steps_total, act_buf):
         """The launches of a window, bound once (engine.step_n_launcher: buffers validated
         here, each launch is then one ctypes call).  A launch's state_out is its trajectory's
         last state (oc_step_n then writes the final state once), and the next launch starts
@@ -641,18 +634,26 @@ def main() -> int:
             traj, ex_all, coll_all = outs[li % n_sets]
             dst = traj[(n - 1) * S:n * S]
             last = done + n >= n_steps_total
-            out.append(eb.step_n_launcher(src, dst, acts[i0:i0 + n].reshape(-1), n, traj[:n * S], ex_all, coll_all,
-                                          stats, totals if last else None))
+            out.append(eb.step_n_launcher(src, dst, act_buf[i0:i0 + n].reshape(-1), n, traj[:n * S], ex_all,
+                                          coll_all, stats, totals if last else None))
             src = dst
             done += n
             li += 1
-        return out
+        return out, src
 
-    timed = plan(K)
-    # warmup: at least W untimed steps, rounded up to whole launches of the timed length (every
-    # oc_step_n launch a profiler sees has the timed shape, summary path included), and repeated
-    # for at least --min-warmup-ms so that the clocks have left their idle state
-    warm = plan(-(-max(W, 1) // n_per) * n_per)
+    timed, _ = plan(K, acts)
+    # The warmup steps its own action stream (another seed): the window never replays a launch
+    # the warmup ran.  The window's actions are written just before it (untimed), as a policy
+    # writes them before a step: at the driver's shape (K = 20, 42 MB) they are then
+    # Infinity-Cache resident.  The same window is timed again with the actions evicted
+    # (window_cold_actions).
+    acts_w = torch.empty_like(acts)
+    for i in range(K):
+        eb.gen_actions(acts_w[i], step=i, seed=args.seed + 1, env_offset=sh.env_offset)
+    # warmup 1: at least W untimed steps, rounded up to whole launches of the timed length
+    # (every oc_step_n launch a profiler sees has the timed shape, summary path included), and
+    # repeated for at least --min-warmup-ms so that the clocks have left their idle state
+    warm, _ = plan(-(-max(W, 1) // n_per) * n_per, acts_w)
     warm_steps, t_w = 0, time.perf_counter()
     while True:
         eb.reset(s_a)
@@ -663,7 +664,21 @@ def main() -> int:
         warm_steps += len(warm) * n_per
         if warm_steps >= W and (time.perf_counter() - t_w) * 1e3 >= args.min_warmup_ms:
             break
+    # warmup 2: the window starts where a long run is, not at a reset.  From a reset, W_run
+    # steps (ten episodes and more) desynchronise the envs that finish early; W_run is chosen
+    # so that the window's middle falls on the step where the timed-out episodes end (t =
+    # max_T) and the one after, where they auto-reset: the window runs the rare
+    # path (reset, timeout, episode statistics), at 1 step in max_T + 1 otherwise.
+    period = args.max_T + 1
+    w_run = max(n_per, 10 * period + (args.max_T - K // 2 if args.max_T > 0 else 0))
     eb.reset(s_a)
+    chain, end = plan(w_run, acts_w)
+    for f in chain:
+        f()
+    s_a.copy_(end)
+    warm_steps += w_run
+    for i in range(K):  # the window's actions, written now (same values as generated above)
+        eb.gen_actions(acts[i], step=i, seed=args.seed, env_offset=sh.env_offset)
     stats.zero_()
     torch.cuda.synchronize()
 
@@ -714,6 +729,20 @@ def main() -> int:
         torch.cuda.synchronize()
         kern_total_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs)
     kern_ms = ocdist.max_over_ranks(kern_total_ms / (reps * len(segs)) * 1e-3, dev) * 1e3
+    # the same window with its actions evicted from the Infinity Cache (1 GiB written between)
+    flush = torch.empty(1 << 30, dtype=torch.uint8, device=dev)
+    flush.fill_(1)
+    stats.zero_()
+    del flush
+    ocdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for f in timed:
+        f()
+    ocdist.gather_summaries(summary_row, summary_all)
+    torch.cuda.synchronize()
+    ocdist.barrier()
+    cold_max = ocdist.max_over_ranks(time.perf_counter() - t0, dev)
     nS = eb.layout.num_planes  # state bytes per env (the u16 t counts 2)
     bytes_launch = (nS + n_per * (nS + 2 * A + 1)) * sh.batch
     bytes_env_step = bytes_launch / (n_per * sh.batch)
@@ -742,10 +771,18 @@ def main() -> int:
             "launch": "oc_step_n: %d launches x %d steps; every step's state, executed actions and collision "
                       "mask written to HBM" % (len(segs), n_per),
             "warmup_steps_run": warm_steps,
+            "window_starts_after_steps": w_run,
+            "window_actions": "written by gen_actions just before the window (untimed); the warmup steps another "
+                              "stream",
         },
+        "open_loop": True,
+        "window_cold_actions": {
+            "value": world * sh.batch * K / cold_max, "ms_per_step": cold_max * 1e3 / K,
+            "note": "the same window from the same state, its actions evicted from the Infinity Cache first"},
         "roofline": {
             "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+            "frac_wall": bytes_env_step * sh.batch * K / elapsed_max / 1e9 / HBM_PEAK_GBS,
             "kernel": "oc_step_n_kernel<%d,%d>" % (A, eb.K), "steps_per_launch": n_per,
             "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_env_step": bytes_env_step,
             "kernel_ms_mean": kern_ms, "kernel_ms_source": ("HIP events around %d back-to-back replays of the timed "

@@ -109,6 +109,10 @@ static PyObject* tie_pick(PyObject* self, PyObject* args) {
     PyObject *lst, *sample;
     if (!PyArg_ParseTuple(args, "O!O", &PyList_Type, &lst, &sample)) return NULL;
     const Py_ssize_t n = PyList_GET_SIZE(lst);
+    if (n == 0) {
+        PyErr_SetString(PyExc_ValueError, "tie_pick: no candidates");
+        return NULL;
+    }
     char* m = (char*)PyMem_Malloc((size_t)n + 1);
     if (m == NULL) return PyErr_NoMemory();
     for (Py_ssize_t i = 0; i < n; ++i) m[i] = (char)PyObject_IsTrue(PyList_GET_ITEM(lst, i));
@@ -122,6 +126,10 @@ static PyObject* tie_pick(PyObject* self, PyObject* args) {
 static int min_q(PyObject* costs, PyObject* vks, PyObject* v, double* out) {
     const Py_ssize_t n = PyList_GET_SIZE(costs);
     double m = 0.0;
+    if (n == 0) {  /* Python's min() of an empty sequence */
+        PyErr_SetString(PyExc_ValueError, "min() arg is an empty sequence");
+        return -1;
+    }
     for (Py_ssize_t i = 0; i < n; ++i) {
         double c = PyFloat_AsDouble(PyList_GET_ITEM(costs, i)), x;
         if (c == -1.0 && PyErr_Occurred()) return -1;
@@ -194,11 +202,14 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         PyObject *costs = PyList_GET_ITEM(got, 2), *vks = PyList_GET_ITEM(got, 3), *rx = PyList_GET_ITEM(got, 8);
         const Py_ssize_t n = PyList_GET_SIZE(costs);
         double mu;
-        if (min_q(costs, vks, v_u, &mu) < 0 || set_val(v_u, rx, mu) < 0) goto fail;
+        if (min_q(costs, vks, v_u, &mu) < 0 || set_val(v_u, rx, mu) < 0) goto fail;  /* n == 0 raises here */
         /* ql = [c + v_l[vk]]; argmin with planner.argmin's generator consumption */
         double ql_stack[32];
         double* ql = n <= 32 ? ql_stack : (double*)PyMem_Malloc(sizeof(double) * (size_t)n);
-        if (ql == NULL) goto fail;
+        if (ql == NULL) {
+            PyErr_NoMemory();
+            goto fail;
+        }
         Py_ssize_t im = 0, nmin = 0;
         int err = 0;
         for (Py_ssize_t i = 0; i < n && !err; ++i) {
@@ -225,7 +236,10 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         } else if (!err) {  /* ties: the multinomial draw of planner.argmin */
             char mins_stack[32];
             char* mins = n <= 32 ? mins_stack : (char*)PyMem_Malloc((size_t)n);
-            if (mins == NULL) err = 1;
+            if (mins == NULL) {
+                PyErr_NoMemory();
+                err = 1;
+            }
             for (Py_ssize_t i = 0; i < n && !err; ++i) mins[i] = ql[i] == ql[im];
             if (!err) {
                 pick = tie_pick_c(mins, n, sample);

@@ -27,6 +27,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/oc_engine.h"
 #include "oc_rollout.h"
@@ -275,6 +277,10 @@ __host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
 // of an LDS ring while the four stepping waves read theirs from the other half, and an
 // LDS-only barrier per kLwSteps steps hands the halves over (no vmcnt wait; the stepping waves
 // issue no vector load after their state).  Only the loader waits on memory, for loads alone.
+// Handing the ring over with per-step LDS flags instead (the loader publishes steps filled,
+// each stepping wave the steps it took; a ring of 8 steps, s_sleep polls, no barrier) was
+// measured slower: C3 100-step launches 6.28-6.41 us/step against 6.06-6.12 with the barrier,
+// four alternating rounds on one box, outputs identical (profiles/r04/lw_flags_ab.jsonl).
 constexpr int kLwSteps = 4;
 // A = 3 only: there the stepping waves' drains were a fifth of the time (C3, 100-step launches,
 // one box: 6.42 -> 6.07 us/step, outputs identical).  At A <= 2 the step is store-bound and the
@@ -1156,6 +1162,80 @@ int64_t stats_rows(const oc_handle*, int64_t B) {
     return need < kStatRows ? need : kStatRows;
 }
 
+// oc_cpu_step's worker: the host pass of the same SWAR step (oc_swar.h), words [g0, g1) of
+// the batch (4 envs each, as one lane of oc_step_kernel), per-word rare-event split.
+template <int A, int K, int MODE>
+static void cpu_step_words(const oc_handle* h, const uint8_t* sin, uint8_t* sout, const uint8_t* act,
+                           uint8_t* exo, uint8_t* coll, int64_t B, int64_t P, int64_t g0, int64_t g1,
+                           uint64_t* st) {
+    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+    const LevelArgs& L = h->args;
+    const uint8_t* tbl = (const uint8_t*)L.cls4;
+    auto cls_of = [tbl](uint32_t c) -> uint32_t {
+        return (uint32_t)tbl[c & 0xFFu] | ((uint32_t)tbl[(c >> 8) & 0xFFu] << 8) |
+               ((uint32_t)tbl[(c >> 16) & 0xFFu] << 16) | ((uint32_t)tbl[c >> 24] << 24);
+    };
+    auto rd = [P](const uint8_t* base, int plane, int64_t g) {
+        uint32_t v;
+        memcpy(&v, base + plane * P + 4 * g, 4);
+        return v;
+    };
+    auto wr = [P](uint8_t* base, int plane, int64_t g, uint32_t v) { memcpy(base + plane * P + 4 * g, &v, 4); };
+    uint64_t eps = 0, succ = 0, steps = 0, ncoll = 0, err = 0;
+    for (int64_t g = g0; g < g1; ++g) {
+        uint32_t X[A], Y[A], Hh[A], Lc[K], M[K], AC[A], EX[A], T0, T1, F, CM;
+        for (int a = 0; a < A; ++a) {
+            X[a] = rd(sin, a, g);
+            Y[a] = rd(sin, kPY + a, g);
+            Hh[a] = rd(sin, kPH + a, g);
+            AC[a] = rd(act, a, g);
+        }
+        for (int j = 0; j < K; ++j) {
+            Lc[j] = rd(sin, kPL + j, g);
+            M[j] = rd(sin, kPM + j, g);
+        }
+        memcpy(&T0, sin + kPT * P + 8 * g, 4);
+        memcpy(&T1, sin + kPT * P + 8 * g + 4, 4);
+        F = rd(sin, kPF, g);
+        const uint32_t f_in = F;
+        uint32_t pending = ocsw::at_done80<K, MODE>(L.sw, Lc);
+        const bool full = ocsw::step4<A, K, MODE>(L.sw, X, Y, Hh, Lc, M, T0, T1, F, AC, EX, CM, cls_of,
+                                                  [](uint32_t v) { return v != 0u; }, pending);
+        const int64_t rem = B - g * kEPL;
+        const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (1u << (8 * (uint32_t)rem)) - 1u;
+        ncoll += (uint64_t)__builtin_popcount(CM & vmask);
+        if (full) {
+            const uint32_t ended = (F & ~f_in & vmask) & ocsw::k01;
+            for (int q = 0; q < kEPL; ++q) {
+                if (!((ended >> (8 * q)) & 1u)) continue;
+                ++eps;
+                succ += (F >> (8 * q + 1)) & 1u;
+                err += (F >> (8 * q + 2)) & 1u;
+                steps += ((q < 2 ? T0 : T1) >> (16 * (q & 1))) & 0xFFFFu;
+            }
+        }
+        for (int a = 0; a < A; ++a) {
+            wr(sout, a, g, X[a]);
+            wr(sout, kPY + a, g, Y[a]);
+            wr(sout, kPH + a, g, Hh[a]);
+            if (exo != nullptr) wr(exo, a, g, EX[a]);
+        }
+        for (int j = 0; j < K; ++j) {
+            wr(sout, kPL + j, g, Lc[j]);
+            wr(sout, kPM + j, g, M[j]);
+        }
+        memcpy(sout + kPT * P + 8 * g, &T0, 4);
+        memcpy(sout + kPT * P + 8 * g + 4, &T1, 4);
+        wr(sout, kPF, g, F);
+        if (coll != nullptr) wr(coll, 0, g, CM);
+    }
+    st[OC_STAT_EPISODES] = eps;
+    st[OC_STAT_SUCCESSES] = succ;
+    st[OC_STAT_STEPS] = steps;
+    st[OC_STAT_COLLISIONS] = ncoll;
+    st[OC_STAT_ERRORS] = err;
+}
+
 extern "C" {
 
 int oc_abi_version(void) { return OC_ABI_VERSION; }
@@ -1390,6 +1470,43 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
                        (uint8_t*)state_out, actions, exec_actions, coll_mask, stats, rows)
     OC_DISPATCH_STEP(h, OC_LAUNCH_STEP)
     return hip_check("oc_step launch");
+}
+
+int oc_cpu_step(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
+                uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* totals, int64_t B, int32_t nthreads) {
+    if (h == nullptr || state_in == nullptr || state_out == nullptr || actions == nullptr || B < 0 || nthreads < 0)
+        return fail(OC_EINVAL, "bad argument");
+    if (B == 0) return OC_OK;
+    const int64_t P = pitch_for(B), words = (B + kEPL - 1) / kEPL;
+    if (nthreads == 0) nthreads = (int32_t)std::thread::hardware_concurrency();
+    int64_t nt = nthreads < 1 ? 1 : nthreads;
+    if (nt > (words + 4095) / 4096) nt = (words + 4095) / 4096;  // >= 4096 words (16 Ki envs) per thread
+    if (nt < 1) nt = 1;
+    std::vector<uint64_t> part((size_t)nt * OC_NSTATS, 0);
+    auto run = [&](int64_t i) {
+        const int64_t g0 = words * i / nt, g1 = words * (i + 1) / nt;
+        const uint8_t* si = (const uint8_t*)state_in;
+        uint8_t* so = (uint8_t*)state_out;
+        uint64_t* st = part.data() + i * OC_NSTATS;
+#define OC_CPU_STEP(A, K, MODE) cpu_step_words<A, K, MODE>(h, si, so, actions, exec_actions, coll_mask, B, P, g0, g1, st)
+        OC_DISPATCH_STEP(h, OC_CPU_STEP)
+#undef OC_CPU_STEP
+        return OC_OK;
+    };
+    int rc = OC_OK;
+    if (nt == 1) {
+        rc = run(0);
+    } else {
+        std::vector<std::thread> pool;
+        std::vector<int> rcs((size_t)nt, OC_OK);
+        for (int64_t i = 0; i < nt; ++i) pool.emplace_back([&, i] { rcs[(size_t)i] = run(i); });
+        for (auto& t : pool) t.join();
+        for (int r : rcs) rc = rc != OC_OK ? rc : r;
+    }
+    if (rc == OC_OK && totals != nullptr)
+        for (int64_t i = 0; i < nt; ++i)
+            for (int c = 0; c < OC_NSTATS; ++c) totals[c] += part[(size_t)(i * OC_NSTATS + c)];
+    return rc;
 }
 
 int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions, void* traj,

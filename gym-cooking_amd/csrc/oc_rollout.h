@@ -107,6 +107,16 @@ struct RowT {
     OC_RH void set_mask(int j, uint32_t v) { set(mask, j, v); }
 };
 
+// Some lane of the wave (the active ones) has p: a wave-uniform trip count for the bound walks
+// (every lane of the host build is its own wave).
+OC_RH bool wave_any(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __ballot(p) != 0ull;
+#else
+    return p;
+#endif
+}
+
 // byte v occurs in one of the four bytes of w
 OC_RH bool has_byte(uint32_t w, uint32_t v) {
     const uint32_t x = w ^ (v * 0x01010101u);
@@ -388,34 +398,50 @@ struct RowOps {
         return ((const uint16_t*)(T + kNodeOff))[c * 5 + d];
     }
     OC_RH int dn(int u, int v) const {  // nx.shortest_path_length between node ids, or -1
-        if (u == kNoNode || v == kNoNode) return -1;
-        const int d = T[kDistOff + u * L.nnodes + v];
-        return d == kNone ? -1 : d;
+        // branch-free: a missing node reads entry (0, 0) and is masked, so every lane of a
+        // wave issues the same table reads
+        const bool none = u == kNoNode || v == kNoNode;
+        const int d = T[kDistOff + (none ? 0 : u * L.nnodes + v)];
+        return none || d == kNone ? -1 : d;
     }
 
     // World.get_lower_bound_between_helper (world.py:148-264) with check_bound (:266-283).  The
     // agents' node ids are looked up once, the A-side distances once per A approach and (two
     // agents) the B-side distances once per B approach, out of the pair loop; the arithmetic
-    // and the (ia, ib) order are the reference's.  Only Merge comes here: Chop and Deliver have
-    // a static B side (helper_static).
+    // is the reference's.  Only Merge comes here: Chop and Deliver have a static B side
+    // (helper_static).
+    // Uniform across lanes: the approach loops run 1 or 4 times for the whole wave (4 when some
+    // lane's square is collidable, wave_any), never a per-lane trip count.  A Floor square has
+    // one node (its own, approach 4), looked up for every approach index; repeated pairs give
+    // the same bound, which the min takes once.  The reference's (ia, ib) order does not
+    // matter: the result is a min.  (Per-lane trip counts of 1 or 4 per side left 0.56 of the
+    // lanes active per VALU instruction in oc_bounds_kernel, with more SALU than VALU
+    // instructions, profiles/r03/c5_static_b2/pmc_c5.json.)
     OC_RH float helper(const Sub& s, int ag0, int ag1, int Ac, int Bc) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
         const bool Acoll = tile(Ac) != kFloor, Bcoll = tile(Bc) != kFloor;
-        const int nA = Acoll ? 4 : 1, nB = Bcoll ? 4 : 1;
+        const int nA = wave_any(Acoll) ? 4 : 1, nB = wave_any(Bcoll) ? 4 : 1;
         const int dx = Ac % L.W - Bc % L.W, dy = Ac / L.W - Bc / L.W;
         const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
         const int u0 = nid(ag0, 4);
+        int vA[4], vB[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            vA[q] = nid(Ac, Acoll ? q : 4);
+            vB[q] = nid(Bc, Bcoll ? q : 4);
+        }
         if (s.n == 1) {
-            for (int ia = 0; ia < nA; ++ia) {
-                const int vA = nid(Ac, Acoll ? ia : 4);
-                const int a1 = dn(u0, vA);
-                if (a1 < 0) continue;
-                for (int ib = 0; ib < nB; ++ib) {
-                    const int b2 = dn(vA, nid(Bc, Bcoll ? ib : 4));
-                    if (b2 < 0) continue;
+#pragma unroll
+            for (int ia = 0; ia < 4; ++ia) {
+                if (ia >= nA) continue;  // wave-uniform
+                const int a1 = dn(u0, vA[ia]);
+#pragma unroll
+                for (int ib = 0; ib < 4; ++ib) {
+                    if (ib >= nB) continue;
+                    const int b2 = dn(vA[ia], vB[ib]);
                     const float bound = (float)(a1 + b2 - 1);
-                    if (bound < lower) lower = bound;
+                    lower = a1 >= 0 && b2 >= 0 && bound < lower ? bound : lower;
                 }
             }
             return lower > 1.0f ? lower : 1.0f;
@@ -424,19 +450,18 @@ struct RowOps {
         float b1B[4], b2B[4];
 #pragma unroll
         for (int ib = 0; ib < 4; ++ib) {
-            b1B[ib] = b2B[ib] = per;
-            if (ib < nB) {
-                const int vB = nid(Bc, Bcoll ? ib : 4);
-                int t;
-                if ((t = dn(u0, vB)) >= 0) b1B[ib] = (float)t;
-                if ((t = dn(u1, vB)) >= 0) b2B[ib] = (float)t;
-            }
-        }
-        for (int ia = 0; ia < nA; ++ia) {
-            const int vA = nid(Ac, Acoll ? ia : 4);
             int t;
-            const float b1A = (t = dn(u0, vA)) < 0 ? per : (float)t;
-            const float b2A = (t = dn(u1, vA)) < 0 ? per : (float)t;
+            b1B[ib] = b2B[ib] = per;
+            if (ib >= nB) continue;
+            b1B[ib] = (t = dn(u0, vB[ib])) < 0 ? per : (float)t;
+            b2B[ib] = (t = dn(u1, vB[ib])) < 0 ? per : (float)t;
+        }
+#pragma unroll
+        for (int ia = 0; ia < 4; ++ia) {
+            if (ia >= nA) continue;
+            int t;
+            const float b1A = (t = dn(u0, vA[ia])) < 0 ? per : (float)t;
+            const float b2A = (t = dn(u1, vA[ia])) < 0 ? per : (float)t;
 #pragma unroll
             for (int ib = 0; ib < 4; ++ib) {
                 if (ib >= nB) continue;
@@ -446,7 +471,7 @@ struct RowOps {
                     mB *= 2.0f;
                 }
                 const float bound = (mA > mB ? mA : mB) + (man - 1.0f) * 0.5f;
-                if (bound < lower) lower = bound;
+                lower = bound < lower ? bound : lower;
             }
         }
         return lower > 1.0f ? lower : 1.0f;
@@ -467,15 +492,16 @@ struct RowOps {
         float lower = per + 1.0f;
         if (nb == 0) return lower;
         const bool Acoll = tile(Ac) != kFloor;
-        const int nA = Acoll ? 4 : 1;
+        const int nA = wave_any(Acoll) ? 4 : 1;  // wave-uniform (a Floor A repeats its node)
         const int u0 = nid(ag0, 4);
         if (s.n == 1) {
-            for (int ia = 0; ia < nA; ++ia) {
+#pragma unroll
+            for (int ia = 0; ia < 4; ++ia) {
+                if (ia >= nA) continue;
                 const int vA = nid(Ac, Acoll ? ia : 4);
-                const int a1 = dn(u0, vA);
-                if (a1 < 0 || dm[vA] == kNone) continue;
-                const float bound = (float)(a1 + (int)dm[vA] - 1);
-                if (bound < lower) lower = bound;
+                const int a1 = dn(u0, vA), m = dm[vA == kNoNode ? 0 : vA];
+                const float bound = (float)(a1 + m - 1);
+                lower = vA != kNoNode && a1 >= 0 && m != kNone && bound < lower ? bound : lower;
             }
         } else {
             const int u1 = nid(ag1, 4), ax = Ac % L.W, ay = Ac / L.W;
@@ -486,7 +512,9 @@ struct RowOps {
                 man = m < man ? m : man;
             }
             float mA = per;
-            for (int ia = 0; ia < nA; ++ia) {
+#pragma unroll
+            for (int ia = 0; ia < 4; ++ia) {
+                if (ia >= nA) continue;
                 const int vA = nid(Ac, Acoll ? ia : 4);
                 int t;
                 const float b1A = (t = dn(u0, vA)) < 0 ? per : (float)t;
@@ -500,29 +528,42 @@ struct RowOps {
         return lower > 1.0f ? lower : 1.0f;
     }
 
-    // Locations of `m` as get_AB_locs_given_objs lists them: un-held items (slot order) then
-    // subtask agents holding one; `skip_deliv` drops Delivery squares (Deliver's A_locs).
-    template <class F>
-    OC_RH void visit_objs(const Row& r, int m, bool skip_deliv, F&& f) const {
+    // Locations of `m` as get_AB_locs_given_objs lists them, as a set of sources: bit k < K an
+    // un-held item in slot k, bit K + a a subtask agent a holding one; `skip_deliv` drops
+    // Delivery squares (Deliver's A_locs).  Built branch-free over every source, so the lanes
+    // of a wave only part ways in the walk over the set bits (usually 0 or 1 per side).
+    OC_RH uint32_t obj_set(const Row& r, int m, bool skip_deliv) const {
         uint32_t held = 0;
 #pragma unroll
-        for (int a = 0; a < A; ++a)
-            if (r.ah(a) != kNone) held |= 1u << r.ah(a);
-        // one rolled loop with one call site: f (a bound walk) is inlined once, not K + A times
-#pragma unroll 1
-        for (int k = 0; k < K + A; ++k) {
-            int c;
-            if (k < K) {
-                c = r.il(k);
-                if (c == kNone || r.im(k) != m || ((held >> k) & 1u)) continue;
-            } else {
-                const int a = k - K, h = r.ah(a);
-                if (!((active >> a) & 1u) || h == kNone || r.im(h) != m) continue;
-                c = agent_cell(r, a);
-            }
-            if (skip_deliv && static_tile(c) == kDelivery) continue;
-            f(c);
+        for (int a = 0; a < A; ++a) {
+            const int h = r.ah(a);
+            held |= h != kNone ? 1u << (h & 31) : 0u;
         }
+        uint32_t set = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int c = r.il(k);
+            const bool ok = c != kNone && r.im(k) == m && !((held >> k) & 1u) &&
+                            !(skip_deliv && static_tile(c) == kDelivery);
+            set |= ok ? 1u << k : 0u;
+        }
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            const int h = r.ah(a);
+            const bool ok = ((active >> a) & 1u) && h != kNone && r.im(h) == m &&
+                            !(skip_deliv && static_tile(agent_cell(r, a)) == kDelivery);
+            set |= ok ? 1u << (K + a) : 0u;
+        }
+        return set;
+    }
+    OC_RH int src_cell(const Row& r, int k) const { return k < K ? r.il(k) : agent_cell(r, k - K); }
+
+    // f(cell) for every location of obj_set (slot order, then agents); one rolled loop with one
+    // call site: f (a bound walk) is inlined once, not K + A times
+    template <class F>
+    OC_RH void visit_objs(const Row& r, int m, bool skip_deliv, F&& f) const {
+#pragma unroll 1
+        for (uint32_t set = obj_set(r, m, skip_deliv); set != 0u; set &= set - 1u) f(src_cell(r, __builtin_ctz(set)));
     }
 
     // get_lower_bound_for_subtask_given_objs (overcooked_environment.py:594-664)

@@ -20,13 +20,15 @@
 //   copy crash (ERR)                   overcooked_environment.py:289 -> :108-113 -> world.py:417
 //   done / reward                      overcooked_environment.py:316-376
 //
-// The includer provides __device__/__forceinline__ and the __builtin_amdgcn_* intrinsics
-// (the HIP compiler; tests/swar_host/ builds this header on the host for unit tests).
+// The includer provides __host__/__device__/__forceinline__ (the HIP compiler; tests/swar_host/
+// builds this header with plain clang++).  Every function here is host and device code: the
+// device pass uses the two AMDGCN intrinsics (v_perm_b32, v_bitop3_b32), the host pass the
+// bit-exact restatements below; the host pass is oc_cpu_step's step (include/oc_engine.h).
 #pragma once
 
 #include <stdint.h>
 
-#define OC_SW __device__ __forceinline__
+#define OC_SW __host__ __device__ __forceinline__
 
 namespace ocsw {
 
@@ -43,22 +45,54 @@ constexpr uint32_t lut3(F f) {
     return r;
 }
 #define OC_LUT(expr) ::ocsw::lut3([](int a, int b, int c) constexpr { (void)a; (void)b; (void)c; return (expr); })
+// v_bitop3_b32: bit i of the result is IMM's bit (a_i << 2 | b_i << 1 | c_i).  On the host
+// IMM is a constant, so the minterm loop folds to a few logic operations.
 template <uint32_t IMM>
-OC_SW uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, IMM); }
+OC_SW uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, IMM);
+#else
+    uint32_t r = 0;
+    for (int i = 0; i < 8; ++i)
+        if (IMM & (1u << i)) r |= ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
+    return r;
+#endif
+}
 
 OC_SW uint32_t sel(uint32_t m, uint32_t a, uint32_t b) { return bop3<OC_LUT(a ? b : c)>(m, a, b); }
 OC_SW uint32_t and3(uint32_t a, uint32_t b, uint32_t c) { return bop3<OC_LUT(a & b & c)>(a, b, c); }
 OC_SW uint32_t or3(uint32_t a, uint32_t b, uint32_t c) { return bop3<OC_LUT(a | b | c)>(a, b, c); }
 OC_SW uint32_t andn(uint32_t a, uint32_t b) { return bop3<OC_LUT(a & !b)>(a, b, 0u); }  // a & ~b
-OC_SW uint32_t perm(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_perm(hi, lo, s); }
+// v_perm_b32: result byte i = selector byte s_i of {hi:lo}: 0-7 a source byte, 8-11 the sign
+// of a 16-bit half replicated, 12 zero, 13 and up 0xFF.
+OC_SW uint32_t perm(uint32_t hi, uint32_t lo, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(hi, lo, s);
+#else
+    // branch-free: a 16-entry byte table (8 source bytes, 4 sign bytes, 0x00, 3 x 0xFF)
+    // indexed by min(q, 13)
+    const uint64_t src = ((uint64_t)hi << 32) | lo;
+    uint8_t tab[16];
+    for (int i = 0; i < 8; ++i) tab[i] = (uint8_t)(src >> (8 * i));
+    for (int i = 0; i < 4; ++i) tab[8 + i] = (uint8_t)(((src >> (16 * i + 15)) & 1u) ? 0xFFu : 0u);
+    tab[12] = 0u;
+    tab[13] = tab[14] = tab[15] = 0xFFu;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t q = (s >> (8 * i)) & 0xFFu;
+        r |= (uint32_t)tab[q < 13u ? q : 13u] << (8 * i);
+    }
+    return r;
+#endif
+}
 
-// In-place updates for the rare path of step4: x = m ? a : x, x &= ~m, x |= m, with the result
-// in x's own register.  The device build (oc_engine.hip) defines them as inline asm whose
-// output is tied to x: the rare path then rewrites the common path's registers, and the
-// common path, where x passes through unchanged, needs no copy per state word at the join
-// (with plain selects the compiler gave the join the rare path's registers and copied 25
-// words on every common-path step).  `a` is wave-uniform (a level constant).  Other
-// includers (the host test harness) get plain C.
+// In-place updates for the rare path of step4: x = m ? a : x, x &= ~m, x |= m.  Both builds
+// (oc_engine.hip and the host test harness) use the plain-C forms below.  A device variant
+// with inline asm tied to x (so that the common path, where x passes through, needs no copy
+// at the join) was compiled and dropped: the step_n kernels came out larger (A = 2: 713 vs
+// 699 VALU instructions; A = 3 with the loader wave: 1,115 vs 948), as the asm blocks pin
+// the operands' registers and keep the compiler from folding the selects.  The hooks stay
+// for such experiments.
 #ifndef OC_TIED_SEL
 #define OC_TIED_SEL(x, m, a) ((x) = ::ocsw::sel((m), (a), (x)))
 #define OC_TIED_ANDN(x, m) ((x) = ::ocsw::andn((x), (m)))

@@ -20,7 +20,7 @@ OC_MAX_CELLS = 255
 OC_MAX_GOALS = 4
 OC_PITCH_ALIGN = 4096
 OC_NSTATS = 5
-OC_ABI_VERSION = 6  # include/oc_engine.h
+OC_ABI_VERSION = 7  # include/oc_engine.h
 OC_EINVAL, OC_EHIP, OC_ELEVEL = -1, -2, -3
 
 OC_FLAG_DONE = 0x01
@@ -32,7 +32,7 @@ OC_STAT_NAMES = ("episodes", "successes", "steps", "collisions", "errors")
 # Every symbol include/oc_engine.h declares (tests check the library exports them all).
 EXPORTED_SYMBOLS = (
     "oc_abi_version", "oc_last_error", "oc_create", "oc_destroy", "oc_get_layout", "oc_reset",
-    "oc_step", "oc_step_n", "oc_rollout", "oc_nav_likelihood", "oc_subtask_bounds", "oc_reachability", "oc_render", "oc_render_ordered",
+    "oc_step", "oc_step_n", "oc_cpu_step", "oc_rollout", "oc_nav_likelihood", "oc_subtask_bounds", "oc_reachability", "oc_render", "oc_render_ordered",
     "oc_gen_actions", "oc_state_checksum", "oc_stats_size", "oc_stats_reduce",
 )
 
@@ -187,6 +187,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.oc_render.argtypes = [vp, vp, vp, vp, ctypes.POINTER(OcRenderDesc), vp, i64, vp]
     lib.oc_render_ordered.restype = ctypes.c_int
     lib.oc_render_ordered.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(OcRenderDesc), vp, i64, vp]
+    lib.oc_cpu_step.restype = ctypes.c_int
+    lib.oc_cpu_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i32]
     lib.oc_step_n.restype = ctypes.c_int
     lib.oc_step_n.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]
     lib.oc_gen_actions.restype = ctypes.c_int

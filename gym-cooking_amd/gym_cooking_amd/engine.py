@@ -25,6 +25,16 @@ def _ptr(t: Optional[torch.Tensor]):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def _bound(fn, args):
+    """A zero-argument callable issuing fn(*args) and raising on its status: one ctypes call
+    per launch (the arguments were validated and converted when it was made)."""
+    check = capi.check
+
+    def launch():
+        check(fn(*args))
+    return launch
+
+
 class OvercookedBatch:
     """B envs of one level on one GPU.
 
@@ -160,47 +170,58 @@ class OvercookedBatch:
             self._check(totals, 8 * capi.OC_NSTATS, _U64)
         args = (self._h, _ptr(state_in), _ptr(state_out), _ptr(actions), _ptr(traj), _ptr(exec_out), _ptr(coll),
                 _ptr(stats), _ptr(totals), self.B, int(n), self._stream())
-        fn, check = self.lib.oc_step_n, capi.check
-
-        def launch():
-            check(fn(*args))
-        return launch
+        return _bound(self.lib.oc_step_n, args)
 
     def rollout(self, state_in: torch.Tensor, state_out: torch.Tensor, actions: torch.Tensor, subtasks,
                 alloc: Optional[torch.Tensor] = None, flags: Optional[torch.Tensor] = None,
                 lower_bound: Optional[torch.Tensor] = None):
         """Navigation-planner rollout rows (oc_rollout): the Level-0 next state of every row
         under its subtask configuration, and (flags u8 [pitch], lower bound f32 [pitch])."""
+        flags = torch.empty(self.pitch, dtype=torch.uint8, device=self.device) if flags is None else flags
+        lower_bound = (torch.empty(self.pitch, dtype=torch.float32, device=self.device)
+                       if lower_bound is None else lower_bound)
+        self.rollout_launcher(state_in, state_out, actions, subtasks, alloc, flags, lower_bound)()
+        return flags, lower_bound
+
+    def rollout_launcher(self, state_in: torch.Tensor, state_out: torch.Tensor, actions: torch.Tensor, subtasks,
+                         alloc: Optional[torch.Tensor], flags: torch.Tensor, lower_bound: torch.Tensor):
+        """An oc_rollout call bound once (buffers validated, the subtask table packed): the
+        returned callable issues it on the stream current now with one ctypes call."""
         self._check(state_in, self.layout.state_bytes)
         self._check(state_out, self.layout.state_bytes)
         self._check(actions, self.A * self.pitch)
         if alloc is not None:
             self._check(alloc, self.pitch)
-        flags = torch.empty(self.pitch, dtype=torch.uint8, device=self.device) if flags is None else flags
-        lower_bound = (torch.empty(self.pitch, dtype=torch.float32, device=self.device)
-                       if lower_bound is None else lower_bound)
         self._check(flags, self.pitch)
         self._check(lower_bound, 4 * self.pitch, (torch.float32,))
         subs = capi.subtask_array(subtasks)
-        capi.check(self.lib.oc_rollout(self._h, _ptr(state_in), _ptr(state_out), _ptr(actions), _ptr(alloc), subs,
-                                       len(subtasks), _ptr(flags), _ptr(lower_bound), self.B, self._stream()))
-        return flags, lower_bound
+        args = (self._h, _ptr(state_in), _ptr(state_out), _ptr(actions), _ptr(alloc), subs, len(subtasks),
+                _ptr(flags), _ptr(lower_bound), self.B, self._stream())
+        return _bound(self.lib.oc_rollout, args)
 
     def nav_likelihood(self, state: torch.Tensor, taken: torch.Tensor, subtasks, self_agent: int,
                        beta: float = 1.3, none_action_prob: float = 0.5, alloc: Optional[torch.Tensor] = None):
         """Bayesian-delegation likelihoods (oc_nav_likelihood): prob_nav_actions of every row's
         allocation given the executed actions `taken` (u8 [A][pitch]); returns
         (likelihood f64 [pitch], flags u8 [pitch])."""
+        out = torch.empty(self.pitch, dtype=torch.float64, device=self.device)
+        flags = torch.empty(self.pitch, dtype=torch.uint8, device=self.device)
+        self.nav_likelihood_launcher(state, taken, subtasks, self_agent, beta, none_action_prob, alloc, out, flags)()
+        return out, flags
+
+    def nav_likelihood_launcher(self, state: torch.Tensor, taken: torch.Tensor, subtasks, self_agent: int,
+                                beta: float, none_action_prob: float, alloc: Optional[torch.Tensor],
+                                out: torch.Tensor, flags: torch.Tensor):
+        """An oc_nav_likelihood call bound once (see rollout_launcher)."""
         self._check(state, self.layout.state_bytes)
         self._check(taken, self.A * self.pitch)
         if alloc is not None:
             self._check(alloc, self.pitch)
-        out = torch.empty(self.pitch, dtype=torch.float64, device=self.device)
-        flags = torch.empty(self.pitch, dtype=torch.uint8, device=self.device)
-        capi.check(self.lib.oc_nav_likelihood(self._h, _ptr(state), _ptr(taken), _ptr(alloc),
-                                              capi.subtask_array(subtasks), len(subtasks), self_agent, beta,
-                                              none_action_prob, _ptr(out), _ptr(flags), self.B, self._stream()))
-        return out, flags
+        self._check(out, 8 * self.pitch, (torch.float64,))
+        self._check(flags, self.pitch)
+        args = (self._h, _ptr(state), _ptr(taken), _ptr(alloc), capi.subtask_array(subtasks), len(subtasks),
+                self_agent, beta, none_action_prob, _ptr(out), _ptr(flags), self.B, self._stream())
+        return _bound(self.lib.oc_nav_likelihood, args)
 
     def subtask_bounds(self, state: torch.Tensor, subtasks, lower_bound: Optional[torch.Tensor] = None,
                        doable: Optional[torch.Tensor] = None):
@@ -208,16 +229,23 @@ class OvercookedBatch:
         get_lower_bound_for_subtask_given_objs and subtask_alloc_is_doable; returns
         (lower bound f32 [S][pitch], doable u8 [S][pitch])."""
         S = len(subtasks)
-        self._check(state, self.layout.state_bytes)
         if lower_bound is None:
             lower_bound = torch.empty((S, self.pitch), dtype=torch.float32, device=self.device)
         if doable is None:
             doable = torch.empty((S, self.pitch), dtype=torch.uint8, device=self.device)
+        self.subtask_bounds_launcher(state, subtasks, lower_bound, doable)()
+        return lower_bound, doable
+
+    def subtask_bounds_launcher(self, state: torch.Tensor, subtasks, lower_bound: torch.Tensor,
+                                doable: torch.Tensor):
+        """An oc_subtask_bounds call bound once (see rollout_launcher)."""
+        S = len(subtasks)
+        self._check(state, self.layout.state_bytes)
         self._check(lower_bound, 4 * S * self.pitch, (torch.float32,))
         self._check(doable, S * self.pitch)
-        capi.check(self.lib.oc_subtask_bounds(self._h, _ptr(state), capi.subtask_array(subtasks), S,
-                                              _ptr(lower_bound), _ptr(doable), self.B, self._stream()))
-        return lower_bound, doable
+        args = (self._h, _ptr(state), capi.subtask_array(subtasks), S, _ptr(lower_bound), _ptr(doable), self.B,
+                self._stream())
+        return _bound(self.lib.oc_subtask_bounds, args)
 
     def reachability(self):
         """The level's static reachability graph (oc_reachability): (node_of u16 [W*H*5] with
@@ -262,3 +290,55 @@ class OvercookedBatch:
             raise ValueError("buffer too small: %d < %d bytes" % (t.numel() * t.element_size(), nbytes))
         if t.data_ptr() % 16:
             raise ValueError("buffer must be 16-byte aligned")
+
+
+class CpuStepper:
+    """oc_cpu_step: the engine's step on the host, for a caller without a GPU (numpy buffers in
+    the oc_step layout).  The same SWAR step as the kernels (its host pass); the GPU path never
+    calls it.  `step` mirrors OvercookedBatch.step (overcooked_environment.py:255-306)."""
+
+    def __init__(self, level, num_agents: int, B: int, max_T: int = 100, nthreads: int = 0):
+        if isinstance(level, str):
+            level = _levels.load_level(level)
+        self.level, self.A, self.B, self.max_T, self.nthreads = level, num_agents, int(B), max_T, nthreads
+        self.lib = capi.load_library()
+        self._desc = capi.level_desc(level, num_agents)
+        h = ctypes.c_void_p()
+        capi.check(self.lib.oc_create(ctypes.byref(self._desc), num_agents, max_T, 0, ctypes.byref(h)))
+        self._h = h
+        lay = capi.OcLayout()
+        capi.check(self.lib.oc_get_layout(self._h, self.B, ctypes.byref(lay)))
+        self.layout, self.K, self.pitch = lay, lay.num_items, lay.pitch
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and getattr(self, "lib", None) is not None:
+            self.lib.oc_destroy(h)
+            self._h = None
+
+    def new_state(self) -> np.ndarray:
+        """The level template in every env (reset(), overcooked_environment.py:201-250), built
+        on the host from the level description."""
+        A, K, P = self.A, self.K, self.pitch
+        s = np.zeros((self.layout.num_planes, P), np.uint8)
+        lv = self.level
+        for a in range(A):
+            s[a], s[A + a], s[2 * A + a] = lv.spawns[a][0], lv.spawns[a][1], 0xFF
+        for j in range(K):
+            c, m = (lv.items[j] if j < len(lv.items) else (0xFF, 0))
+            s[3 * A + j], s[3 * A + K + j] = c, m
+        return s.reshape(-1)
+
+    def step(self, state_in: np.ndarray, state_out: np.ndarray, actions: np.ndarray,
+             exec_out: Optional[np.ndarray] = None, coll: Optional[np.ndarray] = None,
+             totals: Optional[np.ndarray] = None) -> np.ndarray:
+        for a, n in ((state_in, self.layout.state_bytes), (state_out, self.layout.state_bytes),
+                     (actions, self.A * self.pitch), (exec_out, self.A * self.pitch), (coll, self.pitch)):
+            if a is not None and (a.dtype != np.uint8 or not a.flags.c_contiguous or a.nbytes < n):
+                raise ValueError("host buffers: contiguous uint8 of at least %d bytes" % n)
+        if totals is not None and (totals.dtype not in (np.uint64, np.int64) or totals.size < capi.OC_NSTATS):
+            raise ValueError("totals: %d uint64" % capi.OC_NSTATS)
+        p = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+        capi.check(self.lib.oc_cpu_step(self._h, p(state_in), p(state_out), p(actions), p(exec_out), p(coll),
+                                        p(totals), self.B, self.nthreads))
+        return state_out

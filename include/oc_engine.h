@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define OC_ABI_VERSION 6
+#define OC_ABI_VERSION 7
 
 #define OC_MAX_AGENTS 4
 #define OC_MAX_ITEMS 16  /* item slots: K = 4, 8 or 16 per level */
@@ -195,6 +195,18 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
 int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions, void* traj,
               uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, uint64_t* totals, int64_t B, int32_t n,
               void* stream);
+
+/* The same step on the host, for a caller without a GPU (a CPU restatement behind
+ * the same ABI, same layout).  step(), overcooked_environment.py:255-306, exactly as oc_step:
+ * the host pass of the kernel's own SWAR step (oc_swar.h, four envs per 32-bit word, the
+ * v_perm / v_bitop3 byte operations restated bit for bit), threaded over env ranges.
+ *   state_in/state_out, actions, exec_actions, coll_mask : HOST buffers in the oc_step layout
+ *                 (state_in may equal state_out)
+ *   totals      : nullable; OC_NSTATS host uint64, the window's statistics ADDED to it
+ *   nthreads    : worker threads (0 = the host's hardware threads; at least 16 Ki envs each)
+ * It never touches the device; oc_step / oc_step_n never call it (no CPU fallback). */
+int oc_cpu_step(const oc_handle* h, const void* state_in, void* state_out, const uint8_t* actions,
+                uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* totals, int64_t B, int32_t nthreads);
 
 /* Synthetic i.i.d. uniform action codes 0..4 for B envs at step `step`:
  * code = splitmix64(seed ^ gid*0x9E3779B97F4A7C15 ^ step*0xC2B2AE3D27D4EB4F ^ agent) % 5,

@@ -1,35 +1,13 @@
 // TEST INFRASTRUCTURE: host build of the device SWAR step (gym-cooking_amd/csrc/oc_swar.h)
 // so its logic can be checked against the CPU oracle without a GPU.  The two AMDGCN
-// intrinsics it uses are emulated bit-exactly below (v_perm_b32, v_bitop3_b32 semantics);
-// the product library never contains this file.
+// intrinsics it uses have bit-exact host restatements in the header (the host pass of
+// oc_swar.h, which is also oc_cpu_step's); the product library never contains this file.
 #include <stdint.h>
 #include <string.h>
 
-static inline uint32_t host_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
-    const uint64_t src = ((uint64_t)hi << 32) | lo;
-    uint32_t r = 0;
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t s = (sel >> (8 * i)) & 0xFFu;
-        uint32_t b;
-        if (s < 8) b = (uint32_t)(src >> (8 * s)) & 0xFFu;
-        else if (s < 12) b = ((src >> (16 * (s - 8) + 15)) & 1u) ? 0xFFu : 0u;  // sign of a 16-bit half
-        else if (s == 12) b = 0u;
-        else b = 0xFFu;
-        r |= b << (8 * i);
-    }
-    return r;
-}
-static inline uint32_t host_bitop3(uint32_t a, uint32_t b, uint32_t c, uint32_t imm) {
-    uint32_t r = 0;
-    for (int i = 0; i < 8; ++i)
-        if (imm & (1u << i)) r |= ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
-    return r;
-}
 #define __device__
 #define __host__
 #define __forceinline__ inline
-#define __builtin_amdgcn_perm host_perm
-#define __builtin_amdgcn_bitop3_b32 host_bitop3
 
 #include "../../gym-cooking_amd/csrc/oc_swar.h"
 #include "../../include/oc_engine.h"

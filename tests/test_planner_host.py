@@ -288,3 +288,19 @@ def test_native_sample_trial_matches_python_loop():
         assert a1 == a2
         for (l1, u1, g1), (l2, u2, g2) in zip(t1, t2):
             assert l1 == l2 and u1 == u2 and g1 == g2
+
+
+def test_native_errors_raise_python_exceptions():
+    """The extension's error paths set a Python exception (no SystemError): an expanded state
+    with no actions raises ValueError as Python's min() of an empty sequence does, and so does
+    an empty tie pick."""
+    from gym_cooking_amd import planner as pl
+    nat = pl._native
+    assert nat is not None, "the _brtdp extension is not built (make -C gym-cooking_amd/csrc)"
+    with pytest.raises(ValueError):
+        nat.tie_pick([], lambda: 0.5)
+    entry = [None, [], [], [], None, None, True, None, "rx"]
+    with pytest.raises(ValueError):
+        nat.backprop({("x", "sk"): entry}, {}, {}, ["x"], "sk")
+    with pytest.raises(ValueError):
+        nat.forward({("x", "sk"): entry}, {}, {}, "x", "sk", "x", 10, 0, 2.0, [], lambda: 0.5, False)

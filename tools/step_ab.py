@@ -60,12 +60,15 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--child", nargs=4)
+    ap.add_argument("--agents", type=int, nargs="*", help="only the configurations with these agent counts")
     a = ap.parse_args()
     if a.child:
         lib, level, A, n = a.child
         return child(lib, level, int(A), int(n), a.batch, a.reps)
     for r in range(a.rounds):
         for level, A, n in CONFIGS:
+            if a.agents and A not in a.agents:
+                continue
             for lib in a.libs:
                 out = subprocess.run([sys.executable, __file__, "--batch", str(a.batch), "--reps", str(a.reps),
                                       "--child", os.path.abspath(lib), level, str(A), str(n)],
