@@ -564,6 +564,9 @@ def main() -> int:
     ap.add_argument("--kernel-replay-ms", type=float, default=20.0,
                     help="after the timed region, replay its launches back to back for about this long between "
                          "two HIP events to measure the dominant kernel's mean launch duration")
+    ap.add_argument("--window-actions", choices=("fresh", "replay"), default="fresh",
+                    help="fresh: the window's actions are written by gen_actions just before it; replay: the "
+                         "window's launches run once, untimed, just before it (both leave them cache-resident)")
     ap.add_argument("--no-graph", action="store_true", help="per-step line: eager launches instead of a hipGraph")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -677,8 +680,12 @@ def main() -> int:
         f()
     s_a.copy_(end)
     warm_steps += w_run
-    for i in range(K):  # the window's actions, written now (same values as generated above)
-        eb.gen_actions(acts[i], step=i, seed=args.seed, env_offset=sh.env_offset)
+    if args.window_actions == "fresh":
+        for i in range(K):  # the window's actions, written now (same values as generated above)
+            eb.gen_actions(acts[i], step=i, seed=args.seed, env_offset=sh.env_offset)
+    else:  # "replay": the window's own launches once, untimed (they read s_a and write outs only)
+        for f in timed:
+            f()
     stats.zero_()
     torch.cuda.synchronize()
 
@@ -772,8 +779,9 @@ def main() -> int:
                       "mask written to HBM" % (len(segs), n_per),
             "warmup_steps_run": warm_steps,
             "window_starts_after_steps": w_run,
-            "window_actions": "written by gen_actions just before the window (untimed); the warmup steps another "
-                              "stream",
+            "window_actions": ("written by gen_actions just before the window (untimed)" if args.window_actions == "fresh"
+                               else "read by an untimed run of the window's launches just before it") +
+                              "; the warmup steps another stream",
         },
         "open_loop": True,
         "window_cold_actions": {

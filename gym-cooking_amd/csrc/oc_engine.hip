@@ -281,7 +281,10 @@ __host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
 // each stepping wave the steps it took; a ring of 8 steps, s_sleep polls, no barrier) was
 // measured slower: C3 100-step launches 6.28-6.41 us/step against 6.06-6.12 with the barrier,
 // four alternating rounds on one box, outputs identical (profiles/r04/lw_flags_ab.jsonl).
-constexpr int kLwSteps = 4;
+#ifndef OC_LW_STEPS
+#define OC_LW_STEPS 4
+#endif
+constexpr int kLwSteps = OC_LW_STEPS;  // steps per ring half (one barrier per kLwSteps steps)
 // A = 3 only: there the stepping waves' drains were a fifth of the time (C3, 100-step launches,
 // one box: 6.42 -> 6.07 us/step, outputs identical).  At A <= 2 the step is store-bound and the
 // block-wide barrier every kLwSteps steps costs more than the drains (2 agents, 20-step launch:
@@ -550,25 +553,55 @@ __device__ __forceinline__ void stage_roll_tables(const RollArgs& R, const uint8
     __syncthreads();
 }
 
-template <int A, int K>
-__device__ __forceinline__ ocro::RowT<K> load_row(const uint8_t* __restrict__ sin, int64_t P, int64_t e) {
-    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
-    ocro::RowT<K> r;
+// Plane indices of the state layout (oc_get_layout): a wide level (u16 cells) has its item
+// cells' high bytes in K planes after the low ones.
+template <int A, int K, bool W>
+struct Planes {
+    static constexpr int X = 0, Y = A, H = 2 * A, L = 3 * A, LH = 3 * A + K, M = 3 * A + (W ? 2 : 1) * K;
+    static constexpr int T = M + K, F = T + 2, NP = F + 1;
+};
+
+template <int A, int K, bool W = false>
+__device__ __forceinline__ ocro::RowT<K, W> load_row(const uint8_t* __restrict__ sin, int64_t P, int64_t e) {
+    using PL = Planes<A, K, W>;
+    using Row = ocro::RowT<K, W>;
+    Row r;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
         r.x |= (uint32_t)sin[a * P + e] << (8 * a);
-        r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
-        r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
+        r.y |= (uint32_t)sin[(PL::Y + a) * P + e] << (8 * a);
+        r.h |= (uint32_t)sin[(PL::H + a) * P + e] << (8 * a);
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        r.loc[j >> 3] |= (uint64_t)sin[(kPL + j) * P + e] << (8 * (j & 7));
-        r.mask[j >> 3] |= (uint64_t)sin[(kPM + j) * P + e] << (8 * (j & 7));
+        uint64_t c = sin[(PL::L + j) * P + e];
+        if (W) c |= (uint64_t)sin[(PL::LH + j) * P + e] << 8;
+        r.loc[j / Row::LPW] |= c << (Row::kLocBits * (j % Row::LPW));
+        r.mask[j >> 3] |= (uint64_t)sin[(PL::M + j) * P + e] << (8 * (j & 7));
     }
     return r;
 }
 
-template <int A, int K>
+// the row's agent and item planes (t and flags are the caller's)
+template <int A, int K, bool W = false>
+__device__ __forceinline__ void store_row(uint8_t* __restrict__ sout, int64_t P, int64_t e, const ocro::RowT<K, W>& r) {
+    using PL = Planes<A, K, W>;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        sout[a * P + e] = (uint8_t)r.ax(a);
+        sout[(PL::Y + a) * P + e] = (uint8_t)r.ay(a);
+        sout[(PL::H + a) * P + e] = (uint8_t)r.ah(a);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const uint32_t c = (uint32_t)r.il(j);
+        sout[(PL::L + j) * P + e] = (uint8_t)c;
+        if (W) sout[(PL::LH + j) * P + e] = (uint8_t)(c >> 8);
+        sout[(PL::M + j) * P + e] = (uint8_t)r.im(j);
+    }
+}
+
+template <int A, int K, bool W>
 __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                             uint8_t* __restrict__ sout,
                                                             const uint8_t* __restrict__ act,
@@ -581,33 +614,23 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
     stage_roll_tables(R, blob_g, blob_w, subs);
     const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
-    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+    using PL = Planes<A, K, W>;
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-        ocro::RowT<K> r = load_row<A, K>(sin, P, e);
-        const uint16_t t = ((const uint16_t*)(sin + kPT * P))[e];
-        const uint8_t fl_in = sin[kPF * P + e];
+        ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
+        const uint16_t t = ((const uint16_t*)(sin + PL::T * P))[e];
+        const uint8_t fl_in = sin[PL::F * P + e];
         const int ai = alloc != nullptr ? alloc[e] : 0;
         float bound = 0.0f;
         int f = OC_ROLL_BADALLOC;  // an alloc id past num_subtasks: the row is copied unchanged
         if (ai < R.nsub) {
             const ocro::Sub& s = subs[ai];
             const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
-            ocro::RowOps<A, K> ops(R.L, blob);
+            ocro::RowOps<A, K, W> ops(R.L, blob);
             f = ops.run(r, s, c0, c1, bound);
         }
-#pragma unroll
-        for (int a = 0; a < A; ++a) {
-            sout[a * P + e] = (uint8_t)r.ax(a);
-            sout[(kPY + a) * P + e] = (uint8_t)r.ay(a);
-            sout[(kPH + a) * P + e] = (uint8_t)r.ah(a);
-        }
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            sout[(kPL + j) * P + e] = (uint8_t)r.il(j);
-            sout[(kPM + j) * P + e] = (uint8_t)r.im(j);
-        }
-        ((uint16_t*)(sout + kPT * P))[e] = t;
-        sout[kPF * P + e] = fl_in;
+        store_row<A, K, W>(sout, P, e, r);
+        ((uint16_t*)(sout + PL::T * P))[e] = t;
+        sout[PL::F * P + e] = fl_in;
         out_flags[e] = (uint8_t)f;
         lb[e] = bound;
     }
@@ -630,7 +653,7 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
 // 0.35 ms configuration-major, 0.55 ms random order, against 0.44 / 1.29 ms with G = 8; a
 // one-agent table 0.19 ms with G = 8, 0.41 with G = 32.  The None subtask's closed form runs
 // on the group's first lane.
-template <int A, int K, int G>
+template <int A, int K, int G, bool W>
 __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                                const uint8_t* __restrict__ taken_p,
                                                                const uint8_t* __restrict__ alloc,
@@ -651,11 +674,11 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
         int f = OC_LIK_BADALLOC;
         if (ai < R.nsub) {
             const ocro::Sub& s = subs[ai];
-            ocro::RowT<K> r = load_row<A, K>(sin, P, e);
+            ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
             uint32_t taken = 0;
 #pragma unroll
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
-            ocro::RowOps<A, K> ops(R.L, blob);
+            ocro::RowOps<A, K, W> ops(R.L, blob);
             if (s.kind == 0) {
                 f = 0;
                 if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
@@ -754,7 +777,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
 // (configurations and tables in LDS).  Output [subtask][pitch], so each store instruction of a
 // wave covers 64 consecutive envs of one configuration.  Chunking the table multiplies the
 // waves of a launch: the walk is LDS-latency bound and one chunk left 4 waves per SIMD.
-template <int A, int K>
+template <int A, int K, bool W>
 __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                            const uint8_t* __restrict__ blob_g,
                                                            float* __restrict__ lb, uint8_t* __restrict__ doable) {
@@ -764,8 +787,8 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
     const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-        const ocro::RowT<K> r = load_row<A, K>(sin, P, e);
-        ocro::RowOps<A, K> ops(R.L, blob);
+        const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
+        ocro::RowOps<A, K, W> ops(R.L, blob);
         const int i0 = (int)(blockIdx.y * R.nsub / gridDim.y), i1 = (int)((blockIdx.y + 1) * R.nsub / gridDim.y);
         for (int i = i0; i < i1; ++i) {
             float v;
@@ -774,6 +797,101 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
             doable[i * P + e] = ok ? 1 : 0;
         }
     }
+}
+
+// ---- wide levels (more than 255 cells: u16 cell ids) ----------------------------------------
+// The byte-cell SWAR step does not reach past 255 cells; a wide level steps one env per lane
+// with the scalar restatement of the same rules (ocro::RowOps::env_step), over
+// byte-plane loads and stores (64 consecutive bytes per wave instruction).  Such levels are
+// user kitchens; the shipped ones are all narrow.
+struct WideArgs {
+    ocro::RollLevel L;   // W, H, enc; tile_off 0: the table below
+    ocro::StepLevel S;
+    int32_t tile_words;  // the tile-class table's words (W * H bytes rounded up to 4)
+    int64_t pitch, B;
+};
+
+// n steps of every env (oc_step: n = 1, no trajectory): the state stays in registers between
+// the steps; step r's state goes to traj[r] (when given), its executed actions and collision
+// mask to exec_out / coll_out at r * A * pitch / r * pitch; the final state to sout.
+template <int A, int K>
+__global__ __launch_bounds__(kBlock) void oc_step_wide_kernel(WideArgs R, const uint8_t* __restrict__ tiles_g,
+                                                              const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
+                                                              const uint8_t* __restrict__ act,
+                                                              uint8_t* __restrict__ traj, uint8_t* __restrict__ exec_out,
+                                                              uint8_t* __restrict__ coll_out, uint64_t* __restrict__ stats,
+                                                              uint32_t stat_rows, int n) {
+    __shared__ uint32_t tiles_w[ocro::kMaxCellsWide / 4];
+    for (int i = threadIdx.x; i < R.tile_words; i += kBlock) tiles_w[i] = ((const uint32_t*)tiles_g)[i];
+    __syncthreads();
+    using PL = Planes<A, K, true>;
+    const int64_t P = R.pitch;
+    StepStats st;
+    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
+        ocro::RowT<K, true> r = load_row<A, K, true>(sin, P, e);
+        uint32_t t = ((const uint16_t*)(sin + PL::T * P))[e], fl = sin[PL::F * P + e];
+        ocro::RowOps<A, K, true> ops(R.L, (const uint8_t*)tiles_w);
+        for (int q = 0; q < n; ++q) {
+            uint32_t a = 0, ex, cm;
+#pragma unroll
+            for (int i = 0; i < A; ++i) a |= (uint32_t)act[((int64_t)q * A + i) * P + e] << (8 * i);
+            const uint32_t f = ops.env_step(r, t, fl, a, R.S, ex, cm);
+            if ((f & 1u) && !(fl & 1u)) {  // an episode ended (DONE newly set)
+                st.eps += 1u;
+                st.succ += (f >> 1) & 1u;
+                st.err += (f >> 2) & 1u;
+                st.steps += t;
+            }
+            st.coll += __popc(cm);
+            fl = f;
+            if (traj != nullptr) {
+                uint8_t* o = traj + (int64_t)q * PL::NP * P;
+                store_row<A, K, true>(o, P, e, r);
+                ((uint16_t*)(o + PL::T * P))[e] = (uint16_t)t;
+                o[PL::F * P + e] = (uint8_t)fl;
+            }
+            if (exec_out != nullptr) {
+#pragma unroll
+                for (int i = 0; i < A; ++i) exec_out[((int64_t)q * A + i) * P + e] = (uint8_t)(ex >> (8 * i));
+            }
+            if (coll_out != nullptr) coll_out[(int64_t)q * P + e] = (uint8_t)cm;
+        }
+        store_row<A, K, true>(sout, P, e, r);
+        ((uint16_t*)(sout + PL::T * P))[e] = (uint16_t)t;
+        sout[PL::F * P + e] = (uint8_t)fl;
+    }
+    if (stats != nullptr) {
+        const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
+                                       wave_sum(st.err)};
+        if ((threadIdx.x & 63u) == 0u) {
+            unsigned long long* row = (unsigned long long*)stats + (int64_t)(blockIdx.x % stat_rows) * OC_NSTATS;
+#pragma unroll
+            for (int c = 0; c < OC_NSTATS; ++c)
+                if (v[c]) atomicAdd(row + c, (unsigned long long)v[c]);
+        }
+    }
+}
+
+// reset() of a wide level: the template in every env of the pitch
+template <int A, int K>
+__global__ __launch_bounds__(kBlock) void oc_reset_wide_kernel(WideArgs R, uint8_t* __restrict__ s) {
+    using PL = Planes<A, K, true>;
+    const int64_t P = R.pitch, e = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    if (e >= P) return;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        s[a * P + e] = R.S.spawn_x[a];
+        s[(PL::Y + a) * P + e] = R.S.spawn_y[a];
+        s[(PL::H + a) * P + e] = (uint8_t)OC_HOLD_NONE;
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        s[(PL::L + j) * P + e] = (uint8_t)R.S.item_cell[j];
+        s[(PL::LH + j) * P + e] = (uint8_t)(R.S.item_cell[j] >> 8);
+        s[(PL::M + j) * P + e] = R.S.item_mask[j];
+    }
+    ((uint16_t*)(s + PL::T * P))[e] = 0;
+    s[PL::F * P + e] = 0;
 }
 
 // Image observation (oc_render, GameImage.get_image_obs: gym_cooking/misc/game/gameimage.py:31-51,
@@ -1153,6 +1271,12 @@ struct oc_handle {
     uint8_t* roll_blob = nullptr;  // device: the level's rollout table blob (oc_rollout.h)
     int32_t roll_blob_bytes = 0;
     uint8_t roll_blob_host[ocro::kBlobMax];  // the same blob on the host
+    // wide levels (more than 255 cells): the scalar step's tables
+    bool wide = false;
+    ocro::StepLevel step;
+    ocro::RollLevel step_lv;         // W, H, enc; tile_off 0 (the tile table alone)
+    uint8_t* wide_tiles = nullptr;   // device: tile class per cell (W * H rounded up to 4 bytes)
+    uint8_t wide_tiles_host[ocro::kMaxCellsWide];
 };
 
 // Statistics rows, shared by the blocks of every kernel modulo the row count; oc_step_n's
@@ -1236,6 +1360,60 @@ static void cpu_step_words(const oc_handle* h, const uint8_t* sin, uint8_t* sout
     st[OC_STAT_ERRORS] = err;
 }
 
+// oc_cpu_step on a wide level: envs [e0, e1) through the host pass of the scalar step
+template <int A, int K>
+static void cpu_step_wide(const oc_handle* h, const uint8_t* sin, uint8_t* sout, const uint8_t* act, uint8_t* exo,
+                          uint8_t* coll, int64_t P, int64_t e0, int64_t e1, uint64_t* st) {
+    using PL = Planes<A, K, true>;
+    using Row = ocro::RowT<K, true>;
+    uint64_t eps = 0, succ = 0, steps = 0, ncoll = 0, err = 0;
+    ocro::RowOps<A, K, true> ops(h->step_lv, h->wide_tiles_host);
+    for (int64_t e = e0; e < e1; ++e) {
+        Row r;
+        for (int a = 0; a < A; ++a) {
+            r.x |= (uint32_t)sin[a * P + e] << (8 * a);
+            r.y |= (uint32_t)sin[(PL::Y + a) * P + e] << (8 * a);
+            r.h |= (uint32_t)sin[(PL::H + a) * P + e] << (8 * a);
+        }
+        for (int j = 0; j < K; ++j) {
+            r.set_loc(j, (uint32_t)sin[(PL::L + j) * P + e] | ((uint32_t)sin[(PL::LH + j) * P + e] << 8));
+            r.set_mask(j, sin[(PL::M + j) * P + e]);
+        }
+        uint32_t t = (uint32_t)sin[PL::T * P + 2 * e] | ((uint32_t)sin[PL::T * P + 2 * e + 1] << 8);
+        const uint32_t fl = sin[PL::F * P + e];
+        uint32_t a4 = 0, ex, cm;
+        for (int a = 0; a < A; ++a) a4 |= (uint32_t)act[a * P + e] << (8 * a);
+        const uint32_t f = ops.env_step(r, t, fl, a4, h->step, ex, cm);
+        if ((f & 1u) && !(fl & 1u)) {
+            ++eps;
+            succ += (f >> 1) & 1u;
+            err += (f >> 2) & 1u;
+            steps += t;
+        }
+        ncoll += (uint64_t)__builtin_popcount(cm);
+        for (int a = 0; a < A; ++a) {
+            sout[a * P + e] = (uint8_t)r.ax(a);
+            sout[(PL::Y + a) * P + e] = (uint8_t)r.ay(a);
+            sout[(PL::H + a) * P + e] = (uint8_t)r.ah(a);
+            if (exo != nullptr) exo[a * P + e] = (uint8_t)(ex >> (8 * a));
+        }
+        for (int j = 0; j < K; ++j) {
+            sout[(PL::L + j) * P + e] = (uint8_t)r.il(j);
+            sout[(PL::LH + j) * P + e] = (uint8_t)(r.il(j) >> 8);
+            sout[(PL::M + j) * P + e] = (uint8_t)r.im(j);
+        }
+        sout[PL::T * P + 2 * e] = (uint8_t)t;
+        sout[PL::T * P + 2 * e + 1] = (uint8_t)(t >> 8);
+        sout[PL::F * P + e] = (uint8_t)f;
+        if (coll != nullptr) coll[e] = (uint8_t)cm;
+    }
+    st[OC_STAT_EPISODES] = eps;
+    st[OC_STAT_SUCCESSES] = succ;
+    st[OC_STAT_STEPS] = steps;
+    st[OC_STAT_COLLISIONS] = ncoll;
+    st[OC_STAT_ERRORS] = err;
+}
+
 extern "C" {
 
 int oc_abi_version(void) { return OC_ABI_VERSION; }
@@ -1245,13 +1423,14 @@ const char* oc_last_error(void) { return g_last_error.c_str(); }
 int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_t device, oc_handle** out) {
     if (lv == nullptr || out == nullptr) return fail(OC_EINVAL, "null argument");
     const int W = lv->width, H = lv->height;
-    if (W < 3 || H < 3 || W * H > OC_MAX_CELLS)
-        return fail(OC_ELEVEL, "grid %dx%d: width and height >= 3 and at most %d cells", W, H, OC_MAX_CELLS);
+    if (W < 3 || H < 3 || W > 255 || H > 255 || W * H > OC_MAX_CELLS)
+        return fail(OC_ELEVEL, "grid %dx%d: width and height 3..255 and at most %d cells", W, H, OC_MAX_CELLS);
     if (num_agents < 1 || num_agents > OC_MAX_AGENTS) return fail(OC_EINVAL, "num_agents %d", num_agents);
     if (lv->num_spawns < num_agents || lv->num_spawns > OC_MAX_AGENTS) return fail(OC_ELEVEL, "num_spawns %d", lv->num_spawns);
     if (lv->num_items < 0 || lv->num_items > OC_MAX_ITEMS) return fail(OC_ELEVEL, "num_items %d", lv->num_items);
     if (lv->num_goals < 1 || lv->num_goals > OC_MAX_GOALS) return fail(OC_ELEVEL, "num_goals %d", lv->num_goals);
     if (max_T < 0 || max_T > 65535) return fail(OC_EINVAL, "max_T %d", max_T);
+    const bool wide = W * H > ocro::kMaxCells;  // u16 cell ids: the scalar step (oc_step_wide_kernel)
     LevelArgs L{};
     L.W = W;
     L.H = H;
@@ -1259,7 +1438,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     for (int c = 0; c < W * H; ++c) {
         const int t = lv->tiles[c];
         if (t < OC_TILE_FLOOR || t > OC_TILE_DELIVERY) return fail(OC_ELEVEL, "tile %d at cell %d", t, c);
-        L.cls4[c >> 2] |= (uint32_t)ocsw::tile_class(t) << (8 * (c & 3));
+        if (!wide) L.cls4[c >> 2] |= (uint32_t)ocsw::tile_class(t) << (8 * (c & 3));
         if (t == OC_TILE_DELIVERY && L.done_cell < 0) L.done_cell = c;
     }
     if (L.done_cell < 0) return fail(OC_ELEVEL, "no Delivery tile");
@@ -1269,9 +1448,10 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     uint32_t seen_food = 0;
     int per_food[3] = {0, 0, 0};
     const int K = lv->num_items <= 4 ? 4 : (lv->num_items <= 8 ? 8 : 16);
-    uint8_t cell[16], mask[16];
+    uint16_t cell[16];
+    uint8_t mask[16], cell8[16];
     for (int j = 0; j < 16; ++j) {
-        cell[j] = OC_LOC_DEAD;
+        cell[j] = wide ? (uint16_t)OC_LOC_DEAD16 : (uint16_t)OC_LOC_DEAD;
         mask[j] = 0;
     }
     for (int j = 0; j < lv->num_items; ++j) {
@@ -1290,9 +1470,10 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
                 return fail(OC_ELEVEL, "food type present twice: the level needs OC_ENC_COUNTS");
             seen_food |= m & 7u;
         }
-        cell[j] = (uint8_t)c;
+        cell[j] = (uint16_t)c;
         mask[j] = (uint8_t)m;
     }
+    for (int j = 0; j < 16; ++j) cell8[j] = (uint8_t)cell[j];
     for (int a = 0; a < num_agents; ++a) {
         const int x = lv->spawn_x[a], y = lv->spawn_y[a];
         if (x >= W || y >= H || lv->tiles[y * W + x] != OC_TILE_FLOOR) return fail(OC_ELEVEL, "spawn %d not on Floor", a);
@@ -1300,7 +1481,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
         L.tmpl_y |= (uint32_t)y << (8 * a);
     }
     for (int j = 0; j < 16; ++j) {
-        L.tmpl_cell[j >> 2] |= (uint32_t)cell[j] << (8 * (j & 3));
+        L.tmpl_cell[j >> 2] |= (uint32_t)cell8[j] << (8 * (j & 3));
         L.tmpl_mask[j >> 2] |= (uint32_t)mask[j] << (8 * (j & 3));
     }
     for (int g = 0; g < lv->num_goals; ++g) L.goals |= (uint32_t)lv->goal_mask[g] << (8 * g);
@@ -1309,9 +1490,32 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     const int dcell[5] = {W, -W, -1, 1, 0};
     for (int c = 0; c < 5; ++c) L.dcell_lut |= (uint64_t)((dcell[c] + 128) & 0xFF) << (8 * c);
     if (max_T > 0x7FFF) return fail(OC_EINVAL, "max_T %d > 32767", max_T);
-    ocsw::build_swar_level(L.sw, W, H, L.done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y,
-                           num_agents, cell, mask, lv->encoding, lv->tiles);
+    if (!wide)
+        ocsw::build_swar_level(L.sw, W, H, L.done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x,
+                               lv->spawn_y, num_agents, cell8, mask, lv->encoding, lv->tiles);
     oc_handle* h = new oc_handle;
+    h->wide = wide;
+    h->step = ocro::StepLevel{};
+    h->step.done_cell = L.done_cell;
+    h->step.max_T = max_T;
+    h->step.ngoals = lv->num_goals;
+    for (int g = 0; g < lv->num_goals; ++g) h->step.goal[g] = lv->goal_mask[g];
+    for (int a = 0; a < num_agents; ++a) {
+        h->step.spawn_x[a] = lv->spawn_x[a];
+        h->step.spawn_y[a] = lv->spawn_y[a];
+    }
+    for (int j = 0; j < 16; ++j) {
+        h->step.item_cell[j] = cell[j];
+        h->step.item_mask[j] = mask[j];
+    }
+    h->step_lv = ocro::RollLevel{};
+    h->step_lv.W = W;
+    h->step_lv.H = H;
+    h->step_lv.perimeter = 2 * (W + H);
+    h->step_lv.enc = lv->encoding;
+    h->step_lv.wide = wide ? 1 : 0;
+    memset(h->wide_tiles_host, 0, sizeof h->wide_tiles_host);
+    for (int c = 0; c < W * H; ++c) h->wide_tiles_host[c] = lv->tiles[c];
     h->level = *lv;
     h->A = num_agents;
     h->K = K;
@@ -1333,7 +1537,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
         if (n < 0) {
             h->roll.nnodes = -1;
         } else {
-            h->roll_blob_bytes = ocro::blob_bytes(n);
+            h->roll_blob_bytes = h->roll.blob_bytes;
             if (hipSetDevice(device) != hipSuccess ||
                 hipMalloc(&h->roll_blob, (size_t)h->roll_blob_bytes) != hipSuccess ||
                 hipMemcpy(h->roll_blob, h->roll_blob_host, (size_t)h->roll_blob_bytes, hipMemcpyHostToDevice) !=
@@ -1341,6 +1545,14 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
                 h->roll_blob = nullptr;  // no device (e.g. a CPU-only build check): rollout unavailable
                 (void)hipGetLastError();
             }
+        }
+    }
+    if (wide) {
+        const size_t tb = (size_t)((W * H + 3) & ~3);
+        if (hipSetDevice(device) != hipSuccess || hipMalloc(&h->wide_tiles, tb) != hipSuccess ||
+            hipMemcpy(h->wide_tiles, h->wide_tiles_host, tb, hipMemcpyHostToDevice) != hipSuccess) {
+            h->wide_tiles = nullptr;  // no device: oc_cpu_step only
+            (void)hipGetLastError();
         }
     }
     *out = h;
@@ -1356,17 +1568,18 @@ int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, i
     *num_nodes = n;
     if (node_of != nullptr) {
         if (node_of_len < (int64_t)cells * 5) return fail(OC_EINVAL, "node_of needs %d entries", cells * 5);
-        memcpy(node_of, h->roll_blob_host + ocro::kNodeOff, (size_t)cells * 5 * sizeof(uint16_t));
+        memcpy(node_of, h->roll_blob_host + h->roll.node_off, (size_t)cells * 5 * sizeof(uint16_t));
     }
     if (dist != nullptr) {
         if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %d bytes", n * n);
-        for (int i = 0; i < n * n; ++i) dist[i] = h->roll_blob_host[ocro::kDistOff + i];
+        for (int i = 0; i < n * n; ++i) dist[i] = h->roll_blob_host[h->roll.dist_off + i];
     }
     return OC_OK;
 }
 
 int oc_destroy(oc_handle* h) {
     if (h != nullptr && h->roll_blob != nullptr) (void)hipFree(h->roll_blob);
+    if (h != nullptr && h->wide_tiles != nullptr) (void)hipFree(h->wide_tiles);
     delete h;
     return OC_OK;
 }
@@ -1380,11 +1593,14 @@ int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
     out->plane_agent_x = 0;
     out->plane_agent_y = A;
     out->plane_agent_hold = 2 * A;
+    const int LK = h->wide ? 2 * K : K;  // item cell planes: low bytes, then (wide) high bytes
     out->plane_item_loc = 3 * A;
-    out->plane_item_mask = 3 * A + K;
-    out->plane_t = 3 * A + 2 * K;
-    out->plane_flags = 3 * A + 2 * K + 2;
-    out->num_planes = 3 * A + 2 * K + 3;
+    out->plane_item_loc_hi = h->wide ? 3 * A + K : -1;
+    out->cell_bytes = h->wide ? 2 : 1;
+    out->plane_item_mask = 3 * A + LK;
+    out->plane_t = 3 * A + LK + K;
+    out->plane_flags = 3 * A + LK + K + 2;
+    out->num_planes = 3 * A + LK + K + 3;
     out->state_bytes = out->num_planes * out->pitch;
     return OC_OK;
 }
@@ -1404,6 +1620,42 @@ int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
         case 316: LAUNCH(3, 16); break;                                                     \
         case 416: LAUNCH(4, 16); break;                                                     \
         default: return fail(OC_EINVAL, "unsupported (A,K)=(%d,%d)", (A_), (K_));           \
+    }
+
+// The planner kernels: narrow (byte cell ids) or wide (u16) rows.
+#define OC_DISPATCH_W(h_, LAUNCH)                                                           \
+    if ((h_)->wide) {                                                                       \
+        switch ((h_)->A * ((h_)->K >= 10 ? 100 : 10) + (h_)->K) {                           \
+            case 14: LAUNCH(1, 4, true); break;                                             \
+            case 24: LAUNCH(2, 4, true); break;                                             \
+            case 34: LAUNCH(3, 4, true); break;                                             \
+            case 44: LAUNCH(4, 4, true); break;                                             \
+            case 18: LAUNCH(1, 8, true); break;                                             \
+            case 28: LAUNCH(2, 8, true); break;                                             \
+            case 38: LAUNCH(3, 8, true); break;                                             \
+            case 48: LAUNCH(4, 8, true); break;                                             \
+            case 116: LAUNCH(1, 16, true); break;                                           \
+            case 216: LAUNCH(2, 16, true); break;                                           \
+            case 316: LAUNCH(3, 16, true); break;                                           \
+            case 416: LAUNCH(4, 16, true); break;                                           \
+            default: return fail(OC_EINVAL, "unsupported (A,K)=(%d,%d)", (h_)->A, (h_)->K); \
+        }                                                                                   \
+    } else {                                                                                \
+        switch ((h_)->A * ((h_)->K >= 10 ? 100 : 10) + (h_)->K) {                           \
+            case 14: LAUNCH(1, 4, false); break;                                            \
+            case 24: LAUNCH(2, 4, false); break;                                            \
+            case 34: LAUNCH(3, 4, false); break;                                            \
+            case 44: LAUNCH(4, 4, false); break;                                            \
+            case 18: LAUNCH(1, 8, false); break;                                            \
+            case 28: LAUNCH(2, 8, false); break;                                            \
+            case 38: LAUNCH(3, 8, false); break;                                            \
+            case 48: LAUNCH(4, 8, false); break;                                            \
+            case 116: LAUNCH(1, 16, false); break;                                          \
+            case 216: LAUNCH(2, 16, false); break;                                          \
+            case 316: LAUNCH(3, 16, false); break;                                          \
+            case 416: LAUNCH(4, 16, false); break;                                          \
+            default: return fail(OC_EINVAL, "unsupported (A,K)=(%d,%d)", (h_)->A, (h_)->K); \
+        }                                                                                   \
     }
 
 // The step kernels: 4-slot levels of the common class (H <= 8, W*H <= 128, presence masks:
@@ -1436,9 +1688,45 @@ int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
         }                                                                                   \
     }
 
+// Wide levels: n steps of the scalar kernel (oc_step: n = 1), statistics folded by
+// oc_stats_reduce when totals are asked for.
+static int step_wide(const oc_handle* h, const void* sin, void* sout, const uint8_t* act, void* traj, uint8_t* ex,
+                     uint8_t* coll, uint64_t* stats, uint64_t* totals, int64_t B, int32_t n, void* stream) {
+    if (h->wide_tiles == nullptr) return fail(OC_EHIP, "level tables not on the device");
+    WideArgs R;
+    R.L = h->step_lv;
+    R.S = h->step;
+    R.tile_words = (h->level.width * h->level.height + 3) / 4;
+    R.pitch = pitch_for(B);
+    R.B = B;
+    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
+    const dim3 grid((unsigned)(need < cap ? need : cap));
+    const uint32_t rows = (uint32_t)stats_rows(h, B);
+    hipStream_t st = (hipStream_t)stream;
+#define OC_LAUNCH_WSTEP(A, K)                                                                                  \
+    hipLaunchKernelGGL((oc_step_wide_kernel<A, K>), grid, dim3(kBlock), 0, st, R, h->wide_tiles,                 \
+                       (const uint8_t*)sin, (uint8_t*)sout, act, (uint8_t*)traj, ex, coll, stats, rows, n)
+    OC_DISPATCH(h->A, h->K, OC_LAUNCH_WSTEP)
+    if (const int rc = hip_check("oc_step (wide) launch")) return rc;
+    return totals != nullptr ? oc_stats_reduce(h, stats, B, totals, stream) : OC_OK;
+}
+
 int oc_reset(const oc_handle* h, void* state, int64_t B, void* stream) {
     if (h == nullptr || state == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
     if (B == 0) return OC_OK;
+    if (h->wide) {
+        WideArgs R;
+        R.L = h->step_lv;
+        R.S = h->step;
+        R.tile_words = 0;
+        R.pitch = pitch_for(B);
+        R.B = B;
+        const dim3 grid((unsigned)(R.pitch / kBlock));
+        hipStream_t st = (hipStream_t)stream;
+#define OC_LAUNCH_WRESET(A, K) hipLaunchKernelGGL((oc_reset_wide_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (uint8_t*)state)
+        OC_DISPATCH(h->A, h->K, OC_LAUNCH_WRESET)
+        return hip_check("oc_reset (wide) launch");
+    }
     LevelArgs L = h->args;
     L.pitch = pitch_for(B);
     L.B = B;
@@ -1457,6 +1745,7 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
     if (((uintptr_t)state_in | (uintptr_t)state_out | (uintptr_t)actions | (uintptr_t)exec_actions |
          (uintptr_t)coll_mask) & 15u)
         return fail(OC_EINVAL, "buffers must be 16-byte aligned");
+    if (h->wide) return step_wide(h, state_in, state_out, actions, nullptr, exec_actions, coll_mask, stats, nullptr, B, 1, stream);
     LevelArgs L = h->args;
     L.pitch = pitch_for(B);
     L.B = B;
@@ -1488,6 +1777,13 @@ int oc_cpu_step(const oc_handle* h, const void* state_in, void* state_out, const
         const uint8_t* si = (const uint8_t*)state_in;
         uint8_t* so = (uint8_t*)state_out;
         uint64_t* st = part.data() + i * OC_NSTATS;
+        if (h->wide) {  // one env at a time; the ranges are in words of 4 envs
+            const int64_t e0 = 4 * g0, e1 = 4 * g1 < B ? 4 * g1 : B;
+#define OC_CPU_WSTEP(A, K) cpu_step_wide<A, K>(h, si, so, actions, exec_actions, coll_mask, P, e0, e1, st)
+            OC_DISPATCH(h->A, h->K, OC_CPU_WSTEP)
+#undef OC_CPU_WSTEP
+            return OC_OK;
+        }
 #define OC_CPU_STEP(A, K, MODE) cpu_step_words<A, K, MODE>(h, si, so, actions, exec_actions, coll_mask, B, P, g0, g1, st)
         OC_DISPATCH_STEP(h, OC_CPU_STEP)
 #undef OC_CPU_STEP
@@ -1523,7 +1819,7 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
     LevelArgs L = h->args;
     L.pitch = pitch_for(B);
     L.B = B;
-    const int64_t NP = 3 * h->A + 2 * h->K + 3;
+    const int64_t NP = 3 * h->A + (h->wide ? 3 : 2) * h->K + 3;
     // state_out may be the trajectory's last state (written once); nothing else may overlap it
     const uint8_t* last_slot = traj ? (const uint8_t*)traj + (int64_t)(n - 1) * NP * L.pitch : nullptr;
     const bool out_is_last = traj != nullptr && (const uint8_t*)state_out == last_slot;
@@ -1536,6 +1832,7 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
         if (overlaps(state_in) || (overlaps(state_out) && !out_is_last))
             return fail(OC_EINVAL, "traj must not overlap the state (state_out may be its last state)");
     }
+    if (h->wide) return step_wide(h, state_in, state_out, actions, traj, exec_actions, coll_mask, stats, totals, B, n, stream);
     if (NP * L.pitch >= (1ll << 31)) return fail(OC_EINVAL, "batch too large for one launch (state must be < 2 GiB)");
     // steps per launch so every per-launch buffer (trajectory, actions) stays < 2 GiB of offsets
     int64_t per = ((1ll << 31) - 1) / (NP * L.pitch);
@@ -1641,12 +1938,12 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
-#define OC_LAUNCH_ROLL(A, K)                                                                                 \
-    if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K>, h->roll_blob_bytes)) return rc;                 \
-    hipLaunchKernelGGL((oc_rollout_kernel<A, K>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,                \
+#define OC_LAUNCH_ROLL(A, K, W)                                                                              \
+    if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W>, h->roll_blob_bytes)) return rc;    \
+    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,             \
                        (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags,    \
                        lower_bound)
-    OC_DISPATCH(h->A, h->K, OC_LAUNCH_ROLL)
+    OC_DISPATCH_W(h, OC_LAUNCH_ROLL)
     return hip_check("oc_rollout launch");
 }
 
@@ -1669,20 +1966,20 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     const int64_t need = (B * G + kBlock - 1) / kBlock, cap = (int64_t)h->cus * (any_joint ? 16 : 8);
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
-#define OC_LAUNCH_LIK(A, K)                                                                                          \
-    if (const int rc = allow_dyn_lds(any_joint ? (const void*)oc_likelihood_kernel<A, K, 32>                          \
-                                               : (const void*)oc_likelihood_kernel<A, K, 8>,                    \
+#define OC_LAUNCH_LIK(A, K, W)                                                                                       \
+    if (const int rc = allow_dyn_lds(any_joint ? (const void*)oc_likelihood_kernel<A, K, 32, W>                       \
+                                               : (const void*)oc_likelihood_kernel<A, K, 8, W>,                 \
                                      h->roll_blob_bytes))                                                            \
         return rc;                                                                                                   \
     if (any_joint)                                                                                                   \
-        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 32>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,          \
+        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 32, W>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,       \
                            (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,   \
                            likelihood, out_flags);                                                                   \
     else                                                                                                             \
-        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 8>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,           \
+        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 8, W>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,        \
                            (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,   \
                            likelihood, out_flags)
-    OC_DISPATCH(h->A, h->K, OC_LAUNCH_LIK)
+    OC_DISPATCH_W(h, OC_LAUNCH_LIK)
     return hip_check("oc_nav_likelihood launch");
 }
 
@@ -1706,11 +2003,11 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
     if (chunks < 1) chunks = 1;
     const dim3 grid((unsigned)bx, (unsigned)chunks);
     hipStream_t st = (hipStream_t)stream;
-#define OC_LAUNCH_BOUNDS(A, K)                                                                             \
-    if (const int rc = allow_dyn_lds((const void*)oc_bounds_kernel<A, K>, h->roll_blob_bytes)) return rc;                 \
-    hipLaunchKernelGGL((oc_bounds_kernel<A, K>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,            \
+#define OC_LAUNCH_BOUNDS(A, K, W)                                                                         \
+    if (const int rc = allow_dyn_lds((const void*)oc_bounds_kernel<A, K, W>, h->roll_blob_bytes)) return rc;  \
+    hipLaunchKernelGGL((oc_bounds_kernel<A, K, W>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,           \
                        (const uint8_t*)state, h->roll_blob, lower_bound, doable)
-    OC_DISPATCH(h->A, h->K, OC_LAUNCH_BOUNDS)
+    OC_DISPATCH_W(h, OC_LAUNCH_BOUNDS)
     return hip_check("oc_subtask_bounds launch");
 }
 
@@ -1727,6 +2024,7 @@ int oc_render_ordered(const oc_handle* h, const void* state, const uint8_t* draw
         return fail(OC_EINVAL, "bad argument");
     const int W = h->level.width, H = h->level.height;
     if (W > kRenderMaxW) return fail(OC_ELEVEL, "render: width %d > %d", W, kRenderMaxW);
+    if (h->wide) return fail(OC_ELEVEL, "render: levels of more than %d cells are not rendered", OC_MAX_NARROW_CELLS);
     if (desc->tile < kRenderPx || desc->tile % kRenderPx != 0 || desc->tile > 1024)
         return fail(OC_EINVAL, "render: tile %d (a multiple of %d)", desc->tile, kRenderPx);
     for (int c = 0; c < OC_RENDER_SIZES; ++c)
@@ -1780,7 +2078,7 @@ int oc_state_checksum(const oc_handle* h, const void* state, int64_t B, uint64_t
     if (hipMemsetAsync(out, 0, sizeof(uint64_t), s) != hipSuccess) return hip_check("oc_state_checksum memset");
     if (B == 0) return OC_OK;
     const int64_t P = pitch_for(B);
-    const int np = 3 * h->A + 2 * h->K + 3;
+    const int np = 3 * h->A + (h->wide ? 3 : 2) * h->K + 3;
     const dim3 grid((unsigned)(P / kEnvsPerBlock));
 #define OC_CK(NP) hipLaunchKernelGGL((oc_checksum_kernel<NP>), grid, dim3(kBlock), 0, s, (const uint8_t*)state, P, B, (unsigned long long*)out)
     switch (np) {
@@ -1792,6 +2090,22 @@ int oc_state_checksum(const oc_handle* h, const void* state, int64_t B, uint64_t
         case 25: OC_CK(25); break;   // A=2 K=8
         case 28: OC_CK(28); break;   // A=3 K=8
         case 31: OC_CK(31); break;   // A=4 K=8
+        case 38: OC_CK(38); break;   // A=1 K=16
+        case 41: OC_CK(41); break;   // A=2 K=16
+        case 44: OC_CK(44); break;   // A=3 K=16
+        case 47: OC_CK(47); break;   // A=4 K=16
+        case 18: OC_CK(18); break;   // wide: A=1 K=4
+        case 21: OC_CK(21); break;   // wide: A=2 K=4
+        case 24: OC_CK(24); break;   // wide: A=3 K=4
+        case 27: OC_CK(27); break;   // wide: A=4 K=4
+        case 30: OC_CK(30); break;   // wide: A=1 K=8
+        case 33: OC_CK(33); break;   // wide: A=2 K=8
+        case 36: OC_CK(36); break;   // wide: A=3 K=8
+        case 39: OC_CK(39); break;   // wide: A=4 K=8
+        case 54: OC_CK(54); break;   // wide: A=1 K=16
+        case 57: OC_CK(57); break;   // wide: A=2 K=16
+        case 60: OC_CK(60); break;   // wide: A=3 K=16
+        case 63: OC_CK(63); break;   // wide: A=4 K=16
         default: return fail(OC_EINVAL, "unsupported plane count %d", np);
     }
     return hip_check("oc_state_checksum launch");

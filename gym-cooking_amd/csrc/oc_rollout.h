@@ -28,7 +28,17 @@
 
 namespace ocro {
 
-constexpr int kMaxCells = 255;  // cell ids are bytes, 0xFF = dead / none
+template <bool B, class T, class F>
+struct ConditionalT {
+    using type = T;
+};
+template <class T, class F>
+struct ConditionalT<false, T, F> {
+    using type = F;
+};
+
+constexpr int kMaxCells = 255;      // narrow levels: cell ids are bytes, 0xFF = dead / none
+constexpr int kMaxCellsWide = 1024;  // wide levels (more than 255 cells): u16 cell ids, 0xFFFF dead
 // compact reachability-graph node ids are u16 (kNoNode = none); at most kMaxNodes nodes keep a
 // block's LDS (blob + 64 configurations + the kernels' own) within the 160 KB of a gfx950 CU;
 // distances are bytes (0xFF = no path), so a graph whose BFS distances reach 255 is refused too
@@ -39,23 +49,39 @@ constexpr int kFloor = 0, kCounter = 1, kCutboard = 2, kDelivery = 3;  // OC_TIL
 constexpr int kNoop = 4;
 constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NAV_ACTIONS + (0, 0)
 
-// Static level tables, one byte blob: tile class per cell, node id per (cell, approach),
-// Cutboard and Delivery cells in scan order, then the nnodes x nnodes distance table.
-constexpr int kTileOff = 0;                        // [256] tile class (cells >= W*H: Counter)
-constexpr int kNodeOff = 256;                      // u16 [256 * 5] cell * 5 + approach (4 = (0, 0))
-constexpr int kCutOff = kNodeOff + 2 * 256 * 5;    // [256] Cutboard cells, L.ncut of them
-constexpr int kDelivOff = kCutOff + 256;           // [256] Delivery cells, L.ndeliv of them
-constexpr int kDistOff = kDelivOff + 256;          // [nnodes][nnodes] BFS distances
-// after the distances, at dmin_off: [2][nnodes] the distance from a node to the nearest
-// Cutboard (row 0) / Delivery (row 1) approach node, 0xFF = none reachable
-constexpr int kBlobMax = kDistOff + kMaxNodes * kMaxNodes + 2 * kMaxNodes;
-OC_RH int blob_bytes(int nnodes) { return (kDistOff + nnodes * nnodes + 2 * nnodes + 3) & ~3; }
+// Static level tables, one byte blob (offsets in RollLevel, set by build_roll_level):
+//   tile_off   [C] tile class per cell (C = 256 for a narrow level: cells >= W*H read Counter;
+//              the cell count rounded up to 4 for a wide one)
+//   node_off   u16 [C * 5] graph node of (cell, approach), approach 4 = (0, 0)
+//   cut_off    Cutboard cells in scan order (L.ncut; u8 narrow, u16 wide)
+//   deliv_off  Delivery cells in scan order (L.ndeliv; u8 narrow, u16 wide)
+//   dist_off   [nnodes][nnodes] BFS distances
+//   dmin_off   [2][nnodes] the distance from a node to the nearest Cutboard (row 0) / Delivery
+//              (row 1) approach node, 0xFF = none reachable
+// A narrow level's offsets are fixed: 0, 256, 2816, 3072, 3328.
+constexpr int kNarrowDistOff = 256 + 2 * 256 * 5 + 256 + 256;
+constexpr int kWideTablesMax = kMaxCellsWide * (1 + 10 + 2 + 2);
+constexpr int kBlobMax = kWideTablesMax + kMaxNodes * kMaxNodes + 2 * kMaxNodes + 4;
 
 struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t W, H, perimeter, nnodes;
     int32_t ncut, ndeliv;
     int32_t enc;       // item mask encoding (OC_ENC_*)
     int32_t dmin_off;  // blob offset of the nearest-Cutboard / nearest-Delivery distance rows
+    int32_t tile_off, node_off, cut_off, deliv_off, dist_off;
+    int32_t wide;      // u16 cell ids (W * H > 255)
+    int32_t blob_bytes;  // the blob's size (a multiple of 4)
+};
+
+// The environment step's level constants (the scalar step of wide levels, RowOps::env_step).
+struct StepLevel {
+    int32_t done_cell;  // first Delivery in scan order (done() reads only it, overcooked_environment.py:349)
+    int32_t max_T;      // 0 = no limit
+    int32_t ngoals;
+    uint8_t goal[4];    // Deliver goal masks
+    uint8_t spawn_x[4], spawn_y[4];
+    uint16_t item_cell[16];  // the template's item slots (dead past the level's items)
+    uint8_t item_mask[16];
 };
 
 struct Sub {  // oc_subtask, device copy
@@ -64,47 +90,52 @@ struct Sub {  // oc_subtask, device copy
 };
 
 // One row's state, packed so that run-time slot / agent indices are shifts, not memory:
-// agent a in byte a of x, y, h (h = held slot or kNone); slot j in byte j % 8 of word j / 8 of
-// loc, mask (one word for K <= 8, two for K = 16; a run-time j picks the word with a select).
-template <int K>
+// agent a in byte a of x, y, h (h = held slot or kNone); slot j's mask in byte j % 8 of word
+// j / 8 of mask, its cell in byte j % 8 of word j / 8 of loc (narrow) or in the 16-bit field
+// j % 4 of word j / 4 (WIDE); a run-time j picks the word with selects on register values.
+template <int K, bool WIDE = false>
 struct RowT {
-    static constexpr int NW = (K + 7) / 8;
+    static constexpr int NW = (K + 7) / 8;          // mask words
+    static constexpr int LPW = WIDE ? 4 : 8;        // cells per location word
+    static constexpr int NL = (K + LPW - 1) / LPW;  // location words
+    static constexpr int kLocBits = WIDE ? 16 : 8;
+    static constexpr uint32_t kDead = WIDE ? 0xFFFFu : 0xFFu;  // OC_LOC_DEAD
     uint32_t x = 0, y = 0, h = 0;
-    uint64_t loc[NW] = {}, mask[NW] = {};
+    uint64_t loc[NL] = {}, mask[NW] = {};
     static OC_RH uint32_t b32(uint32_t w, int i) { return (w >> (8 * i)) & 0xFFu; }
-    static OC_RH uint32_t b64(uint64_t w, int i) { return (uint32_t)(w >> (8 * i)) & 0xFFu; }
     static OC_RH void s32(uint32_t& w, int i, uint32_t v) { w = (w & ~(0xFFu << (8 * i))) | (v << (8 * i)); }
-    static OC_RH void s64(uint64_t& w, int i, uint32_t v) {
-        w = (w & ~(0xFFull << (8 * i))) | ((uint64_t)v << (8 * i));
-    }
-    static OC_RH uint64_t word(const uint64_t (&w)[NW], int j) {
-        if constexpr (NW == 1) {
+    // word i of w[N], selected on register values: folded into a select of addresses the
+    // compiler turns the words into a scratch array with a run-time offset
+    template <int N>
+    static OC_RH uint64_t wsel(const uint64_t (&w)[N], int i) {
+        if constexpr (N == 1) {
             return w[0];
         } else {
-            uint64_t w0 = w[0], w1 = w[1];
+            uint64_t r = w[0];
+#pragma unroll
+            for (int q = 1; q < N; ++q) {
+                uint64_t v = w[q];
 #if defined(__HIP_DEVICE_COMPILE__)
-            // keep the select on register values: folded into a select of addresses it turns
-            // the two words into a scratch array with a run-time offset
-            asm("" : "+v"(w0), "+v"(w1));
+                asm("" : "+v"(r), "+v"(v));
 #endif
-            return j < 8 ? w0 : w1;
+                r = i == q ? v : r;
+            }
+            return r;
         }
     }
-    static OC_RH void set(uint64_t (&w)[NW], int j, uint32_t v) {
-        if constexpr (NW == 1) {
-            s64(w[0], j, v);
-        } else {
-            if (j < 8) s64(w[0], j, v);
-            else s64(w[1], j - 8, v);
-        }
+    template <int N>
+    static OC_RH void wput(uint64_t (&w)[N], int i, int shift, uint64_t field, uint64_t v) {
+#pragma unroll
+        for (int q = 0; q < N; ++q)
+            if (i == q) w[q] = (w[q] & ~(field << shift)) | (v << shift);
     }
     OC_RH int ax(int a) const { return (int)b32(x, a); }
     OC_RH int ay(int a) const { return (int)b32(y, a); }
     OC_RH int ah(int a) const { return (int)b32(h, a); }
-    OC_RH int il(int j) const { return (int)b64(word(loc, j), j & 7); }
-    OC_RH int im(int j) const { return (int)b64(word(mask, j), j & 7); }
-    OC_RH void set_loc(int j, uint32_t v) { set(loc, j, v); }
-    OC_RH void set_mask(int j, uint32_t v) { set(mask, j, v); }
+    OC_RH int il(int j) const { return (int)((wsel(loc, j / LPW) >> (kLocBits * (j % LPW))) & kDead); }
+    OC_RH int im(int j) const { return (int)((wsel(mask, j >> 3) >> (8 * (j & 7))) & 0xFFu); }
+    OC_RH void set_loc(int j, uint32_t v) { wput(loc, j / LPW, kLocBits * (j % LPW), (uint64_t)kDead, (uint64_t)v); }
+    OC_RH void set_mask(int j, uint32_t v) { wput(mask, j >> 3, 8 * (j & 7), 0xFFull, (uint64_t)v); }
 };
 
 // Some lane of the wave (the active ones) has p: a wave-uniform trip count for the bound walks
@@ -123,29 +154,49 @@ OC_RH bool has_byte(uint32_t w, uint32_t v) {
     return ((x - 0x01010101u) & ~x & 0x80808080u) != 0u;
 }
 
-// ---- host: level tables --------------------------------------------------------------------
+// byte / u16 v occurs in one of the fields of w (the AgentCounter cells of a Level-0 view)
+OC_RH bool has_u16(uint64_t w, uint32_t v) {
+    const uint64_t x = w ^ ((uint64_t)v * 0x0001000100010001ull);
+    return ((x - 0x0001000100010001ull) & ~x & 0x8000800080008000ull) != 0ull;
+}
+
+// ---- host: level tables ----------------------------------------------------------------------
 // Builds the reachability graph of make_reachability_graph (world.py:67-108) and its BFS
 // distances into `blob` (kBlobMax bytes).  Returns the node count, or -1 when the level has
-// more than kMaxCells cells, the graph more than kMaxNodes nodes, or a BFS distance past 254.
+// more cells than its layout takes (255 narrow, kMaxCellsWide wide), the graph more than
+// kMaxNodes nodes, or a BFS distance past 254.
 inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uint8_t* tiles, int enc) {
     L.W = W;
     L.enc = enc;
     L.H = H;
     L.perimeter = 2 * (W + H);
     L.ncut = L.ndeliv = 0;
-    if (W * H > kMaxCells) return -1;
-    uint8_t* tile = blob + kTileOff;
-    uint16_t* node = (uint16_t*)(blob + kNodeOff);
-    for (int c = 0; c < 256; ++c) {
-        tile[c] = c < W * H ? tiles[c] : (uint8_t)kCounter;
-        if (c < W * H && tiles[c] == kCutboard) blob[kCutOff + L.ncut++] = (uint8_t)c;
-        if (c < W * H && tiles[c] == kDelivery) blob[kDelivOff + L.ndeliv++] = (uint8_t)c;
+    L.nnodes = -1;
+    const int cells = W * H;
+    L.wide = cells > kMaxCells ? 1 : 0;
+    if (cells > kMaxCellsWide) return -1;
+    const int C = L.wide ? (cells + 3) & ~3 : 256, lb = L.wide ? 2 : 1;  // table cells, list entry bytes
+    L.tile_off = 0;
+    L.node_off = C;
+    L.cut_off = L.node_off + 2 * C * 5;
+    L.deliv_off = L.cut_off + lb * C;
+    L.dist_off = L.deliv_off + lb * C;
+    uint8_t* tile = blob + L.tile_off;
+    uint16_t* node = (uint16_t*)(blob + L.node_off);
+    auto put_list = [&](int off, int i, int c) {
+        if (L.wide) ((uint16_t*)(blob + off))[i] = (uint16_t)c;
+        else blob[off + i] = (uint8_t)c;
+    };
+    for (int c = 0; c < C; ++c) {
+        tile[c] = c < cells ? tiles[c] : (uint8_t)kCounter;
+        if (c < cells && tiles[c] == kCutboard) put_list(L.cut_off, L.ncut++, c);
+        if (c < cells && tiles[c] == kDelivery) put_list(L.deliv_off, L.ndeliv++, c);
     }
-    for (int i = 0; i < 256 * 5; ++i) node[i] = kNoNode;
+    for (int i = 0; i < C * 5; ++i) node[i] = kNoNode;
     int n = 0;
     auto clampx = [&](int v) { return v < 0 ? 0 : (v > W - 1 ? W - 1 : v); };
     auto clampy = [&](int v) { return v < 0 ? 0 : (v > H - 1 ? H - 1 : v); };
-    for (int c = 0; c < W * H; ++c) {
+    for (int c = 0; c < cells; ++c) {
         const int x = c % W, y = c / W;
         const bool coll = tiles[c] != kFloor;
         if (!coll) {
@@ -160,7 +211,6 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
             }
         }
     }
-    L.nnodes = n;
     // adjacency (undirected): floor-floor, and a collidable square's approach node with the
     // floor it is approached from
     static const int opp[4] = {1, 0, 3, 2};
@@ -173,7 +223,7 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
         adj[u][deg[u]++] = (uint16_t)v;
         adj[v][deg[v]++] = (uint16_t)u;
     };
-    for (int c = 0; c < W * H; ++c) {
+    for (int c = 0; c < cells; ++c) {
         const int x = c % W, y = c / W;
         const bool coll = tiles[c] != kFloor;
         for (int d = 0; d < 4; ++d) {
@@ -184,7 +234,7 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
             else if (!coll && !ncoll) link(node[c * 5 + 4], node[nc * 5 + 4]);
         }
     }
-    uint8_t* dist = blob + kDistOff;
+    uint8_t* dist = blob + L.dist_off;
     for (int s = 0; s < n; ++s) {
         uint8_t* row = dist + s * n;
         for (int t = 0; t < n; ++t) row[t] = kNone;
@@ -206,40 +256,60 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
     // Chop and Deliver have a static B side (every Cutboard / every Delivery square, from any
     // side it is approached from): the single-agent bound's min over B of dist(A node, B node)
     // is this per-node table (world.py:175-189 evaluated once per level)
-    L.dmin_off = kDistOff + n * n;
+    L.dmin_off = L.dist_off + n * n;
     for (int side = 0; side < 2; ++side) {
-        const uint8_t* cells = blob + (side == 0 ? kCutOff : kDelivOff);
+        const int off = side == 0 ? L.cut_off : L.deliv_off;
         const int nc = side == 0 ? L.ncut : L.ndeliv;
         uint8_t* dm = blob + L.dmin_off + side * n;
         for (int v = 0; v < n; ++v) {
             int best = kNone;
-            for (int i = 0; i < nc; ++i)
+            for (int i = 0; i < nc; ++i) {
+                const int cell = L.wide ? ((const uint16_t*)(blob + off))[i] : blob[off + i];
                 for (int d = 0; d < 4; ++d) {
-                    const int b = node[cells[i] * 5 + d];
+                    const int b = node[cell * 5 + d];
                     if (b == kNoNode) continue;
                     const int dd = dist[v * n + b];
                     if (dd != kNone && dd < best) best = dd;
                 }
+            }
             dm[v] = (uint8_t)best;
         }
     }
+    L.nnodes = n;
+    L.blob_bytes = (L.dmin_off + 2 * n + 3) & ~3;
     return n;
 }
 
 // ---- row logic ----------------------------------------------------------------------------
-template <int A, int K>
+template <int A, int K, bool WIDE = false>
 struct RowOps {
-    using Row = RowT<K>;
+    using Row = RowT<K, WIDE>;
+    using AcT = typename ConditionalT<WIDE, uint64_t, uint32_t>::type;
+    static constexpr int kDead = (int)Row::kDead;
+    static constexpr AcT kNoAc = ~(AcT)0;
     const RollLevel& L;
     const uint8_t* T;       // the level's table blob (LDS on the device)
-    uint32_t ac = 0xFFFFFFFFu;  // AgentCounter cells of this row's Level-0 view, one per byte (0xFF none)
+    AcT ac = kNoAc;         // AgentCounter cells of this row's Level-0 view, one per byte (narrow) or
+                            // u16 field (wide), all ones = none
     uint32_t active = 0;    // bit a: agent a is a subtask agent
     uint32_t blockers = 0;  // bit a: agent a's cell may not be moved into (get_single_actions)
 
     OC_RH RowOps(const RollLevel& l, const uint8_t* blob) : L(l), T(blob) {}
 
-    OC_RH int static_tile(int cell) const { return T[kTileOff + cell]; }
-    OC_RH int tile(int cell) const { return has_byte(ac, (uint32_t)cell) ? kCounter : T[kTileOff + cell]; }
+    OC_RH int static_tile(int cell) const { return T[L.tile_off + cell]; }
+    OC_RH bool is_ac(int cell) const {
+        if constexpr (WIDE) return has_u16(ac, (uint32_t)cell);
+        else return has_byte(ac, (uint32_t)cell);
+    }
+    OC_RH void set_ac(int a, uint32_t cell) {
+        if constexpr (WIDE) ac = (ac & ~(0xFFFFull << (16 * a))) | ((uint64_t)cell << (16 * a));
+        else Row::s32(ac, a, cell);
+    }
+    OC_RH int tile(int cell) const { return is_ac(cell) ? kCounter : T[L.tile_off + cell]; }
+    OC_RH int list_cell(int off, int i) const {  // Cutboard / Delivery list entry
+        if constexpr (WIDE) return ((const uint16_t*)(T + off))[i];
+        else return T[off + i];
+    }
     OC_RH int cell(int x, int y) const { return y * L.W + x; }
     OC_RH int agent_cell(const Row& r, int a) const { return cell(r.ax(a), r.ay(a)); }
 
@@ -260,13 +330,13 @@ struct RowOps {
             if ((active >> a) & 1u) continue;
             const int hh = r.ah(a);
             if (hh != kNone) {
-                r.set_loc(hh, kNone);
+                r.set_loc(hh, (uint32_t)kDead);
                 r.set_mask(hh, 0);
                 Row::s32(r.h, a, kNone);
             }
             const uint32_t c = (uint32_t)agent_cell(r, a);
-            raised |= has_byte(ac, c);
-            Row::s32(ac, a, c);
+            raised |= is_ac((int)c);
+            set_ac(a, c);
         }
         return raised;
     }
@@ -322,7 +392,7 @@ struct RowOps {
                 if (o >= 0) {
                     if (mergeable(hm, r.im(o))) {  // the holder's item absorbs o
                         r.set_mask(h, (uint32_t)merged(hm, r.im(o)));
-                        r.set_loc(o, kNone);
+                        r.set_loc(o, (uint32_t)kDead);
                         r.set_mask(o, 0);
                     }
                 } else if (t == kCutboard && needs_chopped(hm)) {
@@ -381,7 +451,7 @@ struct RowOps {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const int c = r.il(j);
-            if (c == kNone || r.im(j) != s.goal) continue;
+            if (c == kDead || r.im(j) != s.goal) continue;
             if (s.kind == 3) {  // un-held goal items on a Delivery square
                 count += static_tile(c) == kDelivery ? 1 : 0;
             } else {  // distinct locations of goal items, held or not: count a slot's cell once
@@ -395,13 +465,13 @@ struct RowOps {
     }
 
     OC_RH int nid(int c, int d) const {  // graph node of (cell, approach)
-        return ((const uint16_t*)(T + kNodeOff))[c * 5 + d];
+        return ((const uint16_t*)(T + L.node_off))[c * 5 + d];
     }
     OC_RH int dn(int u, int v) const {  // nx.shortest_path_length between node ids, or -1
         // branch-free: a missing node reads entry (0, 0) and is masked, so every lane of a
         // wave issues the same table reads
         const bool none = u == kNoNode || v == kNoNode;
-        const int d = T[kDistOff + (none ? 0 : u * L.nnodes + v)];
+        const int d = T[L.dist_off + (none ? 0 : u * L.nnodes + v)];
         return none || d == kNone ? -1 : d;
     }
 
@@ -486,7 +556,7 @@ struct RowOps {
     //    approach node.
     // helper() clamps each pair's result to >= 1 and starts from perimeter + 1; both are
     // monotone, so the min over B of helper() is this with the same clamp.  Exact in fp32.
-    OC_RH float helper_static(const Sub& s, int ag0, int ag1, int Ac, const uint8_t* bl, int nb,
+    OC_RH float helper_static(const Sub& s, int ag0, int ag1, int Ac, int bl_off, int nb,
                               const uint8_t* dm) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
@@ -507,7 +577,8 @@ struct RowOps {
             const int u1 = nid(ag1, 4), ax = Ac % L.W, ay = Ac / L.W;
             int man = 0x7FFF;
             for (int i = 0; i < nb; ++i) {
-                const int dx = ax - bl[i] % L.W, dy = ay - bl[i] / L.W;
+                const int b = list_cell(bl_off, i);
+                const int dx = ax - b % L.W, dy = ay - b / L.W;
                 const int m = (dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy);
                 man = m < man ? m : man;
             }
@@ -543,8 +614,8 @@ struct RowOps {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int c = r.il(k);
-            const bool ok = c != kNone && r.im(k) == m && !((held >> k) & 1u) &&
-                            !(skip_deliv && static_tile(c) == kDelivery);
+            const bool ok = c != kDead && r.im(k) == m && !((held >> k) & 1u) &&
+                            !(skip_deliv && static_tile(c == kDead ? 0 : c) == kDelivery);
             set |= ok ? 1u << k : 0u;
         }
 #pragma unroll
@@ -588,7 +659,7 @@ struct RowOps {
         }
         float lower = (float)L.perimeter + 1.0f;
         if (s.kind == 1 || s.kind == 3) {  // static B side: one table lookup per A approach
-            const uint8_t* bl = T + (s.kind == 1 ? kCutOff : kDelivOff);
+            const int bl = s.kind == 1 ? L.cut_off : L.deliv_off;
             const int nb = s.kind == 1 ? L.ncut : L.ndeliv;
             const uint8_t* dm = T + L.dmin_off + (s.kind == 1 ? 0 : L.nnodes);
             visit_objs(r, s.start[0], s.kind == 3, [&](int Ac) OC_RL {
@@ -610,7 +681,7 @@ struct RowOps {
     // given_objs; returns BayesianDelegator.subtask_alloc_is_doable (bayesian_delegator.py:98-156):
     // None -> true, else the distance < world.perimeter.
     OC_RH bool full_bound(const Row& r, const Sub& s, float& lb) {
-        ac = 0xFFFFFFFFu;
+        ac = kNoAc;
         active = 1u << s.agent[0];
         if (s.n == 2) active |= 1u << s.agent[1];
         blockers = active;
@@ -642,6 +713,99 @@ struct RowOps {
         return fl;
     }
 
+    // ---- the environment step (OvercookedEnvironment.step, overcooked_environment.py:255-306),
+    // one env: the scalar step of the wide levels, the same rules as ocsw::step4.
+
+    // is_collision (overcooked_environment.py:671-722) of agents i, j with the original action
+    // codes ci, cj: the next squares (unclamped: in the grid, the caller checked), a collidable
+    // one replaced by the agent's own; bit 0 blocks i, bit 1 blocks j
+    OC_RH int collide(const Row& r, int i, int j, int ci, int cj) const {
+        const int lix = r.ax(i), liy = r.ay(i), ljx = r.ax(j), ljy = r.ay(j);
+        int nix = lix + kDX[ci], niy = liy + kDY[ci], njx = ljx + kDX[cj], njy = ljy + kDY[cj];
+        if (static_tile(cell(nix, niy)) != kFloor) { nix = lix; niy = liy; }
+        if (static_tile(cell(njx, njy)) != kFloor) { njx = ljx; njy = ljy; }
+        if (nix == njx && niy == njy) {
+            if (nix == lix && niy == liy && ci != kNoop) return 2;
+            if (njx == ljx && njy == ljy && cj != kNoop) return 1;
+            return 3;
+        }
+        return lix == njx && liy == njy && ljx == nix && ljy == niy ? 3 : 0;
+    }
+
+    // One step of one env.  act: agent a's action code in byte a (codes past 4 are no-ops);
+    // t: the u16 step counter; returns the output flags (OC_FLAG_*) and sets ex (executed codes,
+    // byte a) and cm (collision pairs in itertools.combinations order).
+    OC_RH uint32_t env_step(Row& r, uint32_t& t, uint32_t fl, uint32_t act, const StepLevel& S, uint32_t& ex,
+                            uint32_t& cm) {
+        ac = kNoAc;
+        constexpr uint32_t kNoops = 0x04040404u & (A == 4 ? 0xFFFFFFFFu : (1u << (8 * A)) - 1u);
+        cm = 0u;
+        ex = kNoops;
+        if (fl & 1u) {  // next-step auto-reset (build-defined): the level template
+            r = Row{};
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                Row::s32(r.x, a, S.spawn_x[a]);
+                Row::s32(r.y, a, S.spawn_y[a]);
+                Row::s32(r.h, a, kNone);
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                r.set_loc(j, S.item_cell[j]);
+                r.set_mask(j, S.item_mask[j]);
+            }
+            t = 0u;
+            return 0u;
+        }
+        t = (t + 1u) & 0xFFFFu;  // :257
+        int c[A];
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            const int k = (int)((act >> (8 * a)) & 0xFFu);
+            c[a] = k > kNoop ? kNoop : k;
+        }
+        if (A >= 2) {  // check_collisions looks the unclamped next square up: off the grid it asserts
+            bool off = false;
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                const int nx = r.ax(a) + kDX[c[a]], ny = r.ay(a) + kDY[c[a]];
+                off |= nx < 0 || ny < 0 || nx >= L.W || ny >= L.H;
+            }
+            if (off) return 1u | 4u;  // world.py:429 raises before anything moves: t advanced only
+        }
+        uint32_t blocked = 0u;
+        int pair = 0;
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+#pragma unroll
+            for (int j = i + 1; j < A; ++j, ++pair) {
+                const int b = collide(r, i, j, c[i], c[j]);
+                blocked |= (b & 1 ? 1u << i : 0u) | (b & 2 ? 1u << j : 0u);
+                cm |= b ? 1u << pair : 0u;
+            }
+        ex = 0u;
+#pragma unroll
+        for (int a = 0; a < A; ++a) {  // execute_navigation (:767-770), agents in order
+            const int e = (blocked >> a) & 1u ? kNoop : c[a];
+            interact(r, a, e);
+            ex |= (uint32_t)e << (8 * a);
+        }
+        // new_obs = copy.copy(self) (:289) raises when two co-located agents both hold
+#pragma unroll
+        for (int i = 0; i < A; ++i)
+#pragma unroll
+            for (int j = i + 1; j < A; ++j)
+                if (r.ah(i) != kNone && r.ah(j) != kNone && r.ax(i) == r.ax(j) && r.ay(i) == r.ay(j)) return 1u | 4u;
+        if (S.max_T != 0 && (int)t >= S.max_T) return 1u;  // done(): the timeout first (:328-332)
+        for (int g = 0; g < S.ngoals; ++g) {  // every goal mask at the first Delivery (:344-359)
+            bool ok = false;
+#pragma unroll
+            for (int j = 0; j < K; ++j) ok |= r.il(j) == S.done_cell && r.im(j) == S.goal[g];
+            if (!ok) return 0u;
+        }
+        return 1u | 2u;
+    }
+
     // E2E_BRTDP.Q(state, action, v_l) with value_init's values (e2e_brtdp.py:736-760, :678-729);
     // false where T raises (joint co-location)
     OC_RH bool q_value(const Row& r0, const Sub& s, int c0, int c1, double& q) const {
@@ -668,7 +832,7 @@ struct RowOps {
         if (s.kind == 0) {  // None: one agent, the self agent's movable actions in the full state
             if (s.n != 1) return 4;
             active = blockers = (1u << A) - 1u;
-            ac = 0xFFFFFFFFu;
+            ac = kNoAc;
             int n = 0;
             for (int c = 0; c < 4; ++c) n += single_legal(r, self_agent, c) ? 1 : 0;
             if (n == 0) return 8;

@@ -16,11 +16,12 @@ LIB_PATH = os.path.join(PKG_DIR, "liboc_engine.so")
 
 OC_MAX_AGENTS = 4
 OC_MAX_ITEMS = 16
-OC_MAX_CELLS = 255
+OC_MAX_CELLS = 1024         # grid cells (width and height <= 255)
+OC_MAX_NARROW_CELLS = 255   # up to this many cells: byte cell ids; more ("wide"): u16 ids
 OC_MAX_GOALS = 4
 OC_PITCH_ALIGN = 4096
 OC_NSTATS = 5
-OC_ABI_VERSION = 7  # include/oc_engine.h
+OC_ABI_VERSION = 8  # include/oc_engine.h
 OC_EINVAL, OC_EHIP, OC_ELEVEL = -1, -2, -3
 
 OC_FLAG_DONE = 0x01
@@ -42,7 +43,7 @@ class OcLevelDesc(ctypes.Structure):
         ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("num_items", ctypes.c_int32),
         ("num_spawns", ctypes.c_int32), ("num_goals", ctypes.c_int32),
         ("tiles", ctypes.c_uint8 * OC_MAX_CELLS),
-        ("item_cell", ctypes.c_uint8 * OC_MAX_ITEMS), ("item_mask", ctypes.c_uint8 * OC_MAX_ITEMS),
+        ("item_cell", ctypes.c_uint16 * OC_MAX_ITEMS), ("item_mask", ctypes.c_uint8 * OC_MAX_ITEMS),
         ("spawn_x", ctypes.c_uint8 * OC_MAX_AGENTS), ("spawn_y", ctypes.c_uint8 * OC_MAX_AGENTS),
         ("goal_mask", ctypes.c_uint8 * OC_MAX_GOALS),
         ("encoding", ctypes.c_int32),
@@ -57,6 +58,7 @@ class OcLayout(ctypes.Structure):
         ("plane_agent_hold", ctypes.c_int32), ("plane_item_loc", ctypes.c_int32),
         ("plane_item_mask", ctypes.c_int32), ("plane_t", ctypes.c_int32),
         ("plane_flags", ctypes.c_int32), ("num_planes", ctypes.c_int32),
+        ("plane_item_loc_hi", ctypes.c_int32), ("cell_bytes", ctypes.c_int32),
     ]
 
 
@@ -137,10 +139,18 @@ def item_slots(level: "_lv.Level") -> int:
     return 4 if n <= 4 else (8 if n <= 8 else 16)
 
 
-def layout_planes(A: int, K: int) -> dict:
-    """Plane indices of oc_layout for (A, K) -- mirrors oc_get_layout (pure arithmetic)."""
-    return dict(agent_x=0, agent_y=A, agent_hold=2 * A, item_loc=3 * A, item_mask=3 * A + K,
-                t=3 * A + 2 * K, flags=3 * A + 2 * K + 2, num_planes=3 * A + 2 * K + 3)
+def is_wide(level: "_lv.Level") -> bool:
+    """More than 255 cells: u16 cell ids (the wide layout, include/oc_engine.h oc_layout)."""
+    return level.width * level.height > OC_MAX_NARROW_CELLS
+
+
+def layout_planes(A: int, K: int, wide: bool = False) -> dict:
+    """Plane indices of oc_layout for (A, K) -- mirrors oc_get_layout (pure arithmetic).  A wide
+    level has its item cells' high bytes in K planes after the low ones (item_loc_hi)."""
+    LK = 2 * K if wide else K
+    return dict(agent_x=0, agent_y=A, agent_hold=2 * A, item_loc=3 * A, item_loc_hi=3 * A + K if wide else -1,
+                item_mask=3 * A + LK, t=3 * A + LK + K, flags=3 * A + LK + K + 2, num_planes=3 * A + LK + K + 3,
+                cell_bytes=2 if wide else 1)
 
 
 def pitch_for(B: int) -> int:

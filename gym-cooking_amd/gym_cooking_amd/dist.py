@@ -46,20 +46,17 @@ def shard_global(global_batch: int, rank: int, world: int, local_rank: int = 0) 
     return Shard(rank, world, local_rank, off, base + (1 if rank < rem else 0))
 
 
-def _free_port() -> int:
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def init(backend: str = "nccl") -> Shard:
     """Initialise the process group from torchrun's env (MASTER_ADDR/PORT, RANK, WORLD_SIZE).
 
     With backend "nccl" (RCCL over xGMI) the group is created at EVERY world size, world 1
     included: a single-GPU run then issues the same RCCL all-gather / all-reduce calls as an
-    8-GPU one (a world-1 communicator; rendezvous on a TCP store at 127.0.0.1 when torchrun
-    did not set MASTER_ADDR/PORT).  gloo (the CPU tests) only joins a group for world > 1."""
+    8-GPU one (a world-1 communicator; its rendezvous is an in-process store when torchrun did
+    not set MASTER_ADDR/PORT: no port to probe, none to lose).  The direct communicator of the
+    window's all-gather (RcclComm) is an optimisation of that path: when librccl cannot be
+    loaded or the communicator does not come up, the process group's collectives carry the
+    all-gather instead (a warning on stderr).  gloo (the CPU tests) only joins a group for
+    world > 1."""
     rank, world, local = world_from_env()
     if not dist.is_initialized():
         if backend == "nccl":
@@ -68,10 +65,16 @@ def init(backend: str = "nccl") -> Shard:
             if "MASTER_ADDR" not in os.environ or "MASTER_PORT" not in os.environ:
                 if world != 1:
                     raise RuntimeError("WORLD_SIZE %d without MASTER_ADDR/MASTER_PORT" % world)
-                kw = dict(init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1)
+                kw = dict(store=dist.HashStore(), rank=0, world_size=1)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), **kw)
             global _RCCL
-            _RCCL = RcclComm(torch.device("cuda", local))
+            try:
+                _RCCL = RcclComm(torch.device("cuda", local))
+            except (OSError, RuntimeError, AttributeError) as exc:
+                import sys
+                print("dist: direct RCCL communicator unavailable (%s); all-gathers go through the process "
+                      "group" % exc, file=sys.stderr)
+                _RCCL = None
         elif world > 1:
             dist.init_process_group(backend)
     return Shard(rank, world, local, 0, 0)

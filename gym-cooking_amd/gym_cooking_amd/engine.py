@@ -319,14 +319,17 @@ class CpuStepper:
     def new_state(self) -> np.ndarray:
         """The level template in every env (reset(), overcooked_environment.py:201-250), built
         on the host from the level description."""
-        A, K, P = self.A, self.K, self.pitch
-        s = np.zeros((self.layout.num_planes, P), np.uint8)
+        A, K, P, L = self.A, self.K, self.pitch, self.layout
+        s = np.zeros((L.num_planes, P), np.uint8)
         lv = self.level
         for a in range(A):
             s[a], s[A + a], s[2 * A + a] = lv.spawns[a][0], lv.spawns[a][1], 0xFF
+        dead = 0xFFFF if L.cell_bytes == 2 else 0xFF
         for j in range(K):
-            c, m = (lv.items[j] if j < len(lv.items) else (0xFF, 0))
-            s[3 * A + j], s[3 * A + K + j] = c, m
+            c, m = (lv.items[j] if j < len(lv.items) else (dead, 0))
+            s[L.plane_item_loc + j], s[L.plane_item_mask + j] = c & 0xFF, m
+            if L.cell_bytes == 2:
+                s[L.plane_item_loc_hi + j] = c >> 8
         return s.reshape(-1)
 
     def step(self, state_in: np.ndarray, state_out: np.ndarray, actions: np.ndarray,

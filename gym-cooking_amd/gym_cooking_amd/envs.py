@@ -398,6 +398,18 @@ def is_collision(world, agent1_loc, agent2_loc, agent1_action, agent2_action):
     return execute
 
 
+def _decode_items(b, A: int, K: int):
+    """(item cells, masks, t, flags, dead cell value) of one env's state bytes: the narrow
+    layout (3A + 2K + 3 bytes, byte cells) or the wide one (3A + 3K + 3: the cells' high bytes
+    after the low ones, include/oc_engine.h oc_layout)."""
+    if len(b) == 3 * A + 3 * K + 3:
+        loc = [b[3 * A + j] | (b[3 * A + K + j] << 8) for j in range(K)]
+        m0, dead = 3 * A + 2 * K, 0xFFFF
+    else:
+        loc, m0, dead = b[3 * A:3 * A + K], 3 * A + K, _levels.LOC_DEAD
+    return loc, b[m0:m0 + K], b[m0 + K] | (b[m0 + K + 1] << 8), b[m0 + K + 2], dead
+
+
 def build_views(level: _levels.Level, A: int, K: int, env_bytes: np.ndarray, actions=None, group_names=(),
                 reachability_graph: Optional[ReachabilityGraph] = None):
     """(sim_agents, world, t, flags) of one env from its canonical state bytes
@@ -405,13 +417,11 @@ def build_views(level: _levels.Level, A: int, K: int, env_bytes: np.ndarray, act
     `group_names`: object names whose (possibly empty) groups the world keeps."""
     b = [int(v) for v in env_bytes]
     ax, ay, ah = b[0:A], b[A:2 * A], b[2 * A:3 * A]
-    loc, mask = b[3 * A:3 * A + K], b[3 * A + K:3 * A + 2 * K]
-    t = b[3 * A + 2 * K] | (b[3 * A + 2 * K + 1] << 8)
-    flags = b[3 * A + 2 * K + 2]
+    loc, mask, t, flags, dead = _decode_items(b, A, K)
     held = {h: a for a, h in enumerate(ah) if h != _levels.HOLD_NONE}
     items = {}
     for j in range(K):
-        if loc[j] == _levels.LOC_DEAD:
+        if loc[j] == dead:
             continue
         items[j] = ItemView(j, mask[j], level.xy(loc[j]), j in held, level.encoding)
     agents = []
@@ -506,13 +516,23 @@ class OvercookedEnvironment:
             raise RuntimeError("call reset() before step()")
         names = self.get_agent_names()
         codes = [action_code(action_dict[n]) for n in names]
-        if eng.A >= 2 and self.level.edge:  # check_collisions' unclamped lookup (:692-700)
+        if eng.A >= 2 and self.level.edge and any(
+                self.level.off_grid(a.location[0], a.location[1], codes[names.index(a.name)]) for a in self.sim_agents):
+            # an action off the grid: step raises in check_collisions (is_collision looks the
+            # unclamped square up, :692-700; world.py:429 asserts).  What the reference has done by
+            # then: t += 1 (:257), every sim_agent.action set (:263-264), and a CollisionRepr for
+            # each earlier pair (in combinations order) that collided (:731-752)
+            self.t += 1
             for a in self.sim_agents:
-                x, y = a.location
-                if self.level.off_grid(x, y, codes[names.index(a.name)]):
-                    self.t += 1  # step increments t before it raises (:257)
-                    dx, dy = _levels.ACTIONS[codes[names.index(a.name)]]
-                    raise AssertionError("0 gridsquares at {}: []".format((x + dx, y + dy)))  # world.py:429
+                a.action = _levels.ACTIONS[codes[names.index(a.name)]]
+            for i in range(eng.A):
+                for j in range(i + 1, eng.A):
+                    ai, aj = self.sim_agents[i], self.sim_agents[j]
+                    exec_ = is_collision(self.world, ai.location, aj.location, ai.action, aj.action)  # may raise
+                    if not all(exec_):
+                        self.collisions.append(CollisionRepr(time=self.t, agent_names=[ai.name, aj.name],
+                                                             agent_locations=[ai.location, aj.location]))
+            raise AssertionError("off-grid action without a raise")  # unreachable: some pair raised above
         pre = self._host
         new, ex, coll = eng.step(pre, codes)
         t_now = self.t + 1
@@ -673,6 +693,10 @@ class OvercookedEnvironment:
 def _object_planes(env_bytes: np.ndarray, A: int, K: int) -> Dict[str, np.ndarray]:
     """The held-slot, location and mask planes of one env's state bytes (render.DrawOrder);
     the shim steps a finished env again (it clears DONE), so no auto-reset is implied."""
+    if len(env_bytes) == 3 * A + 3 * K + 3:  # wide layout: DrawOrder reads only whether a slot is live
+        dead = (env_bytes[3 * A:3 * A + K] == 0xFF) & (env_bytes[3 * A + K:3 * A + 2 * K] == 0xFF)
+        return {"ah": env_bytes[2 * A:3 * A], "loc": np.where(dead, 0xFF, 0).astype(np.uint8),
+                "mask": env_bytes[3 * A + 2 * K:3 * A + 3 * K]}
     return {"ah": env_bytes[2 * A:3 * A], "loc": env_bytes[3 * A:3 * A + K], "mask": env_bytes[3 * A + K:3 * A + 2 * K]}
 
 

@@ -35,7 +35,8 @@ Item contents are encoded as a byte mask in one of two encodings (include/oc_eng
   full_name, a sorted multiset of content names (core.py:143-171); a merged object holds only
   foods in their last state and at most one plate (mergeable, core.py:222-241), so the Fresh
   bit only ever marks a single fresh food and the mask is exact for up to 3 of each food.
-Grids of up to 255 cells are supported (cell ids are bytes, 0xFF = dead).
+Grids of up to 1,024 cells (width and height up to 255) are supported: cell ids are bytes
+(0xFF = dead) up to 255 cells, u16 (0xFFFF = dead) past that (the engine's wide layout).
 """
 from __future__ import annotations
 
@@ -69,7 +70,8 @@ MAX_PER_FOOD = 3   # ENC_COUNTS: 2-bit counts
 # Engine limits (include/oc_engine.h).
 MAX_AGENTS = 4
 MAX_ITEMS = 16
-MAX_CELLS = 255
+MAX_CELLS = 1024          # OC_MAX_CELLS
+MAX_NARROW_CELLS = 255    # OC_MAX_NARROW_CELLS: byte cell ids up to here
 MAX_GOALS = 4
 LOC_DEAD = 0xFF
 HOLD_NONE = 0xFF
@@ -297,8 +299,9 @@ class Level:
                              "raises IndexError in World.add_object (world.py:302)" % (self.name, x, y, self.width))
         if len(self.spawns) < num_agents:
             raise ValueError("level %s has %d spawns < %d agents" % (self.name, len(self.spawns), num_agents))
-        if self.ncells > MAX_CELLS:
-            raise ValueError("level %s has %d cells > %d" % (self.name, self.ncells, MAX_CELLS))
+        if self.ncells > MAX_CELLS or self.width > 255 or self.height > 255:
+            raise ValueError("level %s: %dx%d = %d cells (at most %d, sides <= 255)"
+                             % (self.name, self.width, self.height, self.ncells, MAX_CELLS))
         if len(self.items) > MAX_ITEMS:
             raise ValueError("level %s has %d items > %d" % (self.name, len(self.items), MAX_ITEMS))
         per_food = self.food_counts()

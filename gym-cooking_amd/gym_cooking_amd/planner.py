@@ -93,7 +93,22 @@ def _encoding(level) -> int:
 _CAND = {n: list(itertools.product(range(5), repeat=n)) for n in (1, 2)}
 
 
-def _canon(sb: bytes, A: int, K: int, enc: int = 0) -> bytes:
+def _lay(A: int, K: int, wide: bool = False):
+    """(first item-cell plane, first high-byte plane or -1, first mask plane) of a state's bytes:
+    the narrow layout (byte cells) or the wide one (u16 cells: high bytes in K planes after the
+    low ones, include/oc_engine.h oc_layout)."""
+    return (3 * A, 3 * A + K, 3 * A + 2 * K) if wide else (3 * A, -1, 3 * A + K)
+
+
+def _live(b, A: int, K: int, wide: bool = False) -> List[bool]:
+    """Per slot: the item is in the world (its cell is not OC_LOC_DEAD / OC_LOC_DEAD16)."""
+    l0, lh, _ = _lay(A, K, wide)
+    if lh < 0:
+        return [b[l0 + j] != 0xFF for j in range(K)]
+    return [b[l0 + j] != 0xFF or b[lh + j] != 0xFF for j in range(K)]
+
+
+def _canon(sb: bytes, A: int, K: int, enc: int = 0, wide: bool = False) -> bytes:
     """The planner's form of a state: live item slots ordered by (object-group name, slot).
     The reference's repr lists each group's objects in insertion order and nothing else, so
     an item's identity is its group name plus its rank in that group; which slot a merged
@@ -101,8 +116,9 @@ def _canon(sb: bytes, A: int, K: int, enc: int = 0) -> bytes:
     re-inserts the merged object).  Plates, the only name with two members, keep their
     relative slot order, as they keep their order in World.objects."""
     b = bytearray(sb)
-    l0, m0 = 3 * A, 3 * A + K
-    live = sorted((_group_name(b[m0 + j], enc), j) for j in range(K) if b[l0 + j] != 0xFF)
+    l0, lh, m0 = _lay(A, K, wide)
+    alive = _live(b, A, K, wide)
+    live = sorted((_group_name(b[m0 + j], enc), j) for j in range(K) if alive[j])
     order = [j for _, j in live]
     if order == list(range(len(order))):
         return bytes(b)
@@ -110,6 +126,8 @@ def _canon(sb: bytes, A: int, K: int, enc: int = 0) -> bytes:
     locs = [b[l0 + j] for j in order] + [0xFF] * (K - len(order))
     masks = [b[m0 + j] for j in order] + [0] * (K - len(order))
     b[l0:l0 + K], b[m0:m0 + K] = bytes(locs), bytes(masks)
+    if lh >= 0:
+        b[lh:lh + K] = bytes([b[lh + j] for j in order] + [0xFF] * (K - len(order)))
     for a in range(A):
         h = b[2 * A + a]
         if h != 0xFF:
@@ -175,6 +193,7 @@ class _Expander:
     def __init__(self, level, num_agents: int, device):
         from .engine import OvercookedBatch  # raises without liboc_engine.so / a GPU
         self.eb = OvercookedBatch(level, num_agents, self.ROWS, max_T=0, device=device)
+        self.wide = self.eb.layout.cell_bytes == 2  # u16 item cells (a level of more than 255 cells)
         self.A, self.K, self.P = self.eb.A, self.eb.K, self.eb.pitch
         self.enc = self.eb.level.encoding
         self.NP = self.eb.layout.num_planes
@@ -405,7 +424,7 @@ class E2E_BRTDP:
             start = np.frombuffer(full, np.uint8).copy()
             if not self._level:
                 start = self._level0(start, exp)
-            start = np.frombuffer(_canon(start.tobytes(), exp.A, exp.K, exp.enc), np.uint8).copy()
+            start = np.frombuffer(_canon(start.tobytes(), exp.A, exp.K, exp.enc, exp.wide), np.uint8).copy()
             count = self._obj_count(start, exp, level)  # _define_goal_state on the Level-0 env
             # [start, kind, goal mask, cur_obj_count, subtask row, (goal, bound) of the no-op row]
             hit = [start, kind, goal, count, capi.subtask(kind, list(agents), list(starts), goal, count, self._level),
@@ -453,24 +472,29 @@ class E2E_BRTDP:
         kernel treats them as AgentCounters)."""
         s = full.copy()
         A, K = exp.A, exp.K
+        l0, lh, m0 = _lay(A, K, exp.wide)
         for a in range(A):
             if a in self._agents:
                 continue
             h = int(s[2 * A + a])
             if h != 0xFF:
-                s[3 * A + h], s[3 * A + K + h] = 0xFF, 0
+                s[l0 + h], s[m0 + h] = 0xFF, 0
+                if lh >= 0:
+                    s[lh + h] = 0xFF
                 s[2 * A + a] = 0xFF
         return s
 
     def _obj_count(self, s: np.ndarray, exp, level) -> int:
         """cur_obj_count of _define_goal_state (e2e_brtdp.py:435-566) on a Level-0 state."""
         A, K = exp.A, exp.K
+        l0, lh, m0 = _lay(A, K, exp.wide)
         held = {int(s[2 * A + a]) for a in range(A)} - {0xFF}
         deliv = _level_tables(level)[1]
         locs = []
+        alive = _live(s, A, K, exp.wide)
         for j in range(K):
-            c, m = int(s[3 * A + j]), int(s[3 * A + K + j])
-            if c == 0xFF or m != self._goal_mask:
+            c, m = int(s[l0 + j]) | (int(s[lh + j]) << 8 if lh >= 0 else 0), int(s[m0 + j])
+            if not alive[j] or m != self._goal_mask:
                 continue
             if self._kind == 3:
                 if j not in held and c in deliv:
@@ -527,8 +551,8 @@ class E2E_BRTDP:
         sb, groups, agents, lvl = key
         if _native is not None and self.use_native and fl.dtype == np.uint8 and lb.dtype == np.float32:
             return self._expanded_native(key, cand, nxt, fl, lb)
-        NP, K, A, enc = len(sb), self._exp.K, self._exp.A, self._exp.enc
-        l0, m0 = 3 * A, 3 * A + K
+        NP, K, A, enc, wide = len(sb), self._exp.K, self._exp.A, self._exp.enc, self._exp.wide
+        l0, lh, m0 = _lay(A, K, wide)
         raw = nxt.tobytes()
         pmask = sb[m0:m0 + K]
         sk = self._sub_key
@@ -547,8 +571,8 @@ class E2E_BRTDP:
             ns = raw[r * NP:(r + 1) * NP]
             ng = groups
             if ns[m0:m0 + K] != pmask:  # a chop or a merge: a merge makes a new object group (world.py:304-306)
-                ns = _canon(ns, A, K, enc)
-                ng = groups | frozenset(_group_name(m, enc) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
+                ns = _canon(ns, A, K, enc, wide)
+                ng = groups | frozenset(_group_name(m, enc) for m, l in zip(ns[m0:m0 + K], _live(ns, A, K, wide)) if l)
             nk = (ns, ng, agents, lvl)
             if lvl and _copy_crashes(ns, A):
                 crash = crash or set()
@@ -571,12 +595,12 @@ class E2E_BRTDP:
     def _expanded_native(self, key, cand, nxt, fl, lb) -> None:
         """_expanded with the row loop in C (_brtdp.expand): the same entry, field for field."""
         groups = key[1]
-        A, K, enc = self._exp.A, self._exp.K, self._exp.enc
-        l0, m0 = 3 * A, 3 * A + K
+        A, K, enc, wide = self._exp.A, self._exp.K, self._exp.enc, self._exp.wide
+        l0, lh, m0 = _lay(A, K, wide)
 
         def changed(ns):  # a chop or a merge: canonical slot order, a merge's new object group
-            ns = _canon(ns, A, K, enc)
-            return ns, groups | frozenset(_group_name(m, enc) for m, l in zip(ns[m0:m0 + K], ns[l0:l0 + K]) if l != 0xFF)
+            ns = _canon(ns, A, K, enc, wide)
+            return ns, groups | frozenset(_group_name(m, enc) for m, l in zip(ns[m0:m0 + K], _live(ns, A, K, wide)) if l)
         sk = self._sub_key
         nxt = np.ascontiguousarray(nxt)
         entry, illegal = _native.expand(nxt, np.ascontiguousarray(fl), np.ascontiguousarray(lb), cand, key, sk, m0, K,
@@ -835,7 +859,7 @@ class E2E_BRTDP:
         full = env.state_bytes()
         full[exp.t_plane:] = 0
         groups = _groups(env)
-        key = (_canon(full.tobytes(), exp.A, exp.K, exp.enc), groups, tuple(self._agents), self._level)
+        key = (_canon(full.tobytes(), exp.A, exp.K, exp.enc, exp.wide), groups, tuple(self._agents), self._level)
         yield from self._modified_state(key)
 
     def _modified_state(self, key):
@@ -873,10 +897,11 @@ class PlanEnv:
         self._device = device
         self._A = num_agents
         self._bytes = np.asarray(state_bytes, dtype=np.uint8).copy()
-        K = (len(self._bytes) - 3 * num_agents - 3) // 2
-        loc = self._bytes[3 * num_agents:3 * num_agents + K]
-        mask = self._bytes[3 * num_agents + K:3 * num_agents + 2 * K]
-        self._live = [(j, int(m)) for j, (l, m) in enumerate(zip(loc, mask)) if l != 0xFF]
+        wide = capi.is_wide(level if not isinstance(level, str) else _levels.load_level(level))
+        K = (len(self._bytes) - 3 * num_agents - 3) // (3 if wide else 2)
+        _, _, m0 = _lay(num_agents, K, wide)
+        mask = self._bytes[m0:m0 + K]
+        self._live = [(j, int(m)) for j, (l, m) in enumerate(zip(_live(self._bytes, num_agents, K, wide), mask)) if l]
         self._world = None
         self._group_names = frozenset(group_names)
         self._enc = _encoding(level)

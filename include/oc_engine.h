@@ -35,11 +35,13 @@
 extern "C" {
 #endif
 
-#define OC_ABI_VERSION 7
+#define OC_ABI_VERSION 8
 
 #define OC_MAX_AGENTS 4
 #define OC_MAX_ITEMS 16  /* item slots: K = 4, 8 or 16 per level */
-#define OC_MAX_CELLS 255  /* cell ids are bytes; 0xFF is OC_LOC_DEAD */
+#define OC_MAX_CELLS 1024       /* grid cells (width and height <= 255 each) */
+#define OC_MAX_NARROW_CELLS 255 /* levels of at most this many cells have byte cell ids (0xFF is
+                                   OC_LOC_DEAD); larger ("wide") levels u16 ids (OC_LOC_DEAD16) */
 #define OC_MAX_GOALS 4
 #define OC_PITCH_ALIGN 4096
 
@@ -89,6 +91,7 @@ extern "C" {
 
 #define OC_HOLD_NONE 0xFFu
 #define OC_LOC_DEAD 0xFFu
+#define OC_LOC_DEAD16 0xFFFFu
 
 /* flags plane bits */
 #define OC_FLAG_DONE 0x01u    /* done() returned True (overcooked_environment.py:316-363) */
@@ -110,13 +113,13 @@ extern "C" {
 #define OC_NSTATS 5
 
 typedef struct oc_level_desc {
-    int32_t width, height;           /* 3..; width*height <= OC_MAX_CELLS */
+    int32_t width, height;           /* 3..255; width*height <= OC_MAX_CELLS */
     int32_t num_items;               /* <= OC_MAX_ITEMS; OC_ENC_PRESENCE: at most one of each food
                                         type, OC_ENC_COUNTS: at most OC_MC_MAX_PER_FOOD */
     int32_t num_spawns;              /* >= num_agents */
     int32_t num_goals;               /* 1..OC_MAX_GOALS Deliver goal masks */
     uint8_t tiles[OC_MAX_CELLS];     /* OC_TILE_* per cell, cell = y*width + x */
-    uint8_t item_cell[OC_MAX_ITEMS]; /* initial item cells, map scan order */
+    uint16_t item_cell[OC_MAX_ITEMS]; /* initial item cells, map scan order */
     uint8_t item_mask[OC_MAX_ITEMS]; /* initial item content masks */
     uint8_t spawn_x[OC_MAX_AGENTS];
     uint8_t spawn_y[OC_MAX_AGENTS];
@@ -133,11 +136,15 @@ typedef struct oc_layout {
     int32_t plane_agent_x;  /* A planes, u8 */
     int32_t plane_agent_y;  /* A planes, u8 */
     int32_t plane_agent_hold; /* A planes, u8 item slot or OC_HOLD_NONE */
-    int32_t plane_item_loc; /* K planes, u8 cell or OC_LOC_DEAD */
+    int32_t plane_item_loc; /* K planes: the item cells (u8, OC_LOC_DEAD = none), or on a wide level
+                               their low bytes */
     int32_t plane_item_mask;/* K planes, u8 content mask */
     int32_t plane_t;        /* u16 step counter, spans 2 planes */
     int32_t plane_flags;    /* u8 OC_FLAG_* */
-    int32_t num_planes;     /* 3A + 2K + 3 */
+    int32_t num_planes;     /* 3A + 2K + 3; wide: 3A + 3K + 3 */
+    int32_t plane_item_loc_hi; /* wide levels: K planes, the item cells' high bytes (cell =
+                                  lo | hi << 8, OC_LOC_DEAD16 = none); -1 on a narrow level */
+    int32_t cell_bytes;     /* 1 (narrow) or 2 (wide: more than OC_MAX_NARROW_CELLS cells) */
 } oc_layout;
 
 typedef struct oc_handle oc_handle;

@@ -350,17 +350,21 @@ static void unpack(const Cfg* c, const uint8_t* s, int64_t e, Env* env, int* fla
     const uint8_t* ax = s + 0 * A * P;
     const uint8_t* ay = s + 1 * A * P;
     const uint8_t* ah = s + 2 * A * P;
+    /* a wide level (more than OC_MAX_NARROW_CELLS cells): u16 cells, high bytes in K planes
+     * after the low ones (oc_layout.plane_item_loc_hi) */
+    const int wide = c->L->width * c->L->height > OC_MAX_NARROW_CELLS, LK = wide ? 2 * K : K;
     const uint8_t* il = s + 3 * A * P;
-    const uint8_t* im = s + (3 * A + K) * P;
-    const uint16_t* tp = (const uint16_t*)(s + (3 * A + 2 * K) * P);
-    const uint8_t* fl = s + (3 * A + 2 * K + 2) * P;
+    const uint8_t* ilh = s + (3 * A + K) * P;
+    const uint8_t* im = s + (3 * A + LK) * P;
+    const uint16_t* tp = (const uint16_t*)(s + (3 * A + LK + K) * P);
+    const uint8_t* fl = s + (3 * A + LK + K + 2) * P;
     env->t = tp[e];
     *flags = fl[e];
     for (int k = 0; k < K; ++k) {
         Obj* o = &env->objs[k];
         memset(o, 0, sizeof(*o));
-        uint8_t loc = il[k * P + e], m = im[k * P + e];
-        o->alive = loc != OC_LOC_DEAD;
+        const int loc = il[k * P + e] | (wide ? ilh[k * P + e] << 8 : 0), m = im[k * P + e];
+        o->alive = loc != (wide ? (int)OC_LOC_DEAD16 : (int)OC_LOC_DEAD);
         o->location.x = loc % c->L->width;
         o->location.y = loc / c->L->width;
         obj_set_mask(o, m, c->L->encoding);
@@ -388,10 +392,12 @@ static void pack(const Cfg* c, const Env* env, int flags, uint8_t* s, int64_t e)
     uint8_t* ax = s + 0 * A * P;
     uint8_t* ay = s + 1 * A * P;
     uint8_t* ah = s + 2 * A * P;
+    const int wide = c->L->width * c->L->height > OC_MAX_NARROW_CELLS, LK = wide ? 2 * K : K;
     uint8_t* il = s + 3 * A * P;
-    uint8_t* im = s + (3 * A + K) * P;
-    uint16_t* tp = (uint16_t*)(s + (3 * A + 2 * K) * P);
-    uint8_t* fl = s + (3 * A + 2 * K + 2) * P;
+    uint8_t* ilh = s + (3 * A + K) * P;
+    uint8_t* im = s + (3 * A + LK) * P;
+    uint16_t* tp = (uint16_t*)(s + (3 * A + LK + K) * P);
+    uint8_t* fl = s + (3 * A + LK + K + 2) * P;
     tp[e] = (uint16_t)env->t;
     fl[e] = (uint8_t)flags;
     for (int a = 0; a < A; ++a) {
@@ -403,10 +409,13 @@ static void pack(const Cfg* c, const Env* env, int flags, uint8_t* s, int64_t e)
         const Obj* o = &env->objs[k];
         if (!o->alive) {
             il[k * P + e] = OC_LOC_DEAD;
+            if (wide) ilh[k * P + e] = OC_LOC_DEAD;
             im[k * P + e] = 0;
             continue;
         }
-        il[k * P + e] = (uint8_t)(o->location.y * c->L->width + o->location.x);
+        const int cell = o->location.y * c->L->width + o->location.x;
+        il[k * P + e] = (uint8_t)cell;
+        if (wide) ilh[k * P + e] = (uint8_t)(cell >> 8);
         im[k * P + e] = (uint8_t)obj_mask_enc(o, c->L->encoding);
     }
 }
@@ -707,8 +716,8 @@ static void build_reach(const oc_level_desc* L, Reach* R) {
             if (!dup) { adj[u][deg[u]++] = v; adj[v][deg[v]++] = u; }
         }
     }
-    for (int s0 = 0; s0 < RG_N; ++s0) {
-        for (int t0 = 0; t0 < RG_N; ++t0) R->dist[s0][t0] = -1;
+    for (int s0 = 0; s0 < N * 5; ++s0) { /* rows / columns past the level's cells are never read */
+        for (int t0 = 0; t0 < N * 5; ++t0) R->dist[s0][t0] = -1;
         if (!R->exists[s0]) continue;
         int q[RG_N], qh = 0, qt = 0;
         R->dist[s0][s0] = 0;

@@ -70,7 +70,8 @@ class OracleBatch:
         self.max_T = max_T
         self.B = B
         self.pitch = capi.pitch_for(B)
-        self.planes = capi.layout_planes(self.A, self.K)
+        self.wide = capi.is_wide(level)
+        self.planes = capi.layout_planes(self.A, self.K, self.wide)
         self.desc = capi.level_desc(level, num_agents)
 
     def new_state(self) -> np.ndarray:

@@ -11,24 +11,37 @@
 #include "../../gym-cooking_amd/csrc/oc_rollout.h"
 #include "../../include/oc_engine.h"
 
-template <int A, int K>
+// the planes of oc_layout (a wide level: the item cells' high bytes in K planes after the low)
+template <int A, int K, bool W>
+struct PL {
+    static constexpr int Y = A, H = 2 * A, L = 3 * A, LH = 3 * A + K, M = 3 * A + (W ? 2 : 1) * K, T = M + K, F = T + 2;
+};
+
+template <int A, int K, bool W>
+static ocro::RowT<K, W> load(const uint8_t* sin, int64_t P, int64_t e) {
+    using Pl = PL<A, K, W>;
+    ocro::RowT<K, W> r;
+    for (int a = 0; a < A; ++a) {
+        r.x |= (uint32_t)sin[a * P + e] << (8 * a);
+        r.y |= (uint32_t)sin[(Pl::Y + a) * P + e] << (8 * a);
+        r.h |= (uint32_t)sin[(Pl::H + a) * P + e] << (8 * a);
+    }
+    for (int j = 0; j < K; ++j) {
+        r.set_loc(j, (uint32_t)sin[(Pl::L + j) * P + e] | (W ? (uint32_t)sin[(Pl::LH + j) * P + e] << 8 : 0u));
+        r.set_mask(j, sin[(Pl::M + j) * P + e]);
+    }
+    return r;
+}
+
+template <int A, int K, bool W>
 static void run(const oc_level_desc* lv, const uint8_t* sin, uint8_t* sout, const uint8_t* act, const uint8_t* alloc,
                 const oc_subtask* subs, int nsub, uint8_t* flags, float* lb, int64_t B, int64_t P) {
     static uint8_t blob[ocro::kBlobMax];
     ocro::RollLevel L;
     if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
-    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+    using Pl = PL<A, K, W>;
     for (int64_t e = 0; e < B; ++e) {
-        ocro::RowT<K> r;
-        for (int a = 0; a < A; ++a) {
-            r.x |= (uint32_t)sin[a * P + e] << (8 * a);
-            r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
-            r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
-        }
-        for (int j = 0; j < K; ++j) {
-            r.loc[j >> 3] |= (uint64_t)sin[(kPL + j) * P + e] << (8 * (j & 7));
-            r.mask[j >> 3] |= (uint64_t)sin[(kPM + j) * P + e] << (8 * (j & 7));
-        }
+        ocro::RowT<K, W> r = load<A, K, W>(sin, P, e);
         const int ai = alloc ? alloc[e] : 0;
         float bound = 0.0f;
         int f = OC_ROLL_BADALLOC;
@@ -37,55 +50,46 @@ static void run(const oc_level_desc* lv, const uint8_t* sin, uint8_t* sout, cons
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
                         {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
             const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
-            ocro::RowOps<A, K> ops(L, blob);
+            ocro::RowOps<A, K, W> ops(L, blob);
             f = ops.run(r, s, c0, c1, bound);
         }
         for (int a = 0; a < A; ++a) {
             sout[a * P + e] = (uint8_t)r.ax(a);
-            sout[(kPY + a) * P + e] = (uint8_t)r.ay(a);
-            sout[(kPH + a) * P + e] = (uint8_t)r.ah(a);
+            sout[(Pl::Y + a) * P + e] = (uint8_t)r.ay(a);
+            sout[(Pl::H + a) * P + e] = (uint8_t)r.ah(a);
         }
         for (int j = 0; j < K; ++j) {
-            sout[(kPL + j) * P + e] = (uint8_t)r.il(j);
-            sout[(kPM + j) * P + e] = (uint8_t)r.im(j);
+            sout[(Pl::L + j) * P + e] = (uint8_t)r.il(j);
+            if (W) sout[(Pl::LH + j) * P + e] = (uint8_t)(r.il(j) >> 8);
+            sout[(Pl::M + j) * P + e] = (uint8_t)r.im(j);
         }
-        sout[kPT * P + 2 * e] = sin[kPT * P + 2 * e];
-        sout[kPT * P + 2 * e + 1] = sin[kPT * P + 2 * e + 1];
-        sout[kPF * P + e] = sin[kPF * P + e];
+        sout[Pl::T * P + 2 * e] = sin[Pl::T * P + 2 * e];
+        sout[Pl::T * P + 2 * e + 1] = sin[Pl::T * P + 2 * e + 1];
+        sout[Pl::F * P + e] = sin[Pl::F * P + e];
         flags[e] = (uint8_t)f;
         lb[e] = bound;
     }
 }
 
-template <int A, int K>
+template <int A, int K, bool W>
 static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* taken_p, const uint8_t* alloc,
                 const oc_subtask* subs, int nsub, int self_agent, double beta, double nap, double* out, uint8_t* flags,
                 int64_t B, int64_t P) {
     static uint8_t blob[ocro::kBlobMax];
     ocro::RollLevel L;
     if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
-    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
     for (int64_t e = 0; e < B; ++e) {
         const int ai = alloc ? alloc[e] : 0;
         double v = 0.0;
         int f = OC_LIK_BADALLOC;
         if (ai < nsub) {
-            ocro::RowT<K> r;
-            for (int a = 0; a < A; ++a) {
-                r.x |= (uint32_t)sin[a * P + e] << (8 * a);
-                r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
-                r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
-            }
-            for (int j = 0; j < K; ++j) {
-                r.loc[j >> 3] |= (uint64_t)sin[(kPL + j) * P + e] << (8 * (j & 7));
-                r.mask[j >> 3] |= (uint64_t)sin[(kPM + j) * P + e] << (8 * (j & 7));
-            }
+            ocro::RowT<K, W> r = load<A, K, W>(sin, P, e);
             uint32_t taken = 0;
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
             const oc_subtask& o = subs[ai];
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
                         {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
-            ocro::RowOps<A, K> ops(L, blob);
+            ocro::RowOps<A, K, W> ops(L, blob);
             f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
         }
         out[e] = f == OC_LIK_OK ? v : 0.0;
@@ -96,8 +100,13 @@ static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* take
 extern "C" int lik_host(const oc_level_desc* lv, int A, int K, const uint8_t* sin, const uint8_t* taken,
                         const uint8_t* alloc, const oc_subtask* subs, int nsub, int self_agent, double beta, double nap,
                         double* out, uint8_t* flags, int64_t B, int64_t P) {
-#define L_(a, k) \
-    if (A == a && K == k) { lik<a, k>(lv, sin, taken, alloc, subs, nsub, self_agent, beta, nap, out, flags, B, P); return 0; }
+    const bool wide = lv->width * lv->height > OC_MAX_NARROW_CELLS;
+#define L_(a, k)                                                                                                   \
+    if (A == a && K == k) {                                                                                       \
+        if (wide) lik<a, k, true>(lv, sin, taken, alloc, subs, nsub, self_agent, beta, nap, out, flags, B, P);    \
+        else lik<a, k, false>(lv, sin, taken, alloc, subs, nsub, self_agent, beta, nap, out, flags, B, P);        \
+        return 0;                                                                                                 \
+    }
     L_(1, 4) L_(2, 4) L_(3, 4) L_(4, 4) L_(1, 8) L_(2, 8) L_(3, 8) L_(4, 8) L_(1, 16) L_(2, 16) L_(3, 16) L_(4, 16)
 #undef L_
     return -1;
@@ -106,33 +115,28 @@ extern "C" int lik_host(const oc_level_desc* lv, int A, int K, const uint8_t* si
 extern "C" int roll_host(const oc_level_desc* lv, int A, int K, const uint8_t* sin, uint8_t* sout, const uint8_t* act,
                          const uint8_t* alloc, const oc_subtask* subs, int nsub, uint8_t* flags, float* lb, int64_t B,
                          int64_t P) {
-#define R_(a, k) \
-    if (A == a && K == k) { run<a, k>(lv, sin, sout, act, alloc, subs, nsub, flags, lb, B, P); return 0; }
+    const bool wide = lv->width * lv->height > OC_MAX_NARROW_CELLS;
+#define R_(a, k)                                                                                 \
+    if (A == a && K == k) {                                                                     \
+        if (wide) run<a, k, true>(lv, sin, sout, act, alloc, subs, nsub, flags, lb, B, P);     \
+        else run<a, k, false>(lv, sin, sout, act, alloc, subs, nsub, flags, lb, B, P);         \
+        return 0;                                                                               \
+    }
     R_(1, 4) R_(2, 4) R_(3, 4) R_(4, 4) R_(1, 8) R_(2, 8) R_(3, 8) R_(4, 8) R_(1, 16) R_(2, 16) R_(3, 16) R_(4, 16)
 #undef R_
     return -1;
 }
 
 // oc_bounds_kernel's loop: every env x every configuration, [subtask][pitch] outputs
-template <int A, int K>
+template <int A, int K, bool W>
 static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask* subs, int nsub, float* lb,
                    uint8_t* doable, int64_t B, int64_t P) {
     static uint8_t blob[ocro::kBlobMax];
     ocro::RollLevel L;
     if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
-    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
     for (int64_t e = 0; e < B; ++e) {
-        ocro::RowT<K> r;
-        for (int a = 0; a < A; ++a) {
-            r.x |= (uint32_t)sin[a * P + e] << (8 * a);
-            r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
-            r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
-        }
-        for (int j = 0; j < K; ++j) {
-            r.loc[j >> 3] |= (uint64_t)sin[(kPL + j) * P + e] << (8 * (j & 7));
-            r.mask[j >> 3] |= (uint64_t)sin[(kPM + j) * P + e] << (8 * (j & 7));
-        }
-        ocro::RowOps<A, K> ops(L, blob);
+        const ocro::RowT<K, W> r = load<A, K, W>(sin, P, e);
+        ocro::RowOps<A, K, W> ops(L, blob);
         for (int i = 0; i < nsub; ++i) {
             const oc_subtask& o = subs[i];
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
@@ -146,8 +150,13 @@ static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask
 
 extern "C" int bounds_host(const oc_level_desc* lv, int A, int K, const uint8_t* sin, const oc_subtask* subs, int nsub,
                            float* lb, uint8_t* doable, int64_t B, int64_t P) {
-#define B_(a, k) \
-    if (A == a && K == k) { bounds<a, k>(lv, sin, subs, nsub, lb, doable, B, P); return 0; }
+    const bool wide = lv->width * lv->height > OC_MAX_NARROW_CELLS;
+#define B_(a, k)                                                                          \
+    if (A == a && K == k) {                                                              \
+        if (wide) bounds<a, k, true>(lv, sin, subs, nsub, lb, doable, B, P);             \
+        else bounds<a, k, false>(lv, sin, subs, nsub, lb, doable, B, P);                 \
+        return 0;                                                                        \
+    }
     B_(1, 4) B_(2, 4) B_(3, 4) B_(4, 4) B_(1, 8) B_(2, 8) B_(3, 8) B_(4, 8) B_(1, 16) B_(2, 16) B_(3, 16) B_(4, 16)
 #undef B_
     return -1;

@@ -50,7 +50,7 @@ def test_level_files_match_reference_loader(name):
 
 def test_big_levels_reach_cell_ids_past_127():
     lv = levels.load_level(_path("big-15x17_salad"))
-    assert lv.ncells == 255 == levels.MAX_CELLS
+    assert lv.ncells == 255 == levels.MAX_NARROW_CELLS  # the largest byte-cell (narrow) level
     lv.validate(4)
     assert max(c for c, _ in lv.items) > 127
 
@@ -136,9 +136,15 @@ def test_ragged_long_map_loads_and_step_raises_indexerror():
     lv.within_width().validate(2)
 
 
-def test_grid_past_255_cells_is_refused():
+def test_grid_past_1024_cells_is_refused():
+    """256 cells and more take the wide layout (tests/test_widelevels.py); the engine stops at
+    OC_MAX_CELLS = 1,024 cells (and sides of 255: coordinates are bytes)."""
     rows = ["-" * 16] + ["/" + " " * 14 + "-"] * 14 + ["--*-----tl---pp-"]
-    lv = levels.parse_level_text("\n".join(rows) + "\n\nSalad\n\n2 1\n4 1\n", "too-big")
+    lv = levels.parse_level_text("\n".join(rows) + "\n\nSalad\n\n2 1\n4 1\n", "wide-256")
     assert lv.ncells == 256
+    lv.validate(2)
+    rows = ["-" * 33] + ["/" + " " * 31 + "-"] * 30 + ["--*-----tl---pp" + "-" * 18]
+    lv = levels.parse_level_text("\n".join(rows) + "\n\nSalad\n\n2 1\n4 1\n", "too-big")
+    assert lv.ncells == 33 * 32 > levels.MAX_CELLS
     with pytest.raises(ValueError, match="cells"):
         lv.validate(2)

@@ -24,8 +24,9 @@ class OracleExpander:
     def __init__(self, level, num_agents, device):
         self.ob = oracle.OracleBatch(level, num_agents, 0, self.ROWS)
         self.A, self.K = num_agents, self.ob.K
-        self.enc = (levels.load_level(level) if isinstance(level, str) else level).encoding
-        P = capi.layout_planes(num_agents, self.K)
+        lv = levels.load_level(level) if isinstance(level, str) else level
+        self.enc, self.wide = lv.encoding, capi.is_wide(lv)
+        P = capi.layout_planes(num_agents, self.K, self.wide)
         self.NP, self.t_plane, self.P = P["num_planes"], P["t"], self.ob.pitch
         self.launches = 0
 

@@ -1,0 +1,224 @@
+"""Kitchens of more than 255 cells on the GPU, through the C-ABI (the wide layout: u16 item
+cells; fixtures from tests/golden/gen_widelevels.py, which runs the reference on the same level
+files).  oc_step replays the recorded episodes; oc_step_n (the scalar wide kernel) against the
+CPU oracle on every step's outputs, the in-launch totals and the checksum; oc_reset against the
+template; oc_subtask_bounds and oc_rollout against the reference's rows; rollout, bounds and
+likelihood rows against the oracle on random states; the gym shim replays the episodes; the
+navigation planner over oc_rollout decides as the same search over the oracle's rows; the
+renderer refuses these levels (OC_ELEVEL)."""
+import os
+import types
+
+import numpy as np
+import pytest
+
+import oc_testlib as tl
+import test_rollout_host as th
+import test_widelevels as tw
+from gym_cooking_amd import capi, levels
+
+from oracle import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _batch(level, A, B, max_T=100):
+    from gym_cooking_amd.engine import OvercookedBatch
+    return OvercookedBatch(level, A, B, max_T=max_T, device="cuda:0")
+
+
+def test_engine_replays_wide_level_episodes():
+    import test_gpu_parity as tg
+    fx = tl.load_fixture("widelevels.npz")
+    n = 0
+    for g in tl.episode_groups(fx):
+        eb = _batch(g.level, g.A, g.B, g.max_T)
+        assert eb.layout.cell_bytes == 2
+        s = eb.new_state()
+        eb.reset(s)
+        host = s.cpu().numpy()
+        g.relocate(host, eb.pitch)
+        errs = tl.compare_group(g, tg._gpu_step_fn(eb), host, eb.pitch, g.level.width)
+        assert not errs, "%s A=%d: %s" % (g.level.name, g.A, "\n".join(errs[:10]))
+        n += g.B
+    assert n == len(fx["ep_T"])
+
+
+@pytest.mark.parametrize("name", tw.WIDE)
+@pytest.mark.parametrize("A", [1, 2, 3, 4])
+def test_wide_level_step_n_matches_oracle(name, A):
+    """Two 33-step oc_step_n launches over 20,003 envs (max_T 27), every step's outputs, the
+    in-launch totals, the final state's checksum."""
+    B, n, max_T, seed = 20003, 33, 27, 91 + A
+    lv = levels.load_level(tw._path(name))
+    eb = _batch(lv, A, B, max_T)
+    ob = oracle.OracleBatch(lv, A, max_T, B)
+    P, S = eb.pitch, eb.layout.state_bytes
+    s_in, s_out = eb.new_state(), eb.new_state()
+    eb.reset(s_in)
+    c, c2 = ob.new_state(), ob.new_state()
+    ob.reset(c)
+    assert np.array_equal(tl.env_view(s_in.cpu().numpy(), A, ob.K, P, B), tl.env_view(c, A, ob.K, P, B))
+    ca, cex, ccoll = ob.new_actions(), np.zeros(A * P, np.uint8), np.zeros(P, np.uint8)
+    acts = torch.empty((n, A * P), dtype=torch.uint8, device="cuda:0")
+    traj = torch.empty(n * S, dtype=torch.uint8, device="cuda:0")
+    ex = torch.empty(n * A * P, dtype=torch.uint8, device="cuda:0")
+    coll = torch.empty(n * P, dtype=torch.uint8, device="cuda:0")
+    stats, totals = eb.new_stats(), torch.zeros(5, dtype=torch.int64, device="cuda:0")
+    tot = np.zeros(5, np.int64)
+    for launch in range(2):
+        for r in range(n):
+            eb.gen_actions(acts[r], launch * n + r, seed)
+        eb.step_n(s_in, s_out, acts.reshape(-1), n, traj, ex, coll, stats, totals)
+        tr, exh, colh = traj.view(n, S).cpu().numpy(), ex.view(n, A, P).cpu().numpy(), coll.view(n, P).cpu().numpy()
+        for r in range(n):
+            ob.gen_actions(ca, 0, launch * n + r, seed)
+            fl_in = tl.planes_view(c, A, ob.K, P)["fl"].copy()
+            ob.step(c, c2, ca, cex, ccoll, nthreads=16)
+            c, c2 = c2, c
+            tot += tl.window_totals(fl_in, c, ccoll, A, ob.K, P, B)
+            g, o = tl.env_view(tr[r], A, ob.K, P, B), tl.env_view(c, A, ob.K, P, B)
+            assert np.array_equal(g, o), (launch, r, np.argwhere(g != o)[:5].tolist())
+            assert np.array_equal(exh[r][:, :B], cex.reshape(A, P)[:, :B]), (launch, r)
+            assert np.array_equal(colh[r][:B], ccoll[:B]), (launch, r)
+        assert np.array_equal(totals.cpu().numpy(), tot), launch
+        s_in, s_out = s_out, s_in
+    host = s_in.cpu().numpy()
+    assert np.array_equal(tl.env_view(host, A, ob.K, P, B), tl.env_view(c, A, ob.K, P, B))
+    assert int(eb.checksum(s_in).item()) & (2**64 - 1) == tl.checksum(host, A, ob.K, P, B)
+    assert np.array_equal(eb.reduce_stats(stats).cpu().numpy(), tot)
+    assert tot[0] >= B
+
+
+@pytest.mark.parametrize("cfg", range(2))
+def test_wide_level_bounds_match_reference_rows(cfg):
+    rows = tl.BoundRows(tl.load_fixture("bounds_wide.npz"), cfg)
+    P = capi.pitch_for(rows.B)
+    s = rows.state(P)
+    eb = _batch(rows.level, rows.A, rows.B)
+    for c0 in range(0, len(rows.subtasks), capi.MAX_SUBTASKS):
+        subs = rows.subtasks[c0:c0 + capi.MAX_SUBTASKS]
+        lb, ok = eb.subtask_bounds(torch.from_numpy(s).cuda(), subs)
+        errs = rows.compare(lb[:, :rows.B].cpu().numpy(), ok[:, :rows.B].cpu().numpy(), sub0=c0)
+        assert not errs, "\n".join(errs[:20])
+
+
+@pytest.mark.parametrize("cfg", range(2))
+def test_wide_level_rollout_matches_reference_rows(cfg):
+    fx = tl.load_fixture("rollout_wide.npz")
+    n = 0
+    for rows in tl.RolloutRows(fx, cfg).split(capi.MAX_SUBTASKS):
+        P = capi.pitch_for(rows.B)
+        sin = tl.state_from_canonical(rows.level, rows.A, rows.K, P, rows.agents, rows.items, rows.t)
+        alloc = np.zeros(P, np.uint8)
+        alloc[:rows.B] = rows.alloc
+        eb = _batch(rows.level, rows.A, rows.B)
+        sout = eb.new_state()
+        fl, lb = eb.rollout(torch.from_numpy(sin).cuda(), sout, torch.from_numpy(rows.actions(P)).cuda(),
+                            rows.subtasks, torch.from_numpy(alloc).cuda())
+        errs = rows.compare(sout.cpu().numpy(), fl[:rows.B].cpu().numpy(), lb[:rows.B].cpu().numpy(), P)
+        assert not errs, "\n".join(errs[:20])
+        n += rows.B
+    assert n == int((fx["cfg"] == cfg).sum())
+
+
+@pytest.mark.parametrize("name", tw.WIDE)
+@pytest.mark.parametrize("A", [2, 4])
+def test_wide_level_rows_match_oracle_random(name, A):
+    B = 6000
+    ob, s, acts, subs, alloc = th.random_rollout_case(tw._path(name), A, B, seed=B + A, planner_levels=(0, 1))
+    eb = _batch(ob.level, A, B)
+    o_out = ob.new_state()
+    o_fl, o_lb = ob.rollout(s, o_out, acts, subs, alloc, nthreads=16)
+    g_out = eb.new_state()
+    g_fl, g_lb = eb.rollout(torch.from_numpy(s).cuda(), g_out, torch.from_numpy(acts).cuda(), subs,
+                            torch.from_numpy(alloc).cuda())
+    assert np.array_equal(o_fl, g_fl[:B].cpu().numpy())
+    assert np.array_equal(o_lb, g_lb[:B].cpu().numpy())
+    assert np.array_equal(tl.env_view(o_out, A, ob.K, ob.pitch, B),
+                          tl.env_view(g_out.cpu().numpy(), A, ob.K, ob.pitch, B))
+    subs0 = [capi.subtask(x.kind, list(x.agent[:x.num_agents]), list(x.start_mask), x.goal_mask, x.goal_count, 0)
+             for x in subs]
+    o_b, o_ok = ob.subtask_bounds(s, subs0, nthreads=16)
+    g_b, g_ok = eb.subtask_bounds(torch.from_numpy(s).cuda(), subs0)
+    assert np.array_equal(o_b, g_b[:, :B].cpu().numpy()) and np.array_equal(o_ok, g_ok[:, :B].cpu().numpy())
+    o_v, o_f = ob.nav_likelihood(s, acts, subs0, alloc, 0, 1.3, 0.5, nthreads=16)
+    g_v, g_f = eb.nav_likelihood(torch.from_numpy(s).cuda(), torch.from_numpy(acts).cuda(), subs0, 0, 1.3, 0.5,
+                                 torch.from_numpy(alloc).cuda())
+    g_v, g_f = g_v[:B].cpu().numpy(), g_f[:B].cpu().numpy()
+    assert np.array_equal(o_f, g_f)
+    ok = o_f == capi.LIK_OK
+    assert ok.sum() > 50
+    np.testing.assert_allclose(g_v[ok], o_v[ok], rtol=1e-12)
+
+
+def test_shim_replays_wide_level_episodes():
+    """The gym shim (OvercookedEnvironment over the engine) steps the recorded episodes and
+    reproduces every recorded state."""
+    from gym_cooking_amd.envs import OvercookedEnvironment
+    fx = tl.load_fixture("widelevels.npz")
+    checked = 0
+    for e in range(0, len(fx["ep_T"]), 3):
+        A = int(fx["ep_A"][e])
+        arg = types.SimpleNamespace(level=os.path.join(tl.GOLDEN, str(fx["level_names"][fx["ep_level"][e]])),
+                                    num_agents=A, max_num_timesteps=int(fx["ep_maxT"][e]), seed=1, model1=None,
+                                    model2=None, model3=None, model4=None, record=False, with_image_obs=False)
+        env = OvercookedEnvironment(arg)
+        env.reset()
+        off, aoff = int(fx["ep_state_off"][e]), int(fx["ep_act_off"][e])
+        for step in range(int(fx["ep_T"][e])):
+            codes = fx["act"][aoff + step][:A]
+            ad = {"agent-%d" % (a + 1): levels.ACTIONS[min(int(codes[a]), 4)] for a in range(A)}
+            nxt = off + step + 1
+            if fx["flags"][nxt] & 4:
+                break
+            _, reward, done, _ = env.step(ad)
+            for a, ag in enumerate(env.sim_agents):
+                assert tuple(ag.location) == tuple(int(v) for v in fx["agents"][nxt][a][:2]), (e, step, a)
+            assert env.t == int(fx["t"][nxt]) and bool(done) == bool(fx["flags"][nxt] & 1), (e, step)
+            assert reward == int(bool(fx["flags"][nxt] & 2))
+            checked += 1
+            if done:
+                break
+    assert checked > 500
+
+
+def test_wide_level_render_refused():
+    lv = levels.load_level(tw._path("wide-17x17_salad"))
+    eb = _batch(lv, 2, 8)
+    from gym_cooking_amd.render import Renderer
+    with pytest.raises(capi.LevelError):
+        Renderer(eb).render(eb.reset(eb.new_state()))
+
+
+@pytest.mark.parametrize("name,A,sub,agents", [("wide-17x17_salad", 2, ("Chop", "Tomato"), ("agent-1",)),
+                                                ("wide-23x13_tl", 3, ("Chop", "Lettuce"), ("agent-2",)),
+                                                ("wide-17x17_salad", 2, ("Chop", "Lettuce"), ("agent-1", "agent-2"))])
+def test_wide_level_planner_matches_host_search(name, A, sub, agents):
+    """The navigation planner on a wide kitchen: get_next_action over oc_rollout equals the
+    same search over the CPU oracle's rollout rows (tests/test_planner_host.py's expander),
+    which test_widelevels.py pins to the reference planner's own rows on these kitchens."""
+    import test_planner_host as tp
+    from gym_cooking_amd import recipes
+    from gym_cooking_amd.planner import E2E_BRTDP, PlanEnv
+    lv = levels.load_level(tw._path(name))
+    ob = oracle.OracleBatch(lv, A, 0, 1)
+    s, s2 = ob.new_state(), ob.new_state()
+    ob.reset(s)
+    act = ob.new_actions()
+    for t in range(9):
+        ob.gen_actions(act, 0, t, 5)
+        ob.step(s, s2, act)
+        s, s2 = s2, s
+    view = tl.env_view(s, A, ob.K, ob.pitch, 1)[:, 0]
+    names = sorted({n for n in ("Tomato", "Lettuce", "Plate", "Onion")
+                    if any(m & {"Tomato": 1, "Lettuce": 2, "Onion": 4, "Plate": 8}[n] for _, m in lv.items)})
+    out = []
+    for exp in (None, tp.OracleExpander):
+        env = PlanEnv(lv, A, view, names, device="cuda:0")
+        kw = {} if exp is None else {"expander": exp}
+        p = E2E_BRTDP(alpha=0.01, tau=2, cap=75, main_cap=100, device="cuda:0", rng=np.random.RandomState(3), **kw)
+        a = p.get_next_action(env, getattr(recipes, sub[0])(sub[1]), agents, {})
+        out.append((a, p.cur_obj_count, len(p.v_l), p.v_l[(p._repr(p.start), p._sub_key)]))
+    assert out[0] == out[1], out

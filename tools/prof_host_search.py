@@ -28,10 +28,10 @@ class BatchOracleExpander:
 
     def __init__(self, level, num_agents, device):
         self.level = levels.load_level(level) if isinstance(level, str) else level
-        self.A, self.enc = num_agents, self.level.encoding
+        self.A, self.enc, self.wide = num_agents, self.level.encoding, capi.is_wide(self.level)
         self.ob = oracle.OracleBatch(self.level, num_agents, 0, 4096)
         self.K = self.ob.K
-        P = capi.layout_planes(num_agents, self.K)
+        P = capi.layout_planes(num_agents, self.K, self.wide)
         self.NP, self.t_plane = P["num_planes"], P["t"]
         self.launches = self.rows_done = 0
         self._obs = {}
