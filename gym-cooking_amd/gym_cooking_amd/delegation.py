@@ -33,7 +33,6 @@ from collections import namedtuple
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
-import scipy.special
 
 from . import capi
 from . import recipes as _recipes
@@ -87,6 +86,14 @@ class SubtaskAllocDistribution:
 
 
 _CODE = {a: i for i, a in enumerate(_levels.ACTIONS)}
+
+
+def _softmax_at(x: np.ndarray, i: int):
+    """scipy.special.softmax(x)[i] for a 1-D float64 x (scipy 1.15 _logsumexp.py:250: x - amax,
+    exp, divided by the pairwise np.sum of the exponentials): the same numpy operations on the
+    same array, so the same double, without scipy's per-call argument handling."""
+    e = np.exp(x - np.amax(x))
+    return e[i] / np.sum(e)
 
 
 class BayesianDelegator:
@@ -182,7 +189,7 @@ class BayesianDelegator:
 
     def prob_nav_actions(self, obs_tm1, actions_tm1, subtask, subtask_agent_names, beta, no_level_1) -> float:
         """:461-689.  Q values, legal actions and the None branch's action count come from
-        engine rollout rows; the softmax is scipy's, as the reference's."""
+        engine rollout rows; the softmax is scipy's, as the reference's (_softmax_at)."""
         self._expander(obs_tm1)
         return self.planner._drive(self._prob_nav_actions_gen(obs_tm1, actions_tm1, subtask, subtask_agent_names,
                                                               beta, no_level_1))
@@ -199,10 +206,7 @@ class BayesianDelegator:
             num_actions = int(sum(1 for f in fl if f & capi.ROLL_LEGAL))
             action_prob = (1.0 - self.none_action_prob) / (num_actions)
             diffs = [self.none_action_prob] + [action_prob] * num_actions
-            softmax_diffs = scipy.special.softmax(beta * np.asarray(diffs))
-            if tuple(actions_tm1[subtask_agent_names[0]]) == (0, 0):
-                return softmax_diffs[0]
-            return softmax_diffs[1]
+            return _softmax_at(beta * np.asarray(diffs), 0 if tuple(actions_tm1[subtask_agent_names[0]]) == (0, 0) else 1)
         action = tuple(_CODE[tuple(actions_tm1[a_name])] for a_name in subtask_agent_names)
         state, other_planners = yield from self._state_and_other_planners_gen(
             obs_tm1=obs_tm1, backup_subtask=subtask, no_level_1=no_level_1)
@@ -213,19 +217,16 @@ class BayesianDelegator:
         err = yield from p._taken_action_error_gen(p.start, action)  # Q(state, taken) and the assert below raise
         if err is not None:
             raise err("valid_nav_actions do not hold the taken action {}".format(action))
-        old_q = yield from p._Q_gen(p.start, action, p.v_l)
+        old_q = (yield from p._Q_seq_gen(p.start, (action,), p.v_l))[0]
         yield from p._need(p.start)
         valid_nav_actions = p._succ[(p.start, p._sub_key)][0]  # get_actions(state)
         assert action in valid_nav_actions, "valid_nav_actions: {}\naction: {}".format(valid_nav_actions, action)
         if len(subtask_agent_names) == 2 and self.agent_name in subtask_agent_names:
             other_index = 1 - subtask_agent_names.index(self.agent_name)
             valid_nav_actions = list(filter(lambda x: x[other_index] == action[other_index], valid_nav_actions))
-        qdiffs = []
-        for nav_action in valid_nav_actions:
-            q = yield from p._Q_gen(p.start, nav_action, p.v_l)
-            qdiffs.append(old_q - q)
-        softmax_diffs = scipy.special.softmax(beta * np.asarray(qdiffs))
-        return softmax_diffs[valid_nav_actions.index(action)]
+        qs = yield from p._Q_seq_gen(p.start, valid_nav_actions, p.v_l)
+        qdiffs = [old_q - q for q in qs]
+        return _softmax_at(beta * np.asarray(qdiffs), valid_nav_actions.index(action))
 
     def _doability_pairs(self) -> list:
         return [(t.subtask, tuple(t.subtask_agent_names)) for a in self.probs.enumerate_subtask_allocs() for t in a]

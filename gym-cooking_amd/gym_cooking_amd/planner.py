@@ -407,17 +407,23 @@ class E2E_BRTDP:
         those, kept per expander (many planners set up on the same states: the delegators'
         other-agent planners at every state a Level-1 search visits)."""
         exp = self._exp
-        names = _agent_names(A)
         self.subtask = subtask
-        self.subtask_agent_names = tuple(subtask_agent_names)
-        self.is_joint = len(subtask_agent_names) == 2
-        agents = tuple(names.index(n) for n in subtask_agent_names)
-        assert list(agents) == sorted(agents), "subtask agent names are not in order"
+        san = self.subtask_agent_names = tuple(subtask_agent_names)
+        self.is_joint = len(san) == 2
+        agents = _AGENT_IX.get((A, san))
+        if agents is None:
+            names = _agent_names(A)
+            agents = tuple(names.index(n) for n in san)
+            assert list(agents) == sorted(agents), "subtask agent names are not in order"
+            _AGENT_IX[(A, san)] = agents
         self._agents = list(agents)
         sk = str(subtask)
         self._sub_key = sk
         ck = (full, self._level, agents, sk)
-        hit = exp.__dict__.setdefault("_conf_cache", {}).get(ck)
+        cache = exp.__dict__.get("_conf_cache")
+        if cache is None:
+            cache = exp.__dict__["_conf_cache"] = {}
+        hit = cache.get(ck)
         if hit is None:
             kind, starts, goal = _recipes.subtask_masks(subtask, exp.enc)
             self._kind, self._goal_mask = kind, goal  # _obj_count reads them
@@ -439,7 +445,7 @@ class E2E_BRTDP:
         self._dev = dev
         self.start = self._key(start, groups)
         # the start state: a no-op row gives its goal flag and lower bound
-        return (start, [(_NOOP,) * len(agents)], self._sub)
+        return (start, _NOOP_ROW[len(agents)], self._sub)
 
     def _configured(self, res) -> None:
         _, fl, lb = res
@@ -696,6 +702,42 @@ class E2E_BRTDP:
         expected_value = 1.0 * value_f[(self._repr(nk), self._sub_key)]
         return float(cost + expected_value)
 
+    def _Q_seq_gen(self, key, actions, value_f):
+        """[Q(key, a, value_f) for a in actions], evaluated in order with the side effects of
+        as many _Q_gen calls (T's memo, value_init, the copy-crash raise), as one generator:
+        the belief update's Q passes (bayesian_delegator.py:657-689) without a generator pair
+        per action."""
+        out = []
+        sk = self._sub_key
+        rk = self._repr(key)
+        tmemo, v_l, v_u, succ = self._tmemo, self.v_l, self.v_u, self._succ
+        agents, lvl = tuple(self._agents), self._level
+        for action in actions:
+            cost = self.cost(action)
+            hit = tmemo.get((rk, action))
+            if hit is not None:  # _T_gen's memo path
+                if lvl and _copy_crashes(hit[0], self._exp.A):
+                    _raise_copy_crash(action)
+                nk = (hit[0], hit[1], agents, lvl)
+                vk = (self._repr(nk), sk)
+                if vk not in v_l or vk not in v_u:
+                    _, fl, lb = yield (np.frombuffer(hit[0], np.uint8), [(_NOOP,) * len(agents)], self._sub)
+                    self._value_init(nk, bool(fl[0] & capi.ROLL_GOAL), float(lb[0]))
+            else:
+                if (key, sk) not in succ:
+                    yield from self._need(key)
+                got = succ[(key, sk)]
+                i = got[0].index(action)
+                if got[7] and i in got[7]:
+                    _raise_copy_crash(action)
+                if not got[6]:
+                    self._value_init(got[1][i], got[4][i], got[5][i])
+                nk = got[1][i]
+                if len(tmemo) < 10000:  # lru_cache(maxsize=10000)
+                    tmemo[(rk, action)] = (nk[0], nk[1])
+            out.append(float(cost + 1.0 * value_f[(self._repr(nk), sk)]))
+        return out
+
     def _q_all(self, key, value_f) -> List[float]:
         """[Q(key, a, value_f) for a in get_actions(key)] in one pass (same float64 ops);
         `key` must be expanded."""
@@ -937,6 +979,10 @@ class PlanEnv:
 
 
 _AGENT_NAMES: Dict[int, List[str]] = {}
+
+
+_AGENT_IX: Dict[tuple, tuple] = {}  # (A, subtask agent names) -> their indices
+_NOOP_ROW = {1: [(_NOOP,)], 2: [(_NOOP, _NOOP)]}  # the one candidate of a set-up's no-op row
 
 
 def _agent_names(A: int) -> List[str]:

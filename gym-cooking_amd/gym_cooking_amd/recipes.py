@@ -66,7 +66,10 @@ class Subtask:
         raise NotImplementedError
 
     def __str__(self):
-        return "{}({})".format(self.name, ", ".join(self.args))
+        s = self.__dict__.get("_str")  # name and args do not change: built once (the planners key tables by it)
+        if s is None:
+            s = self.__dict__["_str"] = "{}({})".format(self.name, ", ".join(self.args))
+        return s
 
     __repr__ = __str__
 
