@@ -13,11 +13,17 @@
  * An expanded state's entry (planner.E2E_BRTDP._expanded) is a list:
  *   [0] actions  [1] successor keys  [2] costs (floats)  [3] successor value keys
  *   [4] goal flags  [5] bounds  [6] successors initialised (bool)  [7] copy-crash action
- *   indices (set or None)  [8] this state's value key
+ *   indices (set or None)  [8] this state's value key  [9] (entries built by expand) the
+ *   hashes of [3]'s keys, of [8] and of the successors' (state key, subtask) _succ keys, as a
+ *   bytes of 2n+1 Py_hash_t -- the loops below look values up with them instead of hashing a
+ *   nested tuple per lookup (the dicts are the same; a hash is a pure function of the key).
+ * expand interns the value keys it builds in the planner's key table, so that the keys stored
+ * in v_l / v_u and the ones looked up are mostly one object (a dict compares those by identity).
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <math.h>
+#include <string.h>
 
 /* v[k] as a double; NULL (with KeyError set) when absent */
 static int get_val(PyObject* d, PyObject* k, double* out) {
@@ -37,6 +43,49 @@ static int set_val(PyObject* d, PyObject* k, double x) {
     int r = PyDict_SetItem(d, k, f);
     Py_DECREF(f);
     return r;
+}
+
+/* hash i of an entry's hash table (NULL: none) */
+static inline Py_hash_t hash_at(const char* h, Py_ssize_t i) {
+    Py_hash_t v;
+    memcpy(&v, h + (size_t)i * sizeof(Py_hash_t), sizeof v);
+    return v;
+}
+
+/* An entry's precomputed hashes ([9], see above) for its n successors, or NULL for an entry
+ * built in Python (planner._expanded). */
+static const char* entry_hashes(PyObject* got, Py_ssize_t n) {
+    if (PyList_GET_SIZE(got) < 10) return NULL;
+    PyObject* h = PyList_GET_ITEM(got, 9);
+    if (!PyBytes_Check(h) || PyBytes_GET_SIZE(h) != (Py_ssize_t)sizeof(Py_hash_t) * (2 * n + 1)) return NULL;
+    return PyBytes_AS_STRING(h);
+}
+
+/* get_val / set_val with the key's hash known (h = NULL: hash it) */
+static int get_val_h(PyObject* d, PyObject* k, const char* h, Py_ssize_t i, double* out) {
+    if (h == NULL) return get_val(d, k, out);
+    PyObject* v = _PyDict_GetItem_KnownHash(d, k, hash_at(h, i));
+    if (v == NULL) {
+        if (!PyErr_Occurred()) PyErr_SetObject(PyExc_KeyError, k);
+        return -1;
+    }
+    *out = PyFloat_AsDouble(v);
+    if (*out == -1.0 && PyErr_Occurred()) return -1;
+    return 0;
+}
+
+static int set_val_h(PyObject* d, PyObject* k, const char* h, Py_ssize_t i, double x) {
+    if (h == NULL) return set_val(d, k, x);
+    PyObject* f = PyFloat_FromDouble(x);
+    if (f == NULL) return -1;
+    int r = _PyDict_SetItem_KnownHash(d, k, f, hash_at(h, i));
+    Py_DECREF(f);
+    return r;
+}
+
+/* k in d, with the hash known (h = NULL: hash it); -1 on error */
+static int has_key_h(PyObject* d, PyObject* k, const char* h, Py_ssize_t i) {
+    return h == NULL ? PyDict_Contains(d, k) : _PyDict_Contains_KnownHash(d, k, hash_at(h, i));
 }
 
 /* One uniform double from the tie-break generator (RandomState.random_sample: MT19937's
@@ -123,7 +172,7 @@ static PyObject* tie_pick(PyObject* self, PyObject* args) {
 }
 
 /* min over i of costs[i] + v[vks[i]] (the first minimum), into *out; -1 on error */
-static int min_q(PyObject* costs, PyObject* vks, PyObject* v, double* out) {
+static int min_q(PyObject* costs, PyObject* vks, const char* hs, PyObject* v, double* out) {
     const Py_ssize_t n = PyList_GET_SIZE(costs);
     double m = 0.0;
     if (n == 0) {  /* Python's min() of an empty sequence */
@@ -133,7 +182,7 @@ static int min_q(PyObject* costs, PyObject* vks, PyObject* v, double* out) {
     for (Py_ssize_t i = 0; i < n; ++i) {
         double c = PyFloat_AsDouble(PyList_GET_ITEM(costs, i)), x;
         if (c == -1.0 && PyErr_Occurred()) return -1;
-        if (get_val(v, PyList_GET_ITEM(vks, i), &x) < 0) return -1;
+        if (get_val_h(v, PyList_GET_ITEM(vks, i), hs, i, &x) < 0) return -1;
         const double q = c + x;
         if (i == 0 || q < m) m = q;
     }
@@ -141,49 +190,115 @@ static int min_q(PyObject* costs, PyObject* vks, PyObject* v, double* out) {
     return 0;
 }
 
-/* backprop(succ, v_u, v_l, traj, sk): the trial's backward pass (e2e_brtdp.py:320-331):
- * pop every state of traj and set both of its values to the min over its actions. */
-static PyObject* backprop(PyObject* self, PyObject* args) {
-    PyObject *succ, *v_u, *v_l, *traj, *sk;
-    if (!PyArg_ParseTuple(args, "O!O!O!O!O", &PyDict_Type, &succ, &PyDict_Type, &v_u, &PyDict_Type, &v_l,
-                          &PyList_Type, &traj, &sk))
-        return NULL;
-    for (Py_ssize_t t = PyList_GET_SIZE(traj) - 1; t >= 0; --t) {
-        PyObject* key = PyTuple_Pack(2, PyList_GET_ITEM(traj, t), sk);
-        if (key == NULL) return NULL;
-        PyObject* got = PyDict_GetItemWithError(succ, key);
-        Py_DECREF(key);
-        if (got == NULL) {
-            if (!PyErr_Occurred()) PyErr_SetString(PyExc_KeyError, "backprop: state not expanded");
-            return NULL;
+/* value_init of every successor of an entry, in action order (planner.E2E_BRTDP._init_succ
+ * past its copy-crash check; e2e_brtdp.py:678-729 through T): a key already in both tables is
+ * kept; a goal gets 0.0 / 0.0; else lower = bound * tc must be > 0 (AssertionError "lower: x"
+ * as the reference's assert, after the inserts before it), v_l = lower - 1.09,
+ * v_u = lower * 5 * tc.  Sets the entry's initialised flag. */
+static int init_entry(PyObject* got, PyObject* v_l, PyObject* v_u, double tc) {
+    PyObject *vks = PyList_GET_ITEM(got, 3), *goals = PyList_GET_ITEM(got, 4), *lbs = PyList_GET_ITEM(got, 5);
+    const Py_ssize_t n = PyList_GET_SIZE(vks);
+    const char* hs = entry_hashes(got, n);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject* vk = PyList_GET_ITEM(vks, i);
+        const int il = has_key_h(v_l, vk, hs, i);
+        if (il < 0) return -1;
+        if (il) {
+            const int iu = has_key_h(v_u, vk, hs, i);
+            if (iu < 0) return -1;
+            if (iu) continue;
         }
-        PyObject *costs = PyList_GET_ITEM(got, 2), *vks = PyList_GET_ITEM(got, 3), *rx = PyList_GET_ITEM(got, 8);
-        double mu, ml;
-        if (min_q(costs, vks, v_u, &mu) < 0 || set_val(v_u, rx, mu) < 0) return NULL;
-        if (min_q(costs, vks, v_l, &ml) < 0 || set_val(v_l, rx, ml) < 0) return NULL;
+        const int g = PyObject_IsTrue(PyList_GET_ITEM(goals, i));
+        if (g < 0) return -1;
+        if (g) {
+            if (set_val_h(v_l, vk, hs, i, 0.0) < 0 || set_val_h(v_u, vk, hs, i, 0.0) < 0) return -1;
+            continue;
+        }
+        const double lb = PyFloat_AsDouble(PyList_GET_ITEM(lbs, i));
+        if (lb == -1.0 && PyErr_Occurred()) return -1;
+        const double lower = lb * tc;
+        if (!(lower > 0)) {
+            PyObject* f = PyFloat_FromDouble(lower);
+            if (f != NULL) {
+                PyErr_Format(PyExc_AssertionError, "lower: %R", f);
+                Py_DECREF(f);
+            }
+            return -1;
+        }
+        if (set_val_h(v_l, vk, hs, i, lower - 1.09) < 0 || set_val_h(v_u, vk, hs, i, lower * 5 * tc) < 0) return -1;
     }
-    if (PyList_SetSlice(traj, 0, PyList_GET_SIZE(traj), NULL) < 0) return NULL;
+    Py_INCREF(Py_True);
+    PyList_SetItem(got, 6, Py_True);  /* steals; drops the old flag */
+    return 0;
+}
+
+/* init_succ(entry, v_l, v_u, tc): init_entry for Python (_init_succ after its crash check) */
+static PyObject* init_succ(PyObject* self, PyObject* args) {
+    PyObject *got, *v_l, *v_u;
+    double tc;
+    if (!PyArg_ParseTuple(args, "O!O!O!d", &PyList_Type, &got, &PyDict_Type, &v_l, &PyDict_Type, &v_u, &tc))
+        return NULL;
+    if (PyList_GET_SIZE(got) < 9) {
+        PyErr_SetString(PyExc_ValueError, "init_succ: not a _succ entry");
+        return NULL;
+    }
+    if (init_entry(got, v_l, v_u, tc) < 0) return NULL;
     Py_RETURN_NONE;
 }
 
-/* forward(succ, v_u, v_l, x, sk, rs, cap, counter, tau, traj, sample, resume)
+/* backprop(v_u, v_l, traj, entries): the trial's backward pass (e2e_brtdp.py:320-331): pop
+ * every state of traj and set both of its values to the min over its actions.  entries[t] is
+ * traj[t]'s _succ entry (forward collects them), so no state is looked up again. */
+static PyObject* backprop(PyObject* self, PyObject* args) {
+    PyObject *v_u, *v_l, *traj, *ents;
+    if (!PyArg_ParseTuple(args, "O!O!O!O!", &PyDict_Type, &v_u, &PyDict_Type, &v_l, &PyList_Type, &traj, &PyList_Type,
+                          &ents))
+        return NULL;
+    if (PyList_GET_SIZE(ents) != PyList_GET_SIZE(traj)) {
+        PyErr_SetString(PyExc_ValueError, "backprop: a trajectory state without its entry");
+        return NULL;
+    }
+    for (Py_ssize_t t = PyList_GET_SIZE(ents) - 1; t >= 0; --t) {
+        PyObject* got = PyList_GET_ITEM(ents, t);
+        PyObject *costs = PyList_GET_ITEM(got, 2), *vks = PyList_GET_ITEM(got, 3), *rx = PyList_GET_ITEM(got, 8);
+        const Py_ssize_t n = PyList_GET_SIZE(costs);
+        const char* hs = entry_hashes(got, n);
+        double mu, ml;
+        if (min_q(costs, vks, hs, v_u, &mu) < 0 || set_val_h(v_u, rx, hs, n, mu) < 0) return NULL;
+        if (min_q(costs, vks, hs, v_l, &ml) < 0 || set_val_h(v_l, rx, hs, n, ml) < 0) return NULL;
+    }
+    if (PyList_SetSlice(traj, 0, PyList_GET_SIZE(traj), NULL) < 0) return NULL;
+    if (PyList_SetSlice(ents, 0, PyList_GET_SIZE(ents), NULL) < 0) return NULL;
+    Py_RETURN_NONE;
+}
+
+/* forward(succ, v_u, v_l, x, sk, rs, cap, counter, tau, traj, sample, resume, entries, tc)
  *   -> (status, x, counter, i)
  * The forward loop of runSampleTrial (e2e_brtdp.py:257-318) from state x:
- *   counter += 1; stop past cap; traj.append(x); [x must be expanded and initialised];
+ *   counter += 1; stop past cap; traj.append(x); [x must be expanded]; initialise its
+ *   successors' values if not yet (init_entry, with tc = time_cost + action_cost);
  *   v_u[x] = min_a Q(x, a, v_u); a = argmin_a Q(x, a, v_l); v_l[x] = Q(x, a, v_l);
  *   stop when v_u - v_l of a's successor <= (v_u - v_l of the start) / tau; else x = succ.
+ * Every traj state's entry is appended to `entries` as it is found (backprop reads them).
  * status 0: the trial's forward pass is over (x, counter as reached);
- *         1: x needs Python (not expanded, or its successors not initialised): x is already
- *            counted and in traj -- call again with resume=1 once it is ready;
- *         2: the chosen action's successor is a copy crash (i = its index in the actions). */
+ *         1: x is not expanded: x is already counted and in traj -- call again with resume=1
+ *            once it is;
+ *         2: a copy crash (i = the action index): the chosen action's successor, or, before
+ *            x's successors are initialised, the first crashing one (_init_succ's raise). */
 static PyObject* forward(PyObject* self, PyObject* args) {
-    PyObject *succ, *v_u, *v_l, *x, *sk, *rs, *traj, *sample;
+    PyObject *succ, *v_u, *v_l, *x, *sk, *rs, *traj, *sample, *ents;
     long cap, counter;
-    double tau;
+    double tau, tc;
     int resume;
-    if (!PyArg_ParseTuple(args, "O!O!O!OOOlldO!Op", &PyDict_Type, &succ, &PyDict_Type, &v_u, &PyDict_Type, &v_l, &x,
-                          &sk, &rs, &cap, &counter, &tau, &PyList_Type, &traj, &sample, &resume))
+    if (!PyArg_ParseTuple(args, "O!O!O!OOOlldO!OpO!d", &PyDict_Type, &succ, &PyDict_Type, &v_u, &PyDict_Type, &v_l, &x,
+                          &sk, &rs, &cap, &counter, &tau, &PyList_Type, &traj, &sample, &resume, &PyList_Type, &ents,
+                          &tc))
         return NULL;
+    const Py_hash_t rsh = PyObject_Hash(rs);
+    if (rsh == -1) return NULL;
+    char rsb[sizeof(Py_hash_t)];
+    memcpy(rsb, &rsh, sizeof rsh);
+    Py_hash_t xh = -1;  /* hash of (x, sk) when known from the parent's entry */
     Py_INCREF(x);
     for (;;) {
         if (!resume) {
@@ -194,15 +309,31 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         resume = 0;
         PyObject* key = PyTuple_Pack(2, x, sk);
         if (key == NULL) goto fail;
-        PyObject* got = PyDict_GetItemWithError(succ, key);
+        PyObject* got = xh != -1 ? _PyDict_GetItem_KnownHash(succ, key, xh) : PyDict_GetItemWithError(succ, key);
         Py_DECREF(key);
         if (got == NULL && PyErr_Occurred()) goto fail;
-        if (got == NULL || PyList_GET_ITEM(got, 6) != Py_True)
-            return Py_BuildValue("(iNli)", 1, x, counter, -1);
+        if (got == NULL) return Py_BuildValue("(iNli)", 1, x, counter, -1);
+        if (PyList_Append(ents, got) < 0) goto fail;
+        PyObject* crash = PyList_GET_ITEM(got, 7);
+        if (PyList_GET_ITEM(got, 6) != Py_True) {
+            if (crash != Py_None && PySet_GET_SIZE(crash) > 0) {  /* _init_succ raises on the first */
+                Py_ssize_t first = -1, pos = 0;
+                PyObject* it;
+                Py_hash_t hh;
+                while (_PySet_NextEntry(crash, &pos, &it, &hh)) {
+                    const Py_ssize_t v = PyLong_AsSsize_t(it);
+                    if (v == -1 && PyErr_Occurred()) goto fail;
+                    if (first < 0 || v < first) first = v;
+                }
+                return Py_BuildValue("(iNli)", 2, x, counter, (int)first);
+            }
+            if (init_entry(got, v_l, v_u, tc) < 0) goto fail;
+        }
         PyObject *costs = PyList_GET_ITEM(got, 2), *vks = PyList_GET_ITEM(got, 3), *rx = PyList_GET_ITEM(got, 8);
         const Py_ssize_t n = PyList_GET_SIZE(costs);
+        const char* hs = entry_hashes(got, n);
         double mu;
-        if (min_q(costs, vks, v_u, &mu) < 0 || set_val(v_u, rx, mu) < 0) goto fail;  /* n == 0 raises here */
+        if (min_q(costs, vks, hs, v_u, &mu) < 0 || set_val_h(v_u, rx, hs, n, mu) < 0) goto fail;  /* n == 0 raises here */
         /* ql = [c + v_l[vk]]; argmin with planner.argmin's generator consumption */
         double ql_stack[32];
         double* ql = n <= 32 ? ql_stack : (double*)PyMem_Malloc(sizeof(double) * (size_t)n);
@@ -214,7 +345,7 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         int err = 0;
         for (Py_ssize_t i = 0; i < n && !err; ++i) {
             double c = PyFloat_AsDouble(PyList_GET_ITEM(costs, i)), v;
-            if ((c == -1.0 && PyErr_Occurred()) || get_val(v_l, PyList_GET_ITEM(vks, i), &v) < 0) {
+            if ((c == -1.0 && PyErr_Occurred()) || get_val_h(v_l, PyList_GET_ITEM(vks, i), hs, i, &v) < 0) {
                 err = 1;
                 break;
             }
@@ -249,8 +380,7 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         }
         const double qi = err ? 0.0 : ql[pick];
         if (ql != ql_stack) PyMem_Free(ql);
-        if (err || set_val(v_l, rx, qi) < 0) goto fail;
-        PyObject* crash = PyList_GET_ITEM(got, 7);
+        if (err || set_val_h(v_l, rx, hs, n, qi) < 0) goto fail;
         if (crash != Py_None && PySet_GET_SIZE(crash) > 0) {
             PyObject* pi = PyLong_FromSsize_t(pick);
             if (pi == NULL) goto fail;
@@ -261,12 +391,13 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         }
         PyObject* vk = PyList_GET_ITEM(vks, pick);
         double a, b, c, d;
-        if (get_val(v_u, vk, &a) < 0 || get_val(v_l, vk, &b) < 0 || get_val(v_u, rs, &c) < 0 ||
-            get_val(v_l, rs, &d) < 0)
+        if (get_val_h(v_u, vk, hs, pick, &a) < 0 || get_val_h(v_l, vk, hs, pick, &b) < 0 ||
+            get_val_h(v_u, rs, rsb, 0, &c) < 0 || get_val_h(v_l, rs, rsb, 0, &d) < 0)
             goto fail;
         const double B = a - b, diff = (c - d) / tau;
         if (B <= diff) break;
         PyObject* nx = PyList_GET_ITEM(PyList_GET_ITEM(got, 1), pick);
+        xh = hs != NULL ? hash_at(hs, n + 1 + pick) : -1;
         Py_INCREF(nx);
         Py_DECREF(x);
         x = nx;
@@ -277,20 +408,26 @@ fail:
     return NULL;
 }
 
-/* expand(rows, fl, lb, cand, key, sk, m0, K, A, cost, changed) -> entry, illegal
+/* expand(rows, fl, lb, cand, key, sk, m0, K, A, cost, changed, keys) -> entry, illegal
  * planner.E2E_BRTDP._expanded over one expansion's rollout rows (e2e_brtdp.py:103-206: T,
  * get_actions; value_init's inputs): rows = the successors' state bytes [n][NP] (a buffer),
  * fl = their u8 flags, lb = their f32 bounds, cand = the candidate joint actions in get_actions
  * order, key = (state bytes, group names, agents, Level).  A row whose item masks changed (a
  * chop or a merge) goes through changed(bytes) -> (canonical bytes, group names) in Python.
- * Returns the _succ entry (without its initialised flag set) and {action: row} of the illegal
- * candidates (or None). */
+ * keys: the planner's key table (a dict; None: no interning) -- every value key built here is
+ * replaced by the table's equal key, if it has one.
+ * Returns the _succ entry (without its initialised flag set; with its hashes, [9]) and
+ * {action: row} of the illegal candidates (or None). */
 static PyObject* expand(PyObject* self, PyObject* args) {
-    PyObject *rows_o, *fl_o, *lb_o, *cand, *key, *sk, *cost, *changed;
+    PyObject *rows_o, *fl_o, *lb_o, *cand, *key, *sk, *cost, *changed, *keys;
     Py_ssize_t m0, K, A;
-    if (!PyArg_ParseTuple(args, "OOOO!O!OnnnO!O", &rows_o, &fl_o, &lb_o, &PyList_Type, &cand, &PyTuple_Type, &key, &sk,
-                          &m0, &K, &A, &PyDict_Type, &cost, &changed))
+    if (!PyArg_ParseTuple(args, "OOOO!O!OnnnO!OO", &rows_o, &fl_o, &lb_o, &PyList_Type, &cand, &PyTuple_Type, &key, &sk,
+                          &m0, &K, &A, &PyDict_Type, &cost, &changed, &keys))
         return NULL;
+    if (keys != Py_None && !PyDict_Check(keys)) {
+        PyErr_SetString(PyExc_TypeError, "expand: keys must be a dict or None");
+        return NULL;
+    }
     Py_buffer rb, fb, lbb;
     if (PyObject_GetBuffer(rows_o, &rb, PyBUF_C_CONTIGUOUS) < 0) return NULL;
     if (PyObject_GetBuffer(fl_o, &fb, PyBUF_C_CONTIGUOUS) < 0) {
@@ -303,7 +440,9 @@ static PyObject* expand(PyObject* self, PyObject* args) {
         return NULL;
     }
     PyObject *actions = NULL, *succ = NULL, *costs = NULL, *vks = NULL, *goals = NULL, *lbs = NULL, *crash = NULL,
-             *illegal = NULL, *out = NULL, *ra = NULL, *self_vk = NULL, *self_r = NULL;
+             *illegal = NULL, *out = NULL, *ra = NULL, *self_vk = NULL, *self_r = NULL, *hb = NULL;
+    Py_hash_t* hv = NULL;  /* the value keys' hashes, then the _succ keys' */
+    Py_ssize_t m = 0;      /* legal successors so far */
     PyObject *sb = PyTuple_GET_ITEM(key, 0), *groups = PyTuple_GET_ITEM(key, 1), *agents = PyTuple_GET_ITEM(key, 2),
              *lvl_o = PyTuple_GET_ITEM(key, 3);
     const Py_ssize_t n = PyList_GET_SIZE(cand);
@@ -315,6 +454,11 @@ static PyObject* expand(PyObject* self, PyObject* args) {
     const unsigned char* pm = (const unsigned char*)PyBytes_AS_STRING(sb) + m0;
     if (rb.len < n * NP || fb.len < n || lbb.len < n * (Py_ssize_t)sizeof(float)) {
         PyErr_SetString(PyExc_ValueError, "expand: row buffers shorter than the candidates");
+        goto done;
+    }
+    hv = (Py_hash_t*)PyMem_Malloc(sizeof(Py_hash_t) * (size_t)(2 * n + 1));
+    if (hv == NULL) {
+        PyErr_NoMemory();
         goto done;
     }
     actions = PyList_New(0);
@@ -370,13 +514,30 @@ static PyObject* expand(PyObject* self, PyObject* args) {
         PyObject* rep = PyTuple_Pack(3, ns, ng, ra);
         PyObject* vk = rep ? PyTuple_Pack(2, rep, sk) : NULL;
         Py_XDECREF(rep);
-        if (nk == NULL || vk == NULL) {
+        const Py_hash_t h1 = vk != NULL ? PyObject_Hash(vk) : -1;
+        if (nk != NULL && h1 != -1 && keys != Py_None) {  /* intern */
+            PyObject* c = _PyDict_GetItem_KnownHash(keys, vk, h1);
+            if (c != NULL) {
+                Py_INCREF(c);
+                Py_DECREF(vk);
+                vk = c;
+            } else if (PyErr_Occurred() || _PyDict_SetItem_KnownHash(keys, vk, vk, h1) < 0) {
+                Py_CLEAR(vk);
+            }
+        }
+        PyObject* sk2 = (nk != NULL && vk != NULL) ? PyTuple_Pack(2, nk, sk) : NULL;
+        const Py_hash_t h2 = sk2 != NULL ? PyObject_Hash(sk2) : -1;
+        Py_XDECREF(sk2);
+        if (nk == NULL || vk == NULL || h2 == -1) {
             Py_XDECREF(nk);
             Py_XDECREF(vk);
             Py_DECREF(ns);
             Py_DECREF(ng);
             goto done;
         }
+        hv[m] = h1;
+        hv[n + 1 + m] = h2;
+        ++m;
         if (lvl) {  /* _copy_crashes: two co-located agents that both hold */
             const unsigned char* q = (const unsigned char*)PyBytes_AS_STRING(ns);
             int hit = 0;
@@ -418,8 +579,19 @@ static PyObject* expand(PyObject* self, PyObject* args) {
     }
     self_r = PyTuple_Pack(3, sb, groups, ra);
     if (self_r == NULL || (self_vk = PyTuple_Pack(2, self_r, sk)) == NULL) goto done;
-    out = Py_BuildValue("([OOOOOOOOO]O)", actions, succ, costs, vks, goals, lbs, Py_False, crash ? crash : Py_None,
-                        self_vk, illegal ? illegal : Py_None);
+    if (keys != Py_None) {
+        PyObject* c = PyDict_SetDefault(keys, self_vk, self_vk);
+        if (c == NULL) goto done;
+        Py_INCREF(c);
+        Py_DECREF(self_vk);
+        self_vk = c;
+    }
+    if ((hv[m] = PyObject_Hash(self_vk)) == -1) goto done;
+    memmove(hv + m + 1, hv + n + 1, sizeof(Py_hash_t) * (size_t)m);  /* compact: [m value keys, self, m _succ keys] */
+    hb = PyBytes_FromStringAndSize((const char*)hv, (Py_ssize_t)sizeof(Py_hash_t) * (2 * m + 1));
+    if (hb == NULL) goto done;
+    out = Py_BuildValue("([OOOOOOOOOO]O)", actions, succ, costs, vks, goals, lbs, Py_False, crash ? crash : Py_None,
+                        self_vk, hb, illegal ? illegal : Py_None);
 done:
     Py_XDECREF(actions);
     Py_XDECREF(succ);
@@ -432,6 +604,8 @@ done:
     Py_XDECREF(ra);
     Py_XDECREF(self_r);
     Py_XDECREF(self_vk);
+    Py_XDECREF(hb);
+    PyMem_Free(hv);
     PyBuffer_Release(&rb);
     PyBuffer_Release(&fb);
     PyBuffer_Release(&lbb);
@@ -442,6 +616,7 @@ static PyMethodDef methods[] = {
     {"expand", expand, METH_VARARGS, "_expanded's successor lists from one expansion's rollout rows"},
     {"forward", forward, METH_VARARGS, "runSampleTrial's forward loop over expanded, initialised states"},
     {"backprop", backprop, METH_VARARGS, "runSampleTrial's backward pass"},
+    {"init_succ", init_succ, METH_VARARGS, "value_init of an expanded state's successors"},
     {"tie_pick", tie_pick, METH_VARARGS, "argmin's multinomial tie-break over a list of minima flags"},
     {NULL, NULL, 0, NULL},
 };

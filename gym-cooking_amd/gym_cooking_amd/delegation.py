@@ -63,10 +63,14 @@ class SubtaskAllocDistribution:
         return self.probs[tuple(subtask_alloc)]
 
     def get_max(self, rng=random):
+        max_subtask_allocs = self.max_allocs()
+        return None if max_subtask_allocs is None else rng.choice(max_subtask_allocs)
+
+    def max_allocs(self):
+        """The allocations get_max chooses among (None when there are none)."""
         if len(self.probs) > 0:
             max_prob = max(self.probs.values())
-            max_subtask_allocs = [subtask_alloc for subtask_alloc, p in self.probs.items() if p == max_prob]
-            return rng.choice(max_subtask_allocs)
+            return [subtask_alloc for subtask_alloc, p in self.probs.items() if p == max_prob]
         return None
 
     def update(self, subtask_alloc, factor) -> None:
@@ -102,6 +106,7 @@ class BayesianDelegator:
     ``probs`` is a :class:`SubtaskAllocDistribution` of tuples of :data:`SubtaskAllocation`.
     `rng`: the generator of ``get_max``'s tie-break (default Python's global one, as the
     reference)."""
+    use_memo = True  # the per-update memo of _bayes_update_gen (False: recompute everything)
 
     def __init__(self, agent_name, all_agent_names, model_type, planner, none_action_prob, rng=None):
         self.name = "Bayesian Delegator"
@@ -115,8 +120,12 @@ class BayesianDelegator:
         self._rng = rng if rng is not None else random
 
     # ---- beliefs ------------------------------------------------------------------------
-    def select_subtask(self, agent_name):  # :1009-1017
-        max_subtask_alloc = self.probs.get_max(self._rng)
+    def select_subtask(self, agent_name, max_allocs=False):  # :1009-1017
+        """`max_allocs`: probs.max_allocs(), when the caller has it (several selections from
+        one unchanged distribution); the draw is the same."""
+        if max_allocs is False:
+            max_allocs = self.probs.max_allocs()
+        max_subtask_alloc = None if max_allocs is None else self._rng.choice(max_allocs)
         if max_subtask_alloc is not None:
             for t in max_subtask_alloc:
                 if agent_name in t.subtask_agent_names:
@@ -163,14 +172,23 @@ class BayesianDelegator:
     # ---- inverse planning ---------------------------------------------------------------
     def _other_agent_planners_gen(self, obs, backup_subtask):  # get_other_agent_planners :375-433
         planners = {}
+        top = self.probs.max_allocs()  # nothing below changes probs
         for other_agent_name in self.all_agent_names:
             if other_agent_name != self.agent_name:
-                subtask, subtask_agent_names = self.select_subtask(agent_name=other_agent_name)
+                subtask, subtask_agent_names = self.select_subtask(agent_name=other_agent_name, max_allocs=top)
                 if subtask is None:
                     subtask = backup_subtask
                     subtask_agent_names = tuple(sorted([other_agent_name, self.agent_name]))
-                planner = copy.copy(self.planner)
-                yield from planner._set_settings_gen(obs, subtask, subtask_agent_names)
+                memo = self.planner.__dict__.get("_bayes_memo")
+                mk = ("op", str(subtask), tuple(subtask_agent_names))
+                planner = memo.get(mk) if memo is not None else None
+                if planner is None:
+                    planner = copy.copy(self.planner)
+                    yield from planner._set_settings_gen(obs, subtask, subtask_agent_names)
+                    if memo is not None:
+                        # within one update (one obs) a second set-up of the same subtask and
+                        # agents inserts nothing and sets the same fields: share the first
+                        memo[mk] = planner
                 planners[other_agent_name] = planner
         return planners
 
@@ -197,13 +215,18 @@ class BayesianDelegator:
     def _prob_nav_actions_gen(self, obs_tm1, actions_tm1, subtask, subtask_agent_names, beta, no_level_1):
         assert len(subtask_agent_names) == 1 or len(subtask_agent_names) == 2
         names = obs_tm1.get_agent_names()
+        memo = self.planner.__dict__.get("_bayes_memo")
         if subtask is None:
             assert len(subtask_agent_names) != 2, "Two agents are doing None."
             me = names.index(self.agent_name)
-            # get_single_actions(obs_tm1, self agent) - 1: its legal moves with every agent in place
-            probe = capi.subtask(1, [me], [0, 0], 0, 0, 1)
-            _, fl, _ = yield (obs_tm1.state_bytes(), [(c,) for c in range(4)], probe)
-            num_actions = int(sum(1 for f in fl if f & capi.ROLL_LEGAL))
+            num_actions = memo.get(("none", me)) if memo is not None else None
+            if num_actions is None:
+                # get_single_actions(obs_tm1, self agent) - 1: its legal moves with every agent in place
+                probe = capi.subtask(1, [me], [0, 0], 0, 0, 1)
+                _, fl, _ = yield (obs_tm1.state_bytes(), [(c,) for c in range(4)], probe)
+                num_actions = int(sum(1 for f in fl if f & capi.ROLL_LEGAL))
+                if memo is not None:
+                    memo[("none", me)] = num_actions
             action_prob = (1.0 - self.none_action_prob) / (num_actions)
             diffs = [self.none_action_prob] + [action_prob] * num_actions
             return _softmax_at(beta * np.asarray(diffs), 0 if tuple(actions_tm1[subtask_agent_names[0]]) == (0, 0) else 1)
@@ -213,6 +236,16 @@ class BayesianDelegator:
         if not other_planners:
             raise NotImplementedError("prob_nav_actions without other agents (a 1-agent env or no_level_1)")
         p = self.planner
+        mk = ("q", str(subtask), tuple(subtask_agent_names), action, self.agent_name, beta)
+        hit = memo.get(mk) if memo is not None else None
+        if hit is not None:
+            # The Level-1 Q values do not read the other agents' planners, and within one
+            # update the first evaluation left every value, T memo entry and expansion they
+            # read in place: the same softmax of the same doubles.  The set-up on the same
+            # state and subtask inserts nothing and sets the fields it set then.
+            p.__dict__.update(hit[1])
+            p.other_agent_planners = dict(other_planners)
+            return hit[0]
         yield from p._set_settings_gen(obs_tm1, subtask, subtask_agent_names, other_planners)
         err = yield from p._taken_action_error_gen(p.start, action)  # Q(state, taken) and the assert below raise
         if err is not None:
@@ -226,14 +259,27 @@ class BayesianDelegator:
             valid_nav_actions = list(filter(lambda x: x[other_index] == action[other_index], valid_nav_actions))
         qs = yield from p._Q_seq_gen(p.start, valid_nav_actions, p.v_l)
         qdiffs = [old_q - q for q in qs]
-        return _softmax_at(beta * np.asarray(qdiffs), valid_nav_actions.index(action))
+        out = _softmax_at(beta * np.asarray(qdiffs), valid_nav_actions.index(action))
+        if memo is not None:
+            memo[mk] = (out, {k: p.__dict__[k] for k in _planner.CONF_FIELDS})
+        return out
 
     def _doability_pairs(self) -> list:
         return [(t.subtask, tuple(t.subtask_agent_names)) for a in self.probs.enumerate_subtask_allocs() for t in a]
 
     def _bayes_update_gen(self, obs_tm1, actions_tm1, beta, doable):
         """bayes_update with the doability answers given (`doable`: (subtask, agent names) ->
-        bool, from :meth:`_doability`) and every rollout request yielded."""
+        bool, from :meth:`_doability`) and every rollout request yielded.  The update keeps a
+        memo on its planner (``_bayes_memo``) of the inverse-planning work that repeats within
+        it on the one state obs_tm1 (see _prob_nav_actions_gen, E2E_BRTDP._modified_state);
+        it is dropped when the update ends, before any search can change a value."""
+        self.planner._bayes_memo = {} if self.use_memo else None
+        try:
+            yield from self._bayes_update_body(obs_tm1, actions_tm1, beta, doable)
+        finally:
+            self.planner._bayes_memo = None
+
+    def _bayes_update_body(self, obs_tm1, actions_tm1, beta, doable):
         for subtask_alloc in self.probs.enumerate_subtask_allocs():
             for t in subtask_alloc:
                 if t.subtask is not None and not doable[(t.subtask, tuple(t.subtask_agent_names))]:

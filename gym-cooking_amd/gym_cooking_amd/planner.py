@@ -182,6 +182,29 @@ def argmin(vector, rng=np.random):
     return np.where(rng.multinomial(1, e_x / e_x.sum()))[0][0]
 
 
+def _argmin_plan(vector: list):
+    """What argmin(vector, rng) draws and returns, as data: (index, None) for a unique minimum,
+    (None, tie mask) for ties.  Lets a caller that meets the same Q vector again replay the
+    draw (_argmin_apply) without recomputing it."""
+    m = min(vector)
+    if vector.count(m) == 1:
+        return (vector.index(m), len(vector))
+    return (None, [v == m for v in vector])
+
+
+def _argmin_apply(plan, rng) -> int:
+    """argmin's draw and result from its _argmin_plan (the same consumption of rng)."""
+    i, n = plan
+    if i is not None:
+        if i != n - 1:
+            rng.random_sample()
+        return i
+    if _native is not None:
+        return _native.tie_pick(n, rng.random_sample)
+    e_x = np.array(n, dtype=float)
+    return np.where(rng.multinomial(1, e_x / e_x.sum()))[0][0]
+
+
 class _Expander:
     """An engine batch of up to ROWS rollout rows for a level.  ``run(requests)`` evaluates
     any number of expansion requests -- (state bytes, joint actions, subtask configuration) --
@@ -368,6 +391,7 @@ class E2E_BRTDP:
         self._succ: Dict = {}  # (state key, subtask key) -> [actions, successors, costs, value keys, goal flags, lower bounds, initialised]
         self._tmemo: Dict = {}  # this object's T memo: (repr, action) -> successor (bytes, groups)
         self._illegal: Dict = {}  # (state key, subtask key) -> {action outside get_actions: (next bytes, flags)}
+        self._vkeys: Dict = {}  # value key -> the one object of it the native expansions use (identity lookups)
 
     # ---- configuration (set_settings, e2e_brtdp.py:582-652) --------------------------------
     def __copy__(self):  # e2e_brtdp.py:97-101: a shallow copy shares the value tables (and here the caches)
@@ -610,7 +634,7 @@ class E2E_BRTDP:
         sk = self._sub_key
         nxt = np.ascontiguousarray(nxt)
         entry, illegal = _native.expand(nxt, np.ascontiguousarray(fl), np.ascontiguousarray(lb), cand, key, sk, m0, K,
-                                        A, _COST, changed)
+                                        A, _COST, changed, self.__dict__.get("_vkeys"))
         self._succ[(key, sk)] = entry
         if illegal:
             self._illegal[(key, sk)] = (illegal, nxt.reshape(-1), len(key[0]), fl)
@@ -638,6 +662,8 @@ class E2E_BRTDP:
             _raise_copy_crash(got[0][min(got[7])])
         v_l, v_u = self.v_l, self.v_u
         tc = self.time_cost + self.action_cost
+        if _native is not None and self.use_native:  # the same loop in C (brtdp_host.c init_entry)
+            return _native.init_succ(got, v_l, v_u, tc)
         for vk, g, lb in zip(got[3], got[4], got[5]):  # _value_init of each, inlined (same arithmetic)
             if vk in v_l and vk in v_u:
                 continue
@@ -802,25 +828,27 @@ class E2E_BRTDP:
             v_l[rx] = min([c + v_l[vk] for c, vk in zip(costs, vks)])
 
     def _sample_trial_native(self):
+        """The trial in C: forward runs until a state needs expanding (it initialises
+        successors itself), this generator yields that state's request (what _need yields),
+        and backprop walks the trajectory's entries."""
         sk = self._sub_key
         succ, v_u, v_l, rng = self._succ, self.v_u, self.v_l, self._rng
         rs = (self._repr(self.start), sk)
-        traj = []
+        traj, ents = [], []
+        tc = self.time_cost + self.action_cost
+        cand = _CAND[len(self._agents)]
         x, counter, resume = self.start, 0, False
         while True:
             st, x, counter, i = _native.forward(succ, v_u, v_l, x, sk, rs, self.cap, counter, self.tau, traj,
-                                                rng.random_sample, resume)
+                                                rng.random_sample, resume, ents, tc)
             if st == 0:
                 break
-            if st == 2:  # get_expected_diff's T raises
+            if st == 2:  # get_expected_diff's T raises (or _init_succ's, on the first crashing successor)
                 _raise_copy_crash(succ[(x, sk)][0][i])
-            if (x, sk) not in succ:
-                yield from self._need(x)
-            got = succ[(x, sk)]
-            if not got[6]:
-                self._init_succ(got)
+            res = yield (np.frombuffer(x[0], np.uint8), cand, self._sub)  # st == 1: _need(x)
+            self._expanded(x, cand, res)
             resume = True
-        _native.backprop(succ, v_u, v_l, traj, sk)
+        _native.backprop(v_u, v_l, traj, ents)
 
     def _main(self):  # main
         main_counter = 0
@@ -897,11 +925,18 @@ class E2E_BRTDP:
     def _modified_state_env(self, env):
         if not getattr(self, "_level", 0):
             return
-        exp = self._exp
-        full = env.state_bytes()
-        full[exp.t_plane:] = 0
-        groups = _groups(env)
-        key = (_canon(full.tobytes(), exp.A, exp.K, exp.enc, exp.wide), groups, tuple(self._agents), self._level)
+        memo = self.__dict__.get("_bayes_memo")
+        got = memo.get(("env", self._exp_key, tuple(self._agents), self._level)) if memo is not None else None
+        if got is not None and got[0] is env:  # the update's one state, keyed once
+            key = got[1]
+        else:
+            exp = self._exp
+            full = env.state_bytes()
+            full[exp.t_plane:] = 0
+            groups = _groups(env)
+            key = (_canon(full.tobytes(), exp.A, exp.K, exp.enc, exp.wide), groups, tuple(self._agents), self._level)
+            if memo is not None:
+                memo[("env", self._exp_key, key[2], key[3])] = (env, key)
         yield from self._modified_state(key)
 
     def _modified_state(self, key):
@@ -914,14 +949,27 @@ class E2E_BRTDP:
         if not self._level:
             return
         groups = key[1]
+        memo = self.__dict__.get("_bayes_memo")  # set during a belief update (delegation.py)
         for name, op in self.other_agent_planners.items():
             op._exp, op._exp_key, op._rng = self._exp, self._exp_key, self._rng
             op.other_agent_planners, op._level = {}, 0  # _configure without other planners: Level 0
+            mk = None
+            if memo is not None:
+                # Within one belief update no value is overwritten (value_init only inserts), so
+                # an other-agent set-up met again -- same state, subtask and agents -- has its
+                # start initialised and expanded and the same Q vector: only the draw remains.
+                mk = ("ms", key[0], groups, str(op.subtask), tuple(op.subtask_agent_names))
+                plan = memo.get(mk)
+                if plan is not None:
+                    _argmin_apply(plan, op._rng)
+                    continue
             yield from op._configure_gen(op._configure_raw(self._level_name, self._A, self._dev, key[0], groups,
                                                            op.subtask, op.subtask_agent_names))
             yield from op._need(op.start)
-            acts = op._succ[(op.start, op._sub_key)][0]
-            argmin(op._q_all(op.start, op.v_l), op._rng)
+            plan = _argmin_plan(op._q_all(op.start, op.v_l))
+            if mk is not None:
+                memo[mk] = plan
+            _argmin_apply(plan, op._rng)
 
     def start_values(self) -> Tuple[float, float]:
         """(v_l, v_u) of the current start state."""
@@ -981,6 +1029,11 @@ class PlanEnv:
 _AGENT_NAMES: Dict[int, List[str]] = {}
 
 
+# what a set-up (_configure, _configure_raw, _configure_gen) assigns on the planner, besides
+# other_agent_planners (the belief update's memo replays them)
+CONF_FIELDS = ("_level", "subtask", "subtask_agent_names", "is_joint", "_agents", "_sub_key", "_kind", "_goal_mask",
+               "cur_obj_count", "_sub", "_conf", "_level_name", "_A", "_dev", "start", "_start_goal", "_exp",
+               "_exp_key")
 _AGENT_IX: Dict[tuple, tuple] = {}  # (A, subtask agent names) -> their indices
 _NOOP_ROW = {1: [(_NOOP,)], 2: [(_NOOP, _NOOP)]}  # the one candidate of a set-up's no-op row
 

@@ -102,3 +102,63 @@ def test_host_bayes_update_matches_reference():
                                                                           str(got)[:300], str(want)[:300]))
     assert fx["calls"]
     assert not errs, "%d of %d updates differ:\n%s" % (len(errs), len(fx["calls"]), "\n".join(errs[:6]))
+
+
+def _plain(v):
+    """A planner field as comparable data (arrays as bytes, subtasks and configurations as text)."""
+    if isinstance(v, np.ndarray):
+        return v.tobytes()
+    if isinstance(v, (list, tuple)):
+        return [_plain(x) for x in v]
+    if isinstance(v, (bytes, frozenset, int, float, bool, str)) or v is None:
+        return v
+    return str(bytes(v)) if hasattr(v, "_fields_") else str(v)
+
+
+def test_host_bayes_memo_changes_nothing():
+    """The per-update memo (BayesianDelegator.use_memo) against the plain recomputation, on every
+    recorded update in one batch: the same posteriors and exceptions, and the same state left
+    behind -- both generators' states (the memo replays the argmin and get_max draws), the value
+    tables in insertion order, the expansions and the other-agent planners' subtasks.  The
+    recorded posteriors alone would not see a draw too many or too few."""
+    import test_planner_host as th
+    from gym_cooking_amd.delegation import BayesianDelegator, SubtaskAllocDistribution, bayes_update_batch
+    from gym_cooking_amd.planner import E2E_BRTDP
+    fx = load()
+    calls = fx["calls"]
+
+    def run(memo):
+        ds, obs, acts = [], [], []
+        for c in calls:
+            cfg = fx["configs"][c["cfg"]]
+            o = th._env(cfg["level"], cfg["A"], c)
+            planner = E2E_BRTDP(**fx["params"], rng=np.random.RandomState(c["np_seed"]), expander=th.OracleExpander)
+            d = BayesianDelegator(c["self"], o.get_agent_names(), "bd", planner, fx["none_action_prob"],
+                                  rng=random.Random(c["random_seed"]))
+            d.use_memo = memo
+            allocs = [_alloc(a) for a, _ in c["before"]]
+            d.probs = SubtaskAllocDistribution(allocs)
+            for k, (_, p) in zip(allocs, c["before"]):
+                d.probs.probs[k] = p
+            ds.append(d)
+            obs.append(o)
+            acts.append({n: tuple(a) for n, a in c["actions"].items()})
+        errs = bayes_update_batch(ds, obs, acts, fx["beta"])
+        out = []
+        for d, e in zip(ds, errs):
+            p = d.planner
+            st = p._rng.get_state()
+            out.append((None if e is None else type(e).__name__, list(d.probs.probs.items()), d._rng.getstate(),
+                        (st[0], st[1].tolist(), st[2:]), list(p.v_l.items()), list(p.v_u.items()), list(p._succ),
+                        {n: (str(op.subtask), op.subtask_agent_names)
+                         for n, op in getattr(p, "other_agent_planners", {}).items()},
+                        sorted(k for k in p.__dict__ if not k.startswith("__")),
+                        [(k, _plain(p.__dict__[k])) for k in ("_level", "subtask", "subtask_agent_names", "is_joint",
+                                                              "_agents", "_sub_key", "cur_obj_count", "start",
+                                                              "_start_goal", "_conf") if k in p.__dict__]))
+        return out
+
+    a, b = run(True), run(False)
+    assert len(a) == len(b) == len(calls)
+    bad = [i for i, (x, y) in enumerate(zip(a, b)) if x != y]
+    assert not bad, "%d of %d updates leave a different state with the memo: %s" % (len(bad), len(a), bad[:10])

@@ -302,6 +302,17 @@ def test_native_errors_raise_python_exceptions():
         nat.tie_pick([], lambda: 0.5)
     entry = [None, [], [], [], None, None, True, None, "rx"]
     with pytest.raises(ValueError):
-        nat.backprop({("x", "sk"): entry}, {}, {}, ["x"], "sk")
+        nat.backprop({}, {}, ["x"], [entry])
+    with pytest.raises(ValueError):  # a trajectory state without its entry
+        nat.backprop({}, {}, ["x", "y"], [entry])
     with pytest.raises(ValueError):
-        nat.forward({("x", "sk"): entry}, {}, {}, "x", "sk", "x", 10, 0, 2.0, [], lambda: 0.5, False)
+        nat.forward({("x", "sk"): entry}, {}, {}, "x", "sk", "x", 10, 0, 2.0, [], lambda: 0.5, False, [], 1.1)
+    # value_init's assert (e2e_brtdp.py:722), after the inserts before it, as _init_succ's
+    got = [None, None, None, ["a", "b", "c"], [True, False, False], [2.0, 0.0, 3.0], False, None, "rx"]
+    v_l, v_u = {}, {}
+    with pytest.raises(AssertionError, match="lower: 0.0"):
+        nat.init_succ(got, v_l, v_u, 1.1)
+    assert v_l == {"a": 0.0} and v_u == {"a": 0.0} and got[6] is False
+    got[5][1] = 1.0
+    nat.init_succ(got, v_l, v_u, 1.1)
+    assert got[6] is True and v_l["b"] == 1.0 * 1.1 - 1.09 and v_u["c"] == 3.0 * 1.1 * 5 * 1.1
