@@ -109,6 +109,9 @@ __device__ __forceinline__ uint32_t bld32(__amdgpu_buffer_rsrc_t r, uint32_t vof
 // oc_step_n, whose trajectory stream is far larger than L2, is faster with nt stores instead
 // (tools/stepexp.hip: 4.3 vs 5.2-5.3 us/step at 2^20 envs; sc1 5.3).
 constexpr int kCPsc1 = 16, kCPnt = 2;
+#ifndef OC_STEP_CP
+#define OC_STEP_CP kCPsc1  // oc_step's store policy (an A/B switch: tools/step_ab.py --per-step)
+#endif
 template <int CP = 0>
 __device__ __forceinline__ void bst32(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, CP);
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(kStepBlock) void oc_step_kernel(LevelArgs L, const 
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     StepStats st;
-    step_chunk<A, K, kCPsc1, MODE>(L, tbl, c, b, has_ex, has_coll, P, g, st);
+    step_chunk<A, K, OC_STEP_CP, MODE>(L, tbl, c, b, has_ex, has_coll, P, g, st);
     if (stats != nullptr) {  // wave sums, then fire-and-forget 64-bit atomics into this block's row
         const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
                                        wave_sum(st.err)};

@@ -37,6 +37,7 @@ for i in 1 2; do
   timeout -k 10 600 python bench.py > $O/bench_default_$i.json 2> $O/bench_default_$i.err || { echo BENCH_FAILED; tail -20 $O/bench_default_$i.err; exit 1; }
 done
 timeout -k 10 600 python tools/step_ab.py --libs tools/_ab/liboc_stag0.so tools/_ab/liboc_stag1.so --rounds 4 --agents 3 > $O/step_ab_stagger.jsonl 2> $O/step_ab_stagger.err || { echo AB_FAILED; tail -20 $O/step_ab_stagger.err; exit 1; }
+timeout -k 10 300 python tools/step_ab.py --per-step --libs tools/_ab/liboc_stag0.so tools/_ab/liboc_stepnt.so --rounds 3 > $O/step_ab_perstep_nt.jsonl 2> $O/step_ab_perstep.err || { echo AB2_FAILED; tail -20 $O/step_ab_perstep.err; exit 1; }
 cp tools/_ab/liboc_stag1.so gym-cooking_amd/gym_cooking_amd/liboc_engine.so
 timeout -k 10 600 python -u -m pytest tests/test_c3_stepn_gpu.py -x -v --timeout 300 --timeout-method thread > $O/gputest_c3_stag1.log 2>&1 || { echo C3_STAG1_FAILED; tail -30 $O/gputest_c3_stag1.log; exit 1; }
 tail -1 $O/gputest_c3_stag1.log
