@@ -287,13 +287,10 @@ __host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
 #ifndef OC_LW_STEPS
 #define OC_LW_STEPS 4
 #endif
-// Staggered hand-over (OC_LW_STAGGER): the odd stepping waves meet batch k's barrier between
-// the compute and the stores of step 4k - 1 instead of before step 4k, so at each release the
-// even waves compute while the odd ones store (their batch-k reads all follow the barrier, and
-// their batch k - 1 reads all precede it, so the loader's refill of that half stays safe).
-#ifndef OC_LW_STAGGER
-#define OC_LW_STAGGER 0
-#endif
+// Also measured and dropped (round 4, profiles/r04/lw_stagger/): a staggered hand-over, the odd
+// stepping waves meeting batch k's barrier between the compute and the stores of step 4k - 1
+// (so that at each release the even waves compute while the odd ones store): 6.46-6.51 us/step
+// against 6.04-6.07, four alternating rounds on one box, C3 parity tests green on it.
 constexpr int kLwSteps = OC_LW_STEPS;  // steps per ring half (one barrier per kLwSteps steps)
 // A = 3 only: there the stepping waves' drains were a fifth of the time (C3, 100-step launches,
 // one box: 6.42 -> 6.07 us/step, outputs identical).  At A <= 2 the step is store-bound and the
@@ -392,12 +389,11 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void oc_step_n_
 #pragma unroll
             for (int a = 0; a < A; ++a) nxt[a] = n > 1 ? bld32<LCP>(b.act, vo, (uint32_t)(A + a) * P) : 0u;
         }
-        const bool lag = OC_LW_STAGGER && ((threadIdx.x >> 6) & 1u);  // wave-uniform
         for (int r = 0; r < n; ++r) {
             uint32_t act[A], ex[A], cm;
             if (LW) {
                 const int q = r % kLwSteps;
-                if (q == 0 && (!lag || r == 0)) lds_barrier();  // the loader has filled this batch's half
+                if (q == 0) lds_barrier();  // the loader has filled this batch's half
                 const int h = (r / kLwSteps) & 1;
 #pragma unroll
                 for (int a = 0; a < A; ++a)
@@ -416,7 +412,6 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void oc_step_n_
             const uint32_t f_in = c.wf;
             const bool full = ocsw::step4<A, K, MODE>(L.sw, c.wx, c.wy, c.wh, c.wl, c.wm, T0, T1, c.wf, act, ex,
                                                       cm, cls_of, WaveAny{}, pending);
-            if (LW && lag && r % kLwSteps == kLwSteps - 1 && r + 1 < n) lds_barrier();  // next batch, before the stores
             st.coll += __popc(cm & vmask);
             if (full) {  // episode ends only on the full path
                 const uint32_t ended = (c.wf & ~f_in & vmask) & ocsw::k01;

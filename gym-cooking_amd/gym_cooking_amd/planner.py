@@ -298,18 +298,34 @@ class _Expander:
     def _launch(self, chunk, subs):
         """One oc_rollout launch over the chunk's requests, packed with whole-array copies: the
         states repeated per candidate row, each (candidate list, agents) group's action codes
-        scattered at once."""
+        scattered at once.  A chunk whose requests share one candidate list (a round of
+        expansions: every request is _CAND[1] or _CAND[2]) is packed and split with fixed-stride
+        reshapes instead of per-request offsets."""
         hi, ha, hal = self._hi, self._ha, self._hal
-        counts = np.fromiter((len(req[1]) for req, _ in chunk), np.int64, len(chunk))
-        starts = np.zeros(len(chunk), np.int64)
-        np.cumsum(counts[:-1], out=starts[1:])
-        n = int(counts.sum())
-        hi[:, :n] = np.repeat(np.stack([req[0] for req, _ in chunk]), counts, axis=0).T
+        m = len(chunk)
+        codes0 = chunk[0][0][1]
+        # the request states (byte arrays or bytes) joined into one [m, NP] array: one join and
+        # one frombuffer instead of np.stack's per-array work (10x faster at 100 requests)
+        states = np.frombuffer(b"".join([req[0] for req, _ in chunk]), np.uint8).reshape(m, self.NP)
+        sids = np.fromiter((si for _, si in chunk), np.uint8, m)
+        uniform = all(req[1] is codes0 for req, _ in chunk)
+        if uniform:
+            c = len(codes0)
+            n = c * m
+            counts = starts = None
+            hi[:, :n] = np.repeat(states, c, axis=0).T
+            hal[:n] = np.repeat(sids, c)
+        else:
+            counts = np.fromiter((len(req[1]) for req, _ in chunk), np.int64, m)
+            starts = np.zeros(m, np.int64)
+            np.cumsum(counts[:-1], out=starts[1:])
+            n = int(counts.sum())
+            hi[:, :n] = np.repeat(states, counts, axis=0).T
+            hal[:n] = np.repeat(sids, counts)
         hi[self.t_plane:, :n] = 0  # t and flags: copied through by the kernel, not part of a planner state
         ha[:, :n] = _NOOP
-        hal[:n] = np.repeat(np.fromiter((si for _, si in chunk), np.uint8, len(chunk)), counts)
         groups, agents_of = {}, {}
-        for (req, _), s0 in zip(chunk, starts.tolist()):
+        for i, (req, _) in enumerate(chunk):
             codes, sub = req[1], req[2]
             ag = agents_of.get(id(sub))
             if ag is None:
@@ -317,12 +333,18 @@ class _Expander:
             g = groups.get((id(codes), ag))
             if g is None:
                 g = groups[(id(codes), ag)] = (codes, ag, [])
-            g[2].append(s0)
-        for codes, ag, s0s in groups.values():
-            c = _codes_array(codes)
-            rows = (np.asarray(s0s)[:, None] + np.arange(len(codes))[None, :]).ravel()
+            g[2].append(i)
+        for codes, ag, idx in groups.values():
+            cA = _codes_array(codes)
+            k = len(codes)
+            if uniform and len(idx) == m:  # every request: the whole row range
+                for q, a in enumerate(ag):
+                    ha[a, :n] = np.tile(cA[:, q], m)
+                continue
+            s0 = np.asarray(idx) * k if uniform else starts[idx]
+            rows = (s0[:, None] + np.arange(k)[None, :]).ravel()
             for q, a in enumerate(ag):
-                ha[a, rows] = np.tile(c[:, q], len(s0s))
+                ha[a, rows] = np.tile(cA[:, q], len(idx))
         table = [sub for _, sub in sorted(subs.values(), key=lambda v: v[0])]
         self._d_in.copy_(self._h_in_all, non_blocking=True)  # one H2D
         lib, eb = self.eb.lib, self.eb
@@ -336,6 +358,9 @@ class _Expander:
         nxt = self._ho[:, :n].T.copy()  # [n, NP]: each request's rows are a contiguous slice
         nxt[:, self.t_plane:] = 0
         fl, lb = self._hf[:n].copy(), self._hl[:n].copy()
+        if uniform:  # m views of c rows each
+            c = n // m
+            return list(zip(nxt.reshape(m, c, self.NP), fl.reshape(m, c), lb.reshape(m, c)))
         return [(nxt[s0:s0 + c], fl[s0:s0 + c], lb[s0:s0 + c]) for s0, c in zip(starts.tolist(), counts.tolist())]
 
 
