@@ -287,6 +287,9 @@ __host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
 #ifndef OC_LW_STEPS
 #define OC_LW_STEPS 4
 #endif
+#ifndef OC_LW_X4
+#define OC_LW_X4 0  // the loader's action loads as 16-byte loads (an A/B switch)
+#endif
 // Also measured and dropped (round 4, profiles/r04/lw_stagger/): a staggered hand-over, the odd
 // stepping waves meeting batch k's barrier between the compute and the stores of step 4k - 1
 // (so that at each release the even waves compute while the odd ones store): 6.46-6.51 us/step
@@ -317,7 +320,7 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void oc_step_n_
     __shared__ uint32_t waves_done;
     __shared__ unsigned long long fold[OC_NSTATS][64 + 8];  // the folding wave's partial sums
     // LW: [half][step of the batch][stepping wave][agent][lane] action words
-    __shared__ uint32_t ring[LW ? 2 * kLwSteps * (kBlock / 64) * A * 64 : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t ring[LW ? 2 * kLwSteps * (kBlock / 64) * A * 64 : 1];
     if (threadIdx.x < 64u) tbl4[threadIdx.x] = L.cls4[threadIdx.x];
     if (threadIdx.x == 0u) waves_done = 0u;
     __syncthreads();
@@ -346,6 +349,29 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void oc_step_n_
         if (loader) {
             // the action words of steps r0 .. r0 + kLwSteps - 1 (those < n) into ring half h;
             // this wave issues no store, so its waits are for its own loads only
+#if OC_LW_X4
+            // 16-byte loads: a (step, stepping wave, agent) group is 64 lanes' words = 256 B,
+            // contiguous in the actions and in the ring, so 16 lanes move one group and a wave
+            // instruction four; the whole offset is in the VGPR (the four groups differ in step
+            // and agent).  Past the last step the range check returns zeros.
+            typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+            constexpr int kGroups = kLwSteps * (kBlock / 64) * A;
+            auto fill = [&](int r0, int h) {
+                u32x4v w[kGroups / 4];
+#pragma unroll
+                for (int i = 0; i < kGroups / 4; ++i) {
+                    const int G = 4 * i + (int)(lane >> 4);
+                    const int q = G / ((kBlock / 64) * A), v = (G / A) % (kBlock / 64), a = G % A;
+                    const uint32_t off = (uint32_t)((r0 + q) * A + a) * P + (gb + 64u * v) * 4u + 16u * (lane & 15u);
+                    w[i] = __builtin_amdgcn_raw_buffer_load_b128(b.act, (int)off, 0, LCP);
+                }
+#pragma unroll
+                for (int i = 0; i < kGroups / 4; ++i) {
+                    const int G = 4 * i + (int)(lane >> 4);
+                    *(u32x4v*)&ring[(h * kGroups + G) * 64 + 4 * (lane & 15u)] = w[i];
+                }
+            };
+#else
             auto fill = [&](int r0, int h) {
                 uint32_t w[kLwSteps][kBlock / 64][A];
 #pragma unroll
@@ -365,6 +391,7 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void oc_step_n_
                         for (int a = 0; a < A; ++a)
                             ring[(((h * kLwSteps + q) * (kBlock / 64) + v) * A + a) * 64 + lane] = w[q][v][a];
             };
+#endif
             fill(0, 0);
             for (int r0 = 0; r0 < n; r0 += kLwSteps) {
                 lds_barrier();  // half (r0 / kLwSteps) & 1 is full; the other one has been read
