@@ -110,7 +110,10 @@ __device__ __forceinline__ uint32_t bld32(__amdgpu_buffer_rsrc_t r, uint32_t vof
 // (tools/stepexp.hip: 4.3 vs 5.2-5.3 us/step at 2^20 envs; sc1 5.3).
 constexpr int kCPsc1 = 16, kCPnt = 2;
 #ifndef OC_STEP_CP
-#define OC_STEP_CP kCPsc1  // oc_step's store policy (an A/B switch: tools/step_ab.py --per-step)
+// oc_step's store policy.  nt measured slower for it (hipGraphs of 20 oc_step launches,
+// tools/step_ab.py --per-step, profiles/r04/perstep_nt/: 8.03 vs 8.9-9.5 us/step at A = 2,
+// 9.4-9.5 vs 12.0-12.2 at A = 3, same outputs), so oc_step keeps sc1.
+#define OC_STEP_CP kCPsc1
 #endif
 template <int CP = 0>
 __device__ __forceinline__ void bst32(__amdgpu_buffer_rsrc_t r, uint32_t v, uint32_t voff, uint32_t soff) {
@@ -287,13 +290,13 @@ __host__ __device__ constexpr int64_t ticket_base(int64_t stat_rows) {
 #ifndef OC_LW_STEPS
 #define OC_LW_STEPS 4
 #endif
-#ifndef OC_LW_X4
-#define OC_LW_X4 0  // the loader's action loads as 16-byte loads (an A/B switch)
-#endif
+
 // Also measured and dropped (round 4, profiles/r04/lw_stagger/): a staggered hand-over, the odd
 // stepping waves meeting batch k's barrier between the compute and the stores of step 4k - 1
 // (so that at each release the even waves compute while the odd ones store): 6.46-6.51 us/step
-// against 6.04-6.07, four alternating rounds on one box, C3 parity tests green on it.
+// against 6.04-6.07, four alternating rounds on one box, C3 parity tests green on it; and the
+// loader's loads as 16-byte loads (16 lanes per 256-byte group, a quarter of the load and LDS
+// write instructions): 6.18-6.29 against 6.05-6.12 (profiles/r04/lw_x4/).
 constexpr int kLwSteps = OC_LW_STEPS;  // steps per ring half (one barrier per kLwSteps steps)
 // A = 3 only: there the stepping waves' drains were a fifth of the time (C3, 100-step launches,
 // one box: 6.42 -> 6.07 us/step, outputs identical).  At A <= 2 the step is store-bound and the
@@ -320,7 +323,7 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void oc_step_n_
     __shared__ uint32_t waves_done;
     __shared__ unsigned long long fold[OC_NSTATS][64 + 8];  // the folding wave's partial sums
     // LW: [half][step of the batch][stepping wave][agent][lane] action words
-    __shared__ __attribute__((aligned(16))) uint32_t ring[LW ? 2 * kLwSteps * (kBlock / 64) * A * 64 : 1];
+    __shared__ uint32_t ring[LW ? 2 * kLwSteps * (kBlock / 64) * A * 64 : 1];
     if (threadIdx.x < 64u) tbl4[threadIdx.x] = L.cls4[threadIdx.x];
     if (threadIdx.x == 0u) waves_done = 0u;
     __syncthreads();
@@ -349,29 +352,6 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void oc_step_n_
         if (loader) {
             // the action words of steps r0 .. r0 + kLwSteps - 1 (those < n) into ring half h;
             // this wave issues no store, so its waits are for its own loads only
-#if OC_LW_X4
-            // 16-byte loads: a (step, stepping wave, agent) group is 64 lanes' words = 256 B,
-            // contiguous in the actions and in the ring, so 16 lanes move one group and a wave
-            // instruction four; the whole offset is in the VGPR (the four groups differ in step
-            // and agent).  Past the last step the range check returns zeros.
-            typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-            constexpr int kGroups = kLwSteps * (kBlock / 64) * A;
-            auto fill = [&](int r0, int h) {
-                u32x4v w[kGroups / 4];
-#pragma unroll
-                for (int i = 0; i < kGroups / 4; ++i) {
-                    const int G = 4 * i + (int)(lane >> 4);
-                    const int q = G / ((kBlock / 64) * A), v = (G / A) % (kBlock / 64), a = G % A;
-                    const uint32_t off = (uint32_t)((r0 + q) * A + a) * P + (gb + 64u * v) * 4u + 16u * (lane & 15u);
-                    w[i] = __builtin_amdgcn_raw_buffer_load_b128(b.act, (int)off, 0, LCP);
-                }
-#pragma unroll
-                for (int i = 0; i < kGroups / 4; ++i) {
-                    const int G = 4 * i + (int)(lane >> 4);
-                    *(u32x4v*)&ring[(h * kGroups + G) * 64 + 4 * (lane & 15u)] = w[i];
-                }
-            };
-#else
             auto fill = [&](int r0, int h) {
                 uint32_t w[kLwSteps][kBlock / 64][A];
 #pragma unroll
@@ -391,7 +371,6 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void oc_step_n_
                         for (int a = 0; a < A; ++a)
                             ring[(((h * kLwSteps + q) * (kBlock / 64) + v) * A + a) * 64 + lane] = w[q][v][a];
             };
-#endif
             fill(0, 0);
             for (int r0 = 0; r0 < n; r0 += kLwSteps) {
                 lds_barrier();  // half (r0 / kLwSteps) & 1 is full; the other one has been read
@@ -811,24 +790,127 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
 // (configurations and tables in LDS).  Output [subtask][pitch], so each store instruction of a
 // wave covers 64 consecutive envs of one configuration.  Chunking the table multiplies the
 // waves of a launch: the walk is LDS-latency bound and one chunk left 4 waves per SIMD.
+#ifndef OC_BOUNDS_COMPACT
+#define OC_BOUNDS_COMPACT 1
+#endif
+// Inclusive prefix sum over the wave: wave_sum's scan without its final read.
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src); }
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    return (uint64_t)shfl32((uint32_t)v, src) | ((uint64_t)shfl32((uint32_t)(v >> 32), src) << 32);
+}
+__device__ __forceinline__ int kth_bit(uint32_t set, int k) {  // the k-th set bit (k < popcount)
+    for (int q = 0; q < k; ++q) set &= set - 1u;
+    return __builtin_ctz(set);
+}
+// LDS ordering between the lanes of one wave (its LDS operations run in order; this keeps the
+// compiler from moving them and waits for the outstanding ones)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// One lane per env, every configuration of the block's chunk.  The bound is a min over the
+// env's A locations (Chop, Deliver: bound_static per location) or its (A, B) location pairs
+// (Merge: helper per pair), whose count depends on where the items are: walked per lane, lanes
+// with fewer locations idle while the others finish (0.58 of the lanes active per VALU
+// instruction, profiles/r04/c5/pmc_c5.json).  Compacted (OC_BOUNDS_COMPACT): the wave lists
+// its (env, location or pair) items with a prefix sum of the per-lane counts, and its lanes
+// take them 64 at a time: item j's lane finds the owning env by a binary search over the
+// prefix (shuffles), takes the owner's agent cells, location sets and row words by shuffle,
+// evaluates that one location or pair, and folds it into the owner's minimum with an LDS
+// atomic (the bounds are positive floats, ordered as their bit patterns).  The min is the same
+// whatever the order, so the outputs are identical.
 template <int A, int K, bool W>
 __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                            const uint8_t* __restrict__ blob_g,
                                                            float* __restrict__ lb, uint8_t* __restrict__ doable) {
     extern __shared__ uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
+    __shared__ uint32_t minv[kBlock];
     stage_roll_tables(R, blob_g, blob_w, subs);
     const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
-    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-        const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
+    const int i0 = (int)(blockIdx.y * R.nsub / gridDim.y), i1 = (int)((blockIdx.y + 1) * R.nsub / gridDim.y);
+    if (!OC_BOUNDS_COMPACT) {
+        for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
+            const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
+            ocro::RowOps<A, K, W> ops(R.L, blob);
+            for (int i = i0; i < i1; ++i) {
+                float v;
+                const bool ok = ops.full_bound(r, subs[i], v);
+                lb[i * P + e] = v;
+                doable[i * P + e] = ok ? 1 : 0;
+            }
+        }
+        return;
+    }
+    const int lane = (int)(threadIdx.x & 63u), wbase = (int)(threadIdx.x & ~63u);
+    const float per = (float)R.L.perimeter;
+    // wave-uniform env loop: every lane of the wave runs the shuffles
+    for (int64_t e0 = blockIdx.x * (int64_t)kBlock + wbase; e0 < R.B; e0 += (int64_t)gridDim.x * kBlock) {
+        const int64_t e = e0 + lane;
+        const bool valid = e < R.B;
+        const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, valid ? e : e0);
         ocro::RowOps<A, K, W> ops(R.L, blob);
-        const int i0 = (int)(blockIdx.y * R.nsub / gridDim.y), i1 = (int)((blockIdx.y + 1) * R.nsub / gridDim.y);
         for (int i = i0; i < i1; ++i) {
-            float v;
-            const bool ok = ops.full_bound(r, subs[i], v);
-            lb[i * P + e] = v;
-            doable[i * P + e] = ok ? 1 : 0;
+            const ocro::Sub& s = subs[i];
+            ops.bound_config(s);
+            int ag0, ag1;
+            float pen;
+            ops.bound_agents(r, s, ag0, ag1, pen);
+            const bool walk = valid && (s.kind == 1 || s.kind == 2 || s.kind == 3);
+            const uint32_t setA = walk ? ops.obj_set(r, s.start[0], s.kind == 3) : 0u;
+            const uint32_t setB = walk && s.kind == 2 ? ops.obj_set(r, s.start[1], false) : 0u;
+            const uint32_t cnt = s.kind == 2 ? __popc(setA) * __popc(setB) : __popc(setA);
+            const uint32_t incl = wave_scan(cnt), off = incl - cnt;
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            minv[threadIdx.x] = __float_as_uint(per + 1.0f);
+            wave_lds_sync();
+            const int bl = s.kind == 1 ? R.L.cut_off : R.L.deliv_off;
+            const int nb = s.kind == 1 ? R.L.ncut : R.L.ndeliv;
+            const uint8_t* dm = blob + R.L.dmin_off + (s.kind == 1 ? 0 : R.L.nnodes);
+            for (uint32_t base = 0; base < total; base += 64u) {  // wave-uniform
+                const uint32_t j = base + (uint32_t)lane;
+                int own = 0;  // the last lane whose offset is <= j: item j's env
+#pragma unroll
+                for (int stp = 32; stp > 0; stp >>= 1) own = shfl32(off, own + stp) <= j ? own + stp : own;
+                const uint32_t t = j - shfl32(off, own);
+                const uint32_t oA = shfl32(setA, own), oB = shfl32(setB, own);
+                const int oag0 = (int)shfl32((uint32_t)ag0, own), oag1 = (int)shfl32((uint32_t)ag1, own);
+                ocro::RowT<K, W> ro;  // the owner's cells: agent x / y and item locations
+                ro.x = shfl32(r.x, own);
+                ro.y = shfl32(r.y, own);
+#pragma unroll
+                for (int q = 0; q < ocro::RowT<K, W>::NL; ++q) ro.loc[q] = shfl64(r.loc[q], own);
+                if (j < total) {
+                    float b;
+                    if (s.kind == 2) {
+                        const uint32_t ncB = (uint32_t)__popc(oB);
+                        const int Ac = ops.src_cell(ro, kth_bit(oA, (int)(t / ncB)));
+                        const int Bc = ops.src_cell(ro, kth_bit(oB, (int)(t % ncB)));
+                        b = ops.helper(s, oag0, oag1, Ac, Bc);
+                    } else {
+                        b = ops.helper_static(s, oag0, oag1, ops.src_cell(ro, kth_bit(oA, (int)t)), bl, nb, dm);
+                    }
+                    atomicMin(&minv[wbase + own], __float_as_uint(b));
+                }
+            }
+            wave_lds_sync();
+            const float d = __uint_as_float(minv[threadIdx.x]);
+            if (valid) {
+                lb[i * P + e] = d + pen;
+                doable[i * P + e] = (s.kind == 0 || d < per) ? 1 : 0;
+            }
         }
     }
 }

@@ -646,9 +646,12 @@ struct RowOps {
 
     // The same, split: returns World.get_lower_bound_between's distance (world.py:115-146) and
     // sets `pen` to the holding penalty (overcooked_environment.py:611-640).
-    OC_RH float lower_bound_parts(const Row& r, const Sub& s, float& pen) const {
+    // Its head: the subtask agents' cells (ag0 the first active agent's, ag1 the second's) and
+    // the holding penalty.
+    OC_RH void bound_agents(const Row& r, const Sub& s, int& ag0, int& ag1, float& pen) const {
         pen = 0.0f;
-        int ag0 = 0, ag1 = 0, na = 0;
+        ag0 = ag1 = 0;
+        int na = 0;
 #pragma unroll
         for (int a = 0; a < A; ++a) {
             if (!((active >> a) & 1u)) continue;
@@ -657,6 +660,18 @@ struct RowOps {
             const int h = r.ah(a);
             if (h != kNone && s.kind != 2 && r.im(h) != s.start[0] && r.im(h) != s.goal) pen = 1.0f;
         }
+    }
+    // full_bound's configuration of this object: no Level-0 view, the subtask agents active
+    OC_RH void bound_config(const Sub& s) {
+        ac = kNoAc;
+        active = 1u << s.agent[0];
+        if (s.n == 2) active |= 1u << s.agent[1];
+        blockers = active;
+    }
+
+    OC_RH float lower_bound_parts(const Row& r, const Sub& s, float& pen) const {
+        int ag0, ag1;
+        bound_agents(r, s, ag0, ag1, pen);
         float lower = (float)L.perimeter + 1.0f;
         if (s.kind == 1 || s.kind == 3) {  // static B side: one table lookup per A approach
             const int bl = s.kind == 1 ? L.cut_off : L.deliv_off;
@@ -681,10 +696,7 @@ struct RowOps {
     // given_objs; returns BayesianDelegator.subtask_alloc_is_doable (bayesian_delegator.py:98-156):
     // None -> true, else the distance < world.perimeter.
     OC_RH bool full_bound(const Row& r, const Sub& s, float& lb) {
-        ac = kNoAc;
-        active = 1u << s.agent[0];
-        if (s.n == 2) active |= 1u << s.agent[1];
-        blockers = active;
+        bound_config(s);
         float pen;
         const float d = lower_bound_parts(r, s, pen);
         lb = d + pen;
