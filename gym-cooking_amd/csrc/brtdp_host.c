@@ -23,6 +23,7 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <math.h>
+#include <stdint.h>
 #include <string.h>
 
 /* v[k] as a double; NULL (with KeyError set) when absent */
@@ -88,9 +89,27 @@ static int has_key_h(PyObject* d, PyObject* k, const char* h, Py_ssize_t i) {
     return h == NULL ? PyDict_Contains(d, k) : _PyDict_Contains_KnownHash(d, k, hash_at(h, i));
 }
 
+/* numpy's bit-generator interface (numpy/random/bitgen.h): a legacy RandomState's
+ * random_sample() returns next_double(state) of its bit generator. */
+typedef struct {
+    void* state;
+    uint64_t (*next_uint64)(void* st);
+    uint32_t (*next_uint32)(void* st);
+    double (*next_double)(void* st);
+    uint64_t (*next_raw)(void* st);
+} bitgen_t;
+
 /* One uniform double from the tie-break generator (RandomState.random_sample: MT19937's
- * next_double, the variate numpy's legacy binomial reads); -1 on error. */
+ * next_double, the variate numpy's legacy binomial reads); -1 on error.  `sample` is the bound
+ * random_sample, or the generator's "BitGenerator" capsule (planner._sampler), whose
+ * next_double is the very function random_sample calls: the same stream without a Python call. */
 static int uniform(PyObject* sample, double* u) {
+    if (PyCapsule_CheckExact(sample)) {
+        bitgen_t* bg = (bitgen_t*)PyCapsule_GetPointer(sample, "BitGenerator");
+        if (bg == NULL) return -1;
+        *u = bg->next_double(bg->state);
+        return 0;
+    }
     PyObject* r = PyObject_CallNoArgs(sample);
     if (r == NULL) return -1;
     *u = PyFloat_AsDouble(r);
@@ -359,11 +378,8 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         }
         Py_ssize_t pick = im;
         if (!err && nmin == 1) {
-            if (im != n - 1) {
-                PyObject* r = PyObject_CallNoArgs(sample);
-                if (r == NULL) err = 1;
-                Py_XDECREF(r);
-            }
+            double u;
+            if (im != n - 1 && uniform(sample, &u) < 0) err = 1;
         } else if (!err) {  /* ties: the multinomial draw of planner.argmin */
             char mins_stack[32];
             char* mins = n <= 32 ? mins_stack : (char*)PyMem_Malloc((size_t)n);

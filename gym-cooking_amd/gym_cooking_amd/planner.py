@@ -182,6 +182,19 @@ def argmin(vector, rng=np.random):
     return np.where(rng.multinomial(1, e_x / e_x.sum()))[0][0]
 
 
+def _sampler(rng):
+    """What the native loop draws its uniforms with: for a legacy RandomState over MT19937 (the
+    reference's np.random, or a batched search's RandomState(seed)) its bit generator's capsule
+    -- brtdp_host.c calls the capsule's next_double, the function random_sample() itself calls,
+    so the stream is the same -- else the bound random_sample."""
+    rs = np.random.mtrand._rand if rng is np.random else rng
+    if type(rs) is np.random.RandomState:
+        cap = getattr(getattr(rs, "_bit_generator", None), "capsule", None)
+        if cap is not None:
+            return cap
+    return rng.random_sample
+
+
 def _argmin_plan(vector: list):
     """What argmin(vector, rng) draws and returns, as data: (index, None) for a unique minimum,
     (None, tie mask) for ties.  Lets a caller that meets the same Q vector again replay the
@@ -876,6 +889,8 @@ class E2E_BRTDP:
         _native.backprop(v_u, v_l, traj, ents)
 
     def _main(self):  # main
+        if _native is not None and not self._level and self.use_native:
+            return (yield from self._main_native())
         main_counter = 0
         sk = (self._repr(self.start), self._sub_key)
         diff = self.v_u[sk] - self.v_l[sk]
@@ -883,6 +898,35 @@ class E2E_BRTDP:
             diff = self.v_u[sk] - self.v_l[sk]
             main_counter += 1
             yield from self._sample_trial()
+
+    def _main_native(self):
+        """main() at Level 0 with _sample_trial_native inlined: one generator for all of a
+        search's trials, the loop's constants bound once (none of them changes while it runs)."""
+        sk = self._sub_key
+        succ, v_u, v_l = self._succ, self.v_u, self.v_l
+        rs = (self._repr(self.start), sk)
+        sample = _sampler(self._rng)
+        tc = self.time_cost + self.action_cost
+        cand = _CAND[len(self._agents)]
+        fwd, backprop, expanded = _native.forward, _native.backprop, self._expanded
+        cap, tau, alpha, main_cap, start, sub = self.cap, self.tau, self.alpha, self.main_cap, self.start, self._sub
+        main_counter = 0
+        diff = v_u[rs] - v_l[rs]
+        while diff > alpha and main_counter < main_cap:
+            diff = v_u[rs] - v_l[rs]
+            main_counter += 1
+            traj, ents = [], []
+            x, counter, resume = start, 0, False
+            while True:
+                st, x, counter, i = fwd(succ, v_u, v_l, x, sk, rs, cap, counter, tau, traj, sample, resume, ents, tc)
+                if st == 0:
+                    break
+                if st == 2:  # get_expected_diff's T raises (or _init_succ's, on the first crashing successor)
+                    _raise_copy_crash(succ[(x, sk)][0][i])
+                res = yield (np.frombuffer(x[0], np.uint8), cand, sub)  # st == 1: _need(x)
+                expanded(x, cand, res)
+                resume = True
+            backprop(v_u, v_l, traj, ents)
 
     def _next_action(self, env, subtask, subtask_agent_names, other_agent_planners):
         yield from self._configure_gen(self._configure(env, subtask, subtask_agent_names, other_agent_planners))

@@ -316,3 +316,26 @@ def test_native_errors_raise_python_exceptions():
     got[5][1] = 1.0
     nat.init_succ(got, v_l, v_u, 1.1)
     assert got[6] is True and v_l["b"] == 1.0 * 1.1 - 1.09 and v_u["c"] == 3.0 * 1.1 * 5 * 1.1
+
+
+def test_native_sampler_draws_the_same_stream():
+    """planner._sampler hands the native loop the generator's bit-generator capsule: its draws
+    (tie picks) and the generator's position afterwards equal those through random_sample, for a
+    RandomState and for numpy's global generator (the reference's np.random)."""
+    from gym_cooking_amd import planner as pl
+    nat = pl._native
+    assert nat is not None, "the _brtdp extension is not built (make -C gym-cooking_amd/csrc)"
+    masks = [[True, False, True, True], [False, True], [True] * 7, [False, False, True]]
+    for make in (lambda: np.random.RandomState(11), lambda: (np.random.seed(11), np.random)[1]):
+        r1 = make()
+        assert type(pl._sampler(r1)).__name__ == "PyCapsule"
+        a = [nat.tie_pick(m, pl._sampler(r1)) for m in masks * 20]
+        x1 = r1.random_sample()
+        r2 = make()
+        b = [nat.tie_pick(m, r2.random_sample) for m in masks * 20]
+        assert a == b and x1 == r2.random_sample()
+    class Other:  # anything else: its random_sample
+        def random_sample(self):
+            return 0.25
+    o = Other()
+    assert pl._sampler(o) == o.random_sample
