@@ -564,9 +564,6 @@ def main() -> int:
     ap.add_argument("--kernel-replay-ms", type=float, default=20.0,
                     help="after the timed region, replay its launches back to back for about this long between "
                          "two HIP events to measure the dominant kernel's mean launch duration")
-    ap.add_argument("--prime", choices=("none", "step"), default="none",
-                    help="step: one untimed 1-step oc_step_n launch on scratch buffers right before the window "
-                         "(the kernel's code and the device's queues warm, the window's inputs untouched)")
     ap.add_argument("--window-actions", choices=("fresh", "replay"), default="fresh",
                     help="fresh: the window's actions are written by gen_actions just before it; replay: the "
                          "window's launches run once, untimed, just before it (both leave them cache-resident)")
@@ -690,9 +687,6 @@ def main() -> int:
         for f in timed:
             f()
     stats.zero_()
-    if args.prime == "step":  # reads the window's start state, writes scratch only
-        p_traj, p_ex, p_coll = outs[1]
-        eb.step_n_launcher(s_a, p_traj[:S], acts_w[0].reshape(-1), 1, p_traj[:S], p_ex, p_coll, eb.new_stats())()
     torch.cuda.synchronize()
 
     # ---------------- timed region ----------------
@@ -788,8 +782,6 @@ def main() -> int:
             "window_actions": ("written by gen_actions just before the window (untimed)" if args.window_actions == "fresh"
                                else "read by an untimed run of the window's launches just before it") +
                               "; the warmup steps another stream",
-            "window_primed": ("one untimed 1-step launch on scratch buffers just before the window"
-                              if args.prime == "step" else None),
         },
         "open_loop": True,
         "window_cold_actions": {

@@ -791,7 +791,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
 // wave covers 64 consecutive envs of one configuration.  Chunking the table multiplies the
 // waves of a launch: the walk is LDS-latency bound and one chunk left 4 waves per SIMD.
 #ifndef OC_BOUNDS_COMPACT
-#define OC_BOUNDS_COMPACT 1
+#define OC_BOUNDS_COMPACT 0  // the wave-compacted walk below: parity-green, measured slower (off)
 #endif
 // Inclusive prefix sum over the wave: wave_sum's scan without its final read.
 __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
@@ -829,7 +829,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 // prefix (shuffles), takes the owner's agent cells, location sets and row words by shuffle,
 // evaluates that one location or pair, and folds it into the owner's minimum with an LDS
 // atomic (the bounds are positive floats, ordered as their bit patterns).  The min is the same
-// whatever the order, so the outputs are identical.
+// whatever the order, so the outputs are identical (round 4, profiles/r04/bounds_compact/: the
+// same output digest, the GPU suite green on it).  It lifts the lanes active per VALU
+// instruction from 0.58 to 0.70 but runs 0.129-0.130 ms against 0.118-0.119 at C5: most
+// (env, configuration) pairs have 0 or 1 location, so the walk has little divergence to remove,
+// and the prefix sum, the owner search (shuffles) and the LDS fold cost more VALU and LDS
+// instructions per wave (925 / 98 against 869 / 65) than the idle lanes did.  So it is off.
 template <int A, int K, bool W>
 __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                            const uint8_t* __restrict__ blob_g,
