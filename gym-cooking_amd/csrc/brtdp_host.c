@@ -17,6 +17,9 @@
  *   hashes of [3]'s keys, of [8] and of the successors' (state key, subtask) _succ keys, as a
  *   bytes of 2n+1 Py_hash_t -- the loops below look values up with them instead of hashing a
  *   nested tuple per lookup (the dicts are the same; a hash is a pure function of the key).
+ *   [10] (entries built by expand) the successors' entries as forward meets them (None until
+ *   then): the _succ entry of (successor, subtask) never changes once made, so a trial's next
+ *   step takes it from here instead of a table lookup.
  * expand interns the value keys it builds in the planner's key table, so that the keys stored
  * in v_l / v_u and the ones looked up are mostly one object (a dict compares those by identity).
  */
@@ -318,6 +321,8 @@ static PyObject* forward(PyObject* self, PyObject* args) {
     char rsb[sizeof(Py_hash_t)];
     memcpy(rsb, &rsh, sizeof rsh);
     Py_hash_t xh = -1;  /* hash of (x, sk) when known from the parent's entry */
+    PyObject* links = NULL;  /* the parent's successor-entry list ([10]) and x's slot in it */
+    Py_ssize_t link = -1;
     Py_INCREF(x);
     for (;;) {
         if (!resume) {
@@ -326,12 +331,20 @@ static PyObject* forward(PyObject* self, PyObject* args) {
             if (PyList_Append(traj, x) < 0) goto fail;
         }
         resume = 0;
-        PyObject* key = PyTuple_Pack(2, x, sk);
-        if (key == NULL) goto fail;
-        PyObject* got = xh != -1 ? _PyDict_GetItem_KnownHash(succ, key, xh) : PyDict_GetItemWithError(succ, key);
-        Py_DECREF(key);
-        if (got == NULL && PyErr_Occurred()) goto fail;
-        if (got == NULL) return Py_BuildValue("(iNli)", 1, x, counter, -1);
+        PyObject* got = links != NULL ? PyList_GET_ITEM(links, link) : Py_None;
+        if (got == Py_None) {
+            PyObject* key = PyTuple_Pack(2, x, sk);
+            if (key == NULL) goto fail;
+            got = xh != -1 ? _PyDict_GetItem_KnownHash(succ, key, xh) : PyDict_GetItemWithError(succ, key);
+            Py_DECREF(key);
+            if (got == NULL && PyErr_Occurred()) goto fail;
+            if (got == NULL) return Py_BuildValue("(iNli)", 1, x, counter, -1);
+            if (links != NULL) {  /* remember it in the parent's entry */
+                Py_INCREF(got);
+                PyList_SetItem(links, link, got);  /* steals; drops the None */
+            }
+        }
+        links = NULL;
         if (PyList_Append(ents, got) < 0) goto fail;
         PyObject* crash = PyList_GET_ITEM(got, 7);
         if (PyList_GET_ITEM(got, 6) != Py_True) {
@@ -414,6 +427,11 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         if (B <= diff) break;
         PyObject* nx = PyList_GET_ITEM(PyList_GET_ITEM(got, 1), pick);
         xh = hs != NULL ? hash_at(hs, n + 1 + pick) : -1;
+        if (PyList_GET_SIZE(got) > 10 && PyList_Check(PyList_GET_ITEM(got, 10)) &&
+            PyList_GET_SIZE(PyList_GET_ITEM(got, 10)) == n) {
+            links = PyList_GET_ITEM(got, 10);
+            link = pick;
+        }
         Py_INCREF(nx);
         Py_DECREF(x);
         x = nx;
@@ -424,22 +442,31 @@ fail:
     return NULL;
 }
 
-/* expand(rows, fl, lb, cand, key, sk, m0, K, A, cost, changed, keys) -> entry, illegal
+/* expand(rows, fl, lb, cand, key, sk, m0, K, A, cost, changed, keys[, succ, illegal_tbl])
+ *   -> (entry, illegal), or None when it stores them itself
  * planner.E2E_BRTDP._expanded over one expansion's rollout rows (e2e_brtdp.py:103-206: T,
  * get_actions; value_init's inputs): rows = the successors' state bytes [n][NP] (a buffer),
  * fl = their u8 flags, lb = their f32 bounds, cand = the candidate joint actions in get_actions
  * order, key = (state bytes, group names, agents, Level).  A row whose item masks changed (a
- * chop or a merge) goes through changed(bytes) -> (canonical bytes, group names) in Python.
+ * chop or a merge) goes through changed(bytes, group names) -> (canonical bytes, group names)
+ * in Python.  With `succ` and `illegal_tbl` (dicts) it stores the entry as succ[(key, sk)] and
+ * the illegal candidates as illegal_tbl[(key, sk)] = (illegal, rows, NP, fl), as
+ * planner._expanded_native does, and returns None.
  * keys: the planner's key table (a dict; None: no interning) -- every value key built here is
  * replaced by the table's equal key, if it has one.
  * Returns the _succ entry (without its initialised flag set; with its hashes, [9]) and
  * {action: row} of the illegal candidates (or None). */
 static PyObject* expand(PyObject* self, PyObject* args) {
-    PyObject *rows_o, *fl_o, *lb_o, *cand, *key, *sk, *cost, *changed, *keys;
+    PyObject *rows_o, *fl_o, *lb_o, *cand, *key, *sk, *cost, *changed, *keys, *store = Py_None, *ill_tbl = Py_None;
     Py_ssize_t m0, K, A;
-    if (!PyArg_ParseTuple(args, "OOOO!O!OnnnO!OO", &rows_o, &fl_o, &lb_o, &PyList_Type, &cand, &PyTuple_Type, &key, &sk,
-                          &m0, &K, &A, &PyDict_Type, &cost, &changed, &keys))
+    if (!PyArg_ParseTuple(args, "OOOO!O!OnnnO!OO|OO", &rows_o, &fl_o, &lb_o, &PyList_Type, &cand, &PyTuple_Type, &key,
+                          &sk, &m0, &K, &A, &PyDict_Type, &cost, &changed, &keys, &store, &ill_tbl))
         return NULL;
+    if ((store != Py_None && !PyDict_Check(store)) || (ill_tbl != Py_None && !PyDict_Check(ill_tbl)) ||
+        ((store == Py_None) != (ill_tbl == Py_None))) {
+        PyErr_SetString(PyExc_TypeError, "expand: succ and illegal_tbl must both be dicts or both be absent");
+        return NULL;
+    }
     if (keys != Py_None && !PyDict_Check(keys)) {
         PyErr_SetString(PyExc_TypeError, "expand: keys must be a dict or None");
         return NULL;
@@ -456,7 +483,7 @@ static PyObject* expand(PyObject* self, PyObject* args) {
         return NULL;
     }
     PyObject *actions = NULL, *succ = NULL, *costs = NULL, *vks = NULL, *goals = NULL, *lbs = NULL, *crash = NULL,
-             *illegal = NULL, *out = NULL, *ra = NULL, *self_vk = NULL, *self_r = NULL, *hb = NULL;
+             *illegal = NULL, *out = NULL, *ra = NULL, *self_vk = NULL, *self_r = NULL, *hb = NULL, *links = NULL;
     Py_hash_t* hv = NULL;  /* the value keys' hashes, then the _succ keys' */
     Py_ssize_t m = 0;      /* legal successors so far */
     PyObject *sb = PyTuple_GET_ITEM(key, 0), *groups = PyTuple_GET_ITEM(key, 1), *agents = PyTuple_GET_ITEM(key, 2),
@@ -508,7 +535,7 @@ static PyObject* expand(PyObject* self, PyObject* args) {
         if (memcmp(row + m0, pm, (size_t)K) != 0) {  /* a chop or a merge */
             PyObject* b = PyBytes_FromStringAndSize((const char*)row, NP);
             if (b == NULL) goto done;
-            PyObject* t = PyObject_CallOneArg(changed, b);
+            PyObject* t = PyObject_CallFunctionObjArgs(changed, b, groups, NULL);
             Py_DECREF(b);
             if (t == NULL) goto done;
             ns = PyTuple_GetItem(t, 0);
@@ -606,8 +633,28 @@ static PyObject* expand(PyObject* self, PyObject* args) {
     memmove(hv + m + 1, hv + n + 1, sizeof(Py_hash_t) * (size_t)m);  /* compact: [m value keys, self, m _succ keys] */
     hb = PyBytes_FromStringAndSize((const char*)hv, (Py_ssize_t)sizeof(Py_hash_t) * (2 * m + 1));
     if (hb == NULL) goto done;
-    out = Py_BuildValue("([OOOOOOOOOO]O)", actions, succ, costs, vks, goals, lbs, Py_False, crash ? crash : Py_None,
-                        self_vk, hb, illegal ? illegal : Py_None);
+    if ((links = PyList_New(m)) == NULL) goto done;
+    for (Py_ssize_t i = 0; i < m; ++i) {
+        Py_INCREF(Py_None);
+        PyList_SET_ITEM(links, i, Py_None);
+    }
+    out = Py_BuildValue("([OOOOOOOOOOO]O)", actions, succ, costs, vks, goals, lbs, Py_False, crash ? crash : Py_None,
+                        self_vk, hb, links, illegal ? illegal : Py_None);
+    if (out != NULL && store != Py_None) {  /* store them: succ[(key, sk)], illegal_tbl[(key, sk)] */
+        PyObject* k2 = PyTuple_Pack(2, key, sk);
+        int bad = k2 == NULL || PyDict_SetItem(store, k2, PyTuple_GET_ITEM(out, 0)) < 0;
+        if (!bad && illegal != NULL) {
+            PyObject* rec = Py_BuildValue("(OOnO)", illegal, rows_o, NP, fl_o);
+            bad = rec == NULL || PyDict_SetItem(ill_tbl, k2, rec) < 0;
+            Py_XDECREF(rec);
+        }
+        Py_XDECREF(k2);
+        Py_CLEAR(out);
+        if (!bad) {
+            Py_INCREF(Py_None);
+            out = Py_None;
+        }
+    }
 done:
     Py_XDECREF(actions);
     Py_XDECREF(succ);
@@ -621,6 +668,7 @@ done:
     Py_XDECREF(self_r);
     Py_XDECREF(self_vk);
     Py_XDECREF(hb);
+    Py_XDECREF(links);
     PyMem_Free(hv);
     PyBuffer_Release(&rb);
     PyBuffer_Release(&fb);

@@ -32,6 +32,7 @@ e2e_brtdp.py:842-878), drawing the same random numbers as the reference.
 from __future__ import annotations
 
 import contextlib
+import functools
 import gc
 import itertools
 import types
@@ -377,6 +378,13 @@ class _Expander:
         return [(nxt[s0:s0 + c], fl[s0:s0 + c], lb[s0:s0 + c]) for s0, c in zip(starts.tolist(), counts.tolist())]
 
 
+def _changed_row(A: int, K: int, enc: int, wide: bool, m0: int, ns: bytes, groups: FrozenSet[str]):
+    """A successor row whose item masks changed (a chop or a merge): its canonical bytes and
+    its group names, plus a merge's new object group (world.py:304-306)."""
+    ns = _canon(ns, A, K, enc, wide)
+    return ns, groups | frozenset(_group_name(m, enc) for m, l in zip(ns[m0:m0 + K], _live(ns, A, K, wide)) if l)
+
+
 def _copy_crashes(sb: bytes, A: int) -> bool:
     """Two agents on one square that both hold an item: the reference's copy of such a state
     raises (overcooked_environment.py:108-113 -> world.py:417).  At Level 1 every agent is in the
@@ -660,22 +668,25 @@ class E2E_BRTDP:
         if illegal:  # what T would do with them (only asked for by taken_action_error): decoded there
             self._illegal[(key, sk)] = (illegal, raw, NP, fl)
 
-    def _expanded_native(self, key, cand, nxt, fl, lb) -> None:
-        """_expanded with the row loop in C (_brtdp.expand): the same entry, field for field."""
-        groups = key[1]
-        A, K, enc, wide = self._exp.A, self._exp.K, self._exp.enc, self._exp.wide
-        l0, lh, m0 = _lay(A, K, wide)
+    def _native_expander(self):
+        """(m0, changed) of _brtdp.expand for this planner's expander: the item-mask plane
+        offset and the callback for a row whose masks changed (a chop or a merge: canonical slot
+        order, a merge's new object group), kept per expander."""
+        exp = self._exp
+        got = exp.__dict__.get("_native_x")
+        if got is None:
+            A, K, enc, wide = exp.A, exp.K, exp.enc, exp.wide
+            m0 = _lay(A, K, wide)[2]
+            got = exp.__dict__["_native_x"] = (m0, functools.partial(_changed_row, A, K, enc, wide, m0))
+        return got
 
-        def changed(ns):  # a chop or a merge: canonical slot order, a merge's new object group
-            ns = _canon(ns, A, K, enc, wide)
-            return ns, groups | frozenset(_group_name(m, enc) for m, l in zip(ns[m0:m0 + K], _live(ns, A, K, wide)) if l)
-        sk = self._sub_key
-        nxt = np.ascontiguousarray(nxt)
-        entry, illegal = _native.expand(nxt, np.ascontiguousarray(fl), np.ascontiguousarray(lb), cand, key, sk, m0, K,
-                                        A, _COST, changed, self.__dict__.get("_vkeys"))
-        self._succ[(key, sk)] = entry
-        if illegal:
-            self._illegal[(key, sk)] = (illegal, nxt.reshape(-1), len(key[0]), fl)
+    def _expanded_native(self, key, cand, nxt, fl, lb) -> None:
+        """_expanded with the row loop in C (_brtdp.expand, which also stores the entry and the
+        illegal candidates): the same entry, field for field."""
+        m0, changed = self._native_expander()
+        _native.expand(np.ascontiguousarray(nxt), np.ascontiguousarray(fl), np.ascontiguousarray(lb), cand, key,
+                       self._sub_key, m0, self._exp.K, self._exp.A, _COST, changed, self.__dict__.get("_vkeys"),
+                       self._succ, self._illegal)
 
     def _drive(self, gen):
         """Run a search generator to completion, one launch per request."""
@@ -909,6 +920,9 @@ class E2E_BRTDP:
         tc = self.time_cost + self.action_cost
         cand = _CAND[len(self._agents)]
         fwd, backprop, expanded = _native.forward, _native.backprop, self._expanded
+        m0, changed = self._native_expander()
+        K, A, expand, vkeys, ill_tbl = self._exp.K, self._exp.A, _native.expand, self.__dict__.get("_vkeys"), self._illegal
+        u8, f32 = np.dtype(np.uint8), np.dtype(np.float32)
         cap, tau, alpha, main_cap, start, sub = self.cap, self.tau, self.alpha, self.main_cap, self.start, self._sub
         main_counter = 0
         diff = v_u[rs] - v_l[rs]
@@ -924,7 +938,12 @@ class E2E_BRTDP:
                 if st == 2:  # get_expected_diff's T raises (or _init_succ's, on the first crashing successor)
                     _raise_copy_crash(succ[(x, sk)][0][i])
                 res = yield (np.frombuffer(x[0], np.uint8), cand, sub)  # st == 1: _need(x)
-                expanded(x, cand, res)
+                nxt, fl, lb = res
+                if fl.dtype == u8 and lb.dtype == f32:  # _expanded_native, inlined
+                    expand(np.ascontiguousarray(nxt), np.ascontiguousarray(fl), np.ascontiguousarray(lb), cand, x, sk,
+                           m0, K, A, _COST, changed, vkeys, succ, ill_tbl)
+                else:
+                    expanded(x, cand, res)
                 resume = True
             backprop(v_u, v_l, traj, ents)
 
@@ -975,6 +994,8 @@ class E2E_BRTDP:
         if ill is None or action not in ill[0]:
             return None
         r, raw, NP, fl = ill[0][action], ill[1], ill[2], ill[3]
+        if isinstance(raw, np.ndarray):  # the rows array the native expansion kept, [n, NP]
+            raw = raw.reshape(-1)
         got = {action: (bytes(raw[r * NP:(r + 1) * NP]), int(fl[r]))}
         if (self._repr(key), action) in self._tmemo:  # T answers from its memo; the assert raises
             return AssertionError
