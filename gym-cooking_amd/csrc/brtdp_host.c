@@ -17,9 +17,6 @@
  *   hashes of [3]'s keys, of [8] and of the successors' (state key, subtask) _succ keys, as a
  *   bytes of 2n+1 Py_hash_t -- the loops below look values up with them instead of hashing a
  *   nested tuple per lookup (the dicts are the same; a hash is a pure function of the key).
- *   [10] (entries built by expand) the successors' entries as forward meets them (None until
- *   then): the _succ entry of (successor, subtask) never changes once made, so a trial's next
- *   step takes it from here instead of a table lookup.
  * expand interns the value keys it builds in the planner's key table, so that the keys stored
  * in v_l / v_u and the ones looked up are mostly one object (a dict compares those by identity).
  */
@@ -321,8 +318,6 @@ static PyObject* forward(PyObject* self, PyObject* args) {
     char rsb[sizeof(Py_hash_t)];
     memcpy(rsb, &rsh, sizeof rsh);
     Py_hash_t xh = -1;  /* hash of (x, sk) when known from the parent's entry */
-    PyObject* links = NULL;  /* the parent's successor-entry list ([10]) and x's slot in it */
-    Py_ssize_t link = -1;
     Py_INCREF(x);
     for (;;) {
         if (!resume) {
@@ -331,20 +326,12 @@ static PyObject* forward(PyObject* self, PyObject* args) {
             if (PyList_Append(traj, x) < 0) goto fail;
         }
         resume = 0;
-        PyObject* got = links != NULL ? PyList_GET_ITEM(links, link) : Py_None;
-        if (got == Py_None) {
-            PyObject* key = PyTuple_Pack(2, x, sk);
-            if (key == NULL) goto fail;
-            got = xh != -1 ? _PyDict_GetItem_KnownHash(succ, key, xh) : PyDict_GetItemWithError(succ, key);
-            Py_DECREF(key);
-            if (got == NULL && PyErr_Occurred()) goto fail;
-            if (got == NULL) return Py_BuildValue("(iNli)", 1, x, counter, -1);
-            if (links != NULL) {  /* remember it in the parent's entry */
-                Py_INCREF(got);
-                PyList_SetItem(links, link, got);  /* steals; drops the None */
-            }
-        }
-        links = NULL;
+        PyObject* key = PyTuple_Pack(2, x, sk);
+        if (key == NULL) goto fail;
+        PyObject* got = xh != -1 ? _PyDict_GetItem_KnownHash(succ, key, xh) : PyDict_GetItemWithError(succ, key);
+        Py_DECREF(key);
+        if (got == NULL && PyErr_Occurred()) goto fail;
+        if (got == NULL) return Py_BuildValue("(iNli)", 1, x, counter, -1);
         if (PyList_Append(ents, got) < 0) goto fail;
         PyObject* crash = PyList_GET_ITEM(got, 7);
         if (PyList_GET_ITEM(got, 6) != Py_True) {
@@ -427,11 +414,6 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         if (B <= diff) break;
         PyObject* nx = PyList_GET_ITEM(PyList_GET_ITEM(got, 1), pick);
         xh = hs != NULL ? hash_at(hs, n + 1 + pick) : -1;
-        if (PyList_GET_SIZE(got) > 10 && PyList_Check(PyList_GET_ITEM(got, 10)) &&
-            PyList_GET_SIZE(PyList_GET_ITEM(got, 10)) == n) {
-            links = PyList_GET_ITEM(got, 10);
-            link = pick;
-        }
         Py_INCREF(nx);
         Py_DECREF(x);
         x = nx;
@@ -483,7 +465,7 @@ static PyObject* expand(PyObject* self, PyObject* args) {
         return NULL;
     }
     PyObject *actions = NULL, *succ = NULL, *costs = NULL, *vks = NULL, *goals = NULL, *lbs = NULL, *crash = NULL,
-             *illegal = NULL, *out = NULL, *ra = NULL, *self_vk = NULL, *self_r = NULL, *hb = NULL, *links = NULL;
+             *illegal = NULL, *out = NULL, *ra = NULL, *self_vk = NULL, *self_r = NULL, *hb = NULL;
     Py_hash_t* hv = NULL;  /* the value keys' hashes, then the _succ keys' */
     Py_ssize_t m = 0;      /* legal successors so far */
     PyObject *sb = PyTuple_GET_ITEM(key, 0), *groups = PyTuple_GET_ITEM(key, 1), *agents = PyTuple_GET_ITEM(key, 2),
@@ -553,9 +535,15 @@ static PyObject* expand(PyObject* self, PyObject* args) {
             ng = groups;
             Py_INCREF(ng);
         }
+        /* Keys of bytes, a frozenset of names, ints and strings: no tuple here can be part of a
+         * reference cycle, so the collector is told not to walk them (CPython would untrack them
+         * itself at its first pass over them, after walking each once; a search makes millions). */
         PyObject* nk = PyTuple_Pack(4, ns, ng, agents, lvl_o);
         PyObject* rep = PyTuple_Pack(3, ns, ng, ra);
         PyObject* vk = rep ? PyTuple_Pack(2, rep, sk) : NULL;
+        if (nk) PyObject_GC_UnTrack(nk);
+        if (rep) PyObject_GC_UnTrack(rep);
+        if (vk) PyObject_GC_UnTrack(vk);
         Py_XDECREF(rep);
         const Py_hash_t h1 = vk != NULL ? PyObject_Hash(vk) : -1;
         if (nk != NULL && h1 != -1 && keys != Py_None) {  /* intern */
@@ -633,18 +621,21 @@ static PyObject* expand(PyObject* self, PyObject* args) {
     memmove(hv + m + 1, hv + n + 1, sizeof(Py_hash_t) * (size_t)m);  /* compact: [m value keys, self, m _succ keys] */
     hb = PyBytes_FromStringAndSize((const char*)hv, (Py_ssize_t)sizeof(Py_hash_t) * (2 * m + 1));
     if (hb == NULL) goto done;
-    if ((links = PyList_New(m)) == NULL) goto done;
-    for (Py_ssize_t i = 0; i < m; ++i) {
-        Py_INCREF(Py_None);
-        PyList_SET_ITEM(links, i, Py_None);
+    out = Py_BuildValue("([OOOOOOOOOO]O)", actions, succ, costs, vks, goals, lbs, Py_False, crash ? crash : Py_None,
+                        self_vk, hb, illegal ? illegal : Py_None);
+    if (out != NULL) {  /* the entry and its lists hold no reference back to a container: no cycles */
+        PyObject* e = PyTuple_GET_ITEM(out, 0);
+        for (Py_ssize_t i = 0; i < 6; ++i) PyObject_GC_UnTrack(PyList_GET_ITEM(e, i));
+        PyObject_GC_UnTrack(e);
+        PyObject_GC_UnTrack(self_vk);
     }
-    out = Py_BuildValue("([OOOOOOOOOOO]O)", actions, succ, costs, vks, goals, lbs, Py_False, crash ? crash : Py_None,
-                        self_vk, hb, links, illegal ? illegal : Py_None);
     if (out != NULL && store != Py_None) {  /* store them: succ[(key, sk)], illegal_tbl[(key, sk)] */
         PyObject* k2 = PyTuple_Pack(2, key, sk);
+        if (k2 != NULL) PyObject_GC_UnTrack(k2);  /* (state key, subtask key): no cycle */
         int bad = k2 == NULL || PyDict_SetItem(store, k2, PyTuple_GET_ITEM(out, 0)) < 0;
         if (!bad && illegal != NULL) {
             PyObject* rec = Py_BuildValue("(OOnO)", illegal, rows_o, NP, fl_o);
+            if (rec != NULL) PyObject_GC_UnTrack(rec);
             bad = rec == NULL || PyDict_SetItem(ill_tbl, k2, rec) < 0;
             Py_XDECREF(rec);
         }
@@ -668,7 +659,6 @@ done:
     Py_XDECREF(self_r);
     Py_XDECREF(self_vk);
     Py_XDECREF(hb);
-    Py_XDECREF(links);
     PyMem_Free(hv);
     PyBuffer_Release(&rb);
     PyBuffer_Release(&fb);
