@@ -22,6 +22,7 @@ Run:  python bench.py [--gpus N --steps K --warmup W]
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -576,6 +577,9 @@ def main() -> int:
     ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 (3-agent full-divider_tl) line")
     ap.add_argument("--no-planner", action="store_true", help="skip the secondary navigation-planner line")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--host-wait", choices=("auto", "spin"), default="auto",
+                    help="spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device comes up, so a "
+                         "synchronize spins instead of the runtime's default wait")
     ap.add_argument("--selftest-ranks", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -590,6 +594,10 @@ def main() -> int:
     # when the communicator comes up, so fd 1 goes to stderr and the line to a copy of stdout.
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    if args.host_wait == "spin":  # torch's own HIP runtime, before anything initialises the device
+        hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        if hip.hipSetDevice(ctypes.c_int(local)) != 0 or hip.hipSetDeviceFlags(ctypes.c_uint(1)) != 0:
+            raise SystemExit("hipSetDeviceFlags(hipDeviceScheduleSpin) failed")
     ocdist.init("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -782,6 +790,7 @@ def main() -> int:
             "window_actions": ("written by gen_actions just before the window (untimed)" if args.window_actions == "fresh"
                                else "read by an untimed run of the window's launches just before it") +
                               "; the warmup steps another stream",
+            "host_wait": args.host_wait,
         },
         "open_loop": True,
         "window_cold_actions": {
