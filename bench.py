@@ -577,9 +577,11 @@ def main() -> int:
     ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 (3-agent full-divider_tl) line")
     ap.add_argument("--no-planner", action="store_true", help="skip the secondary navigation-planner line")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    ap.add_argument("--host-wait", choices=("auto", "spin"), default="auto",
-                    help="spin: hipSetDeviceFlags(hipDeviceScheduleSpin) before the device comes up, so a "
-                         "synchronize spins instead of the runtime's default wait")
+    ap.add_argument("--host-wait", choices=("auto", "spin"), default="spin",
+                    help="spin (default): hipSetDeviceFlags(hipDeviceScheduleSpin) before the device comes up, so "
+                         "the window's closing synchronize spins on the completion signal; auto: the runtime's default "
+                         "wait, which let the host see a ~90 us kernel's completion 20-40 us late in some windows "
+                         "(profiles/r04/window_wait/)")
     ap.add_argument("--selftest-ranks", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
