@@ -638,7 +638,7 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
         if (ai < R.nsub) {
             const ocro::Sub& s = subs[ai];
             const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
-            ocro::RowOps<A, K, W> ops(R.L, blob);
+            ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             f = ops.run(r, s, c0, c1, bound);
         }
         store_row<A, K, W>(sout, P, e, r);
@@ -691,7 +691,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
             uint32_t taken = 0;
 #pragma unroll
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
-            ocro::RowOps<A, K, W> ops(R.L, blob);
+            ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             if (s.kind == 0) {
                 f = 0;
                 if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
@@ -849,7 +849,7 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
     if (!OC_BOUNDS_COMPACT) {
         for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
             const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
-            ocro::RowOps<A, K, W> ops(R.L, blob);
+            ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             for (int i = i0; i < i1; ++i) {
                 float v;
                 const bool ok = ops.full_bound(r, subs[i], v);
@@ -866,7 +866,7 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
         const int64_t e = e0 + lane;
         const bool valid = e < R.B;
         const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, valid ? e : e0);
-        ocro::RowOps<A, K, W> ops(R.L, blob);
+        ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
         for (int i = i0; i < i1; ++i) {
             const ocro::Sub& s = subs[i];
             ops.bound_config(s);
@@ -1039,7 +1039,9 @@ struct RenderArgs {
     int64_t pitch;
     uint8_t food_sprite[128];
 };
-constexpr int kRenderMaxW = 32, kRenderMaxDraw = 2 * OC_MAX_ITEMS + 3 * OC_MAX_AGENTS;
+// columns a render block lists (one lane per column): 32 for a narrow level, 64 for a wide one
+// (u16 item cells; its lists take twice the LDS, which only wide levels pay)
+constexpr int kRenderMaxW = 32, kRenderMaxWWide = 64, kRenderMaxDraw = 2 * OC_MAX_ITEMS + 3 * OC_MAX_AGENTS;
 constexpr int kRenderPx = 16;  // pixels per lane and iteration: 48 output bytes, three 16-byte stores
 
 // SDL 1.2 per-pixel alpha blit of an RGBA source pixel onto an RGB destination pixel
@@ -1063,24 +1065,26 @@ __device__ __forceinline__ int div_small(int n, int d, float rcp) {
     return q;
 }
 
-template <int A, int K>
+template <int A, int K, bool WIDE>
 __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const uint8_t* __restrict__ state,
                                                            const uint8_t* __restrict__ rank,
                                                            const uint32_t* __restrict__ atlas,
                                                            const uint32_t* __restrict__ bg,
                                                            uint8_t* __restrict__ out) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    __shared__ uint32_t dl_off[kRenderMaxW][kRenderMaxDraw];
-    __shared__ uint32_t dl_geo[kRenderMaxW][kRenderMaxDraw];  // size | offset << 16
-    __shared__ int32_t dl_n[kRenderMaxW];
+    constexpr int kCols = WIDE ? kRenderMaxWWide : kRenderMaxW;
+    __shared__ uint32_t dl_off[kCols][kRenderMaxDraw];
+    __shared__ uint32_t dl_geo[kCols][kRenderMaxDraw];  // size | offset << 16
+    __shared__ int32_t dl_n[kCols];
     // per wave: its 1,024 pixels while it blends, then its 3 KB of packed output
     __shared__ u32x4 pix4[kBlock / 64][64 * kRenderPx / 4];
-    __shared__ uint32_t work[kBlock / 64][64];  // listed lane | row << 6 | cell column << 16 | x in cell << 21
+    __shared__ uint32_t work[kBlock / 64][64];  // listed lane | row << 6 | cell column << 16 | x in cell << 22
     const uint32_t part = blockIdx.x % (uint32_t)R.parts, strip = blockIdx.x / (uint32_t)R.parts;
     const int64_t e = strip / (uint32_t)R.H;
     const int ty = (int)(strip % (uint32_t)R.H);
     const int W = R.W, tile = R.tile;
-    constexpr int kPX = 0, kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K;
+    // planes: a wide level's item cells are u16, low bytes then high bytes, before the masks
+    constexpr int kPX = 0, kPY = A, kPH = 2 * A, kPL = 3 * A, kPLH = 3 * A + K, kPM = 3 * A + (WIDE ? 2 : 1) * K;
     if ((int)threadIdx.x < W) {
         const int tx = threadIdx.x, cell = ty * W + tx;
         const uint8_t* s = state + e;
@@ -1115,8 +1119,10 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
         // when the caller gives ranks (render.DrawOrder), else in slot order ...
         uint32_t here = 0u;
 #pragma unroll
-        for (int j = 0; j < K; ++j)
-            if (s[(kPL + j) * P] == (uint8_t)cell) here |= 1u << j;
+        for (int j = 0; j < K; ++j) {
+            const int c = WIDE ? (int)s[(kPL + j) * P] | (int)s[(kPLH + j) * P] << 8 : (int)s[(kPL + j) * P];
+            if (c == cell) here |= 1u << j;  // a dead slot (0xFF / 0xFFFF) is no cell
+        }
         here &= ~held;
         while (here != 0u) {
             int j = __builtin_ctz(here);
@@ -1195,14 +1201,14 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
                     pix4[wave][4 * lane + q] = u32x4{p[4 * q], p[4 * q + 1], p[4 * q + 2], p[4 * q + 3]};
                 const uint32_t slot =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                work[wave][slot] = (uint32_t)lane | ((uint32_t)r << 6) | ((uint32_t)tx << 16) | ((uint32_t)lx0 << 21);
+                work[wave][slot] = (uint32_t)lane | ((uint32_t)r << 6) | ((uint32_t)tx << 16) | ((uint32_t)lx0 << 22);
             }
             __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave; keep the compiler from moving reads up
             const int npx = kRenderPx * __popcll(mask);
             for (int t = lane; t < npx; t += 64) {
                 const uint32_t ent = work[wave][t >> 4];
                 const int k = t & (kRenderPx - 1), gl = (int)(ent & 63u);
-                const int rr = (int)((ent >> 6) & 0x3FFu), ctx = (int)((ent >> 16) & 31u), lx = (int)(ent >> 21) + k;
+                const int rr = (int)((ent >> 6) & 0x3FFu), ctx = (int)((ent >> 16) & 63u), lx = (int)(ent >> 22) + k;
                 uint32_t dpx = pix[kRenderPx * gl + k];
                 const int n = dl_n[ctx];
                 for (int d = 0; d < n; ++d) {
@@ -1391,7 +1397,7 @@ struct oc_handle {
     ocro::RollLevel roll;       // planner rollout tables (nnodes < 0: graph too large)
     uint8_t* roll_blob = nullptr;  // device: the level's rollout table blob (oc_rollout.h)
     int32_t roll_blob_bytes = 0;
-    uint8_t roll_blob_host[ocro::kBlobMax];  // the same blob on the host
+    std::vector<uint8_t> roll_blob_host;  // the same blob on the host
     // wide levels (more than 255 cells): the scalar step's tables
     bool wide = false;
     ocro::StepLevel step;
@@ -1661,7 +1667,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
             h->roll_blob_bytes = h->roll.blob_bytes;
             if (hipSetDevice(device) != hipSuccess ||
                 hipMalloc(&h->roll_blob, (size_t)h->roll_blob_bytes) != hipSuccess ||
-                hipMemcpy(h->roll_blob, h->roll_blob_host, (size_t)h->roll_blob_bytes, hipMemcpyHostToDevice) !=
+                hipMemcpy(h->roll_blob, h->roll_blob_host.data(), (size_t)h->roll_blob_bytes, hipMemcpyHostToDevice) !=
                     hipSuccess) {
                 h->roll_blob = nullptr;  // no device (e.g. a CPU-only build check): rollout unavailable
                 (void)hipGetLastError();
@@ -1684,16 +1690,16 @@ int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, i
                     int64_t dist_len) {
     if (h == nullptr || num_nodes == nullptr) return fail(OC_EINVAL, "bad argument");
     if (h->roll.nnodes < 0)
-        return fail(OC_ELEVEL, "reachability graph exceeds %d nodes or a distance of 254", ocro::kMaxNodes);
+        return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (%d on a level of more than 255 cells) or a distance of 254", ocro::kMaxNodes, ocro::kMaxNodesWide);
     const int n = h->roll.nnodes, cells = h->level.width * h->level.height;
     *num_nodes = n;
     if (node_of != nullptr) {
         if (node_of_len < (int64_t)cells * 5) return fail(OC_EINVAL, "node_of needs %d entries", cells * 5);
-        memcpy(node_of, h->roll_blob_host + h->roll.node_off, (size_t)cells * 5 * sizeof(uint16_t));
+        memcpy(node_of, h->roll_blob_host.data() + h->roll.node_off, (size_t)cells * 5 * sizeof(uint16_t));
     }
     if (dist != nullptr) {
         if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %d bytes", n * n);
-        for (int i = 0; i < n * n; ++i) dist[i] = h->roll_blob_host[h->roll.dist_off + i];
+        memcpy(dist, h->roll_blob_host.data() + h->roll.dist_off, (size_t)n * n);
     }
     return OC_OK;
 }
@@ -1998,11 +2004,11 @@ static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num
         if (subtasks[i].level != OC_LEVEL0 && !level1_ok)
             return fail(OC_EINVAL, "subtask %d: only oc_rollout takes OC_LEVEL1", i);
     if (num_subtasks < 1 || num_subtasks > OC_MAX_SUBTASKS) return fail(OC_EINVAL, "num_subtasks %d", num_subtasks);
-    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes or a distance of 254", ocro::kMaxNodes);
+    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (%d on a level of more than 255 cells) or a distance of 254", ocro::kMaxNodes, ocro::kMaxNodesWide);
     if (h->roll_blob == nullptr) return fail(OC_EHIP, "rollout tables not on the device");
     R.L = h->roll;
     R.nsub = num_subtasks;
-    R.blob_words = h->roll_blob_bytes / 4;
+    R.blob_words = h->roll.lds_bytes / 4;  // staged in LDS: the whole blob, or a wide level's tables
     R.pitch = pitch_for(B);
     R.B = B;
     for (int i = 0; i < num_subtasks; ++i) {
@@ -2060,8 +2066,8 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_ROLL(A, K, W)                                                                              \
-    if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W>, h->roll_blob_bytes)) return rc;    \
-    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,             \
+    if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W>, h->roll.lds_bytes)) return rc;    \
+    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,             \
                        (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags,    \
                        lower_bound)
     OC_DISPATCH_W(h, OC_LAUNCH_ROLL)
@@ -2090,14 +2096,14 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
 #define OC_LAUNCH_LIK(A, K, W)                                                                                       \
     if (const int rc = allow_dyn_lds(any_joint ? (const void*)oc_likelihood_kernel<A, K, 32, W>                       \
                                                : (const void*)oc_likelihood_kernel<A, K, 8, W>,                 \
-                                     h->roll_blob_bytes))                                                            \
+                                     h->roll.lds_bytes))                                                             \
         return rc;                                                                                                   \
     if (any_joint)                                                                                                   \
-        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 32, W>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,       \
+        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 32, W>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,       \
                            (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,   \
                            likelihood, out_flags);                                                                   \
     else                                                                                                             \
-        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 8, W>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,        \
+        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 8, W>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,        \
                            (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,   \
                            likelihood, out_flags)
     OC_DISPATCH_W(h, OC_LAUNCH_LIK)
@@ -2125,8 +2131,8 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
     const dim3 grid((unsigned)bx, (unsigned)chunks);
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_BOUNDS(A, K, W)                                                                         \
-    if (const int rc = allow_dyn_lds((const void*)oc_bounds_kernel<A, K, W>, h->roll_blob_bytes)) return rc;  \
-    hipLaunchKernelGGL((oc_bounds_kernel<A, K, W>), grid, dim3(kBlock), h->roll_blob_bytes, st, R,           \
+    if (const int rc = allow_dyn_lds((const void*)oc_bounds_kernel<A, K, W>, h->roll.lds_bytes)) return rc;  \
+    hipLaunchKernelGGL((oc_bounds_kernel<A, K, W>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,           \
                        (const uint8_t*)state, h->roll_blob, lower_bound, doable)
     OC_DISPATCH_W(h, OC_LAUNCH_BOUNDS)
     return hip_check("oc_subtask_bounds launch");
@@ -2144,8 +2150,8 @@ int oc_render_ordered(const oc_handle* h, const void* state, const uint8_t* draw
         out == nullptr || B < 0)
         return fail(OC_EINVAL, "bad argument");
     const int W = h->level.width, H = h->level.height;
-    if (W > kRenderMaxW) return fail(OC_ELEVEL, "render: width %d > %d", W, kRenderMaxW);
-    if (h->wide) return fail(OC_ELEVEL, "render: levels of more than %d cells are not rendered", OC_MAX_NARROW_CELLS);
+    const int max_w = h->wide ? kRenderMaxWWide : kRenderMaxW;
+    if (W > max_w) return fail(OC_ELEVEL, "render: width %d > %d", W, max_w);
     if (desc->tile < kRenderPx || desc->tile % kRenderPx != 0 || desc->tile > 1024)
         return fail(OC_EINVAL, "render: tile %d (a multiple of %d)", desc->tile, kRenderPx);
     for (int c = 0; c < OC_RENDER_SIZES; ++c)
@@ -2176,10 +2182,10 @@ int oc_render_ordered(const oc_handle* h, const void* state, const uint8_t* draw
     R.parts = 2;  // two blocks per (env, cell row): 0.198 vs 0.214 ms per 1,024 images (3 or 4: 0.211-0.213)
     const dim3 grid((unsigned)(B * H * R.parts));
     hipStream_t st = (hipStream_t)stream;
-#define OC_LAUNCH_RENDER(A, K)                                                                               \
-    hipLaunchKernelGGL((oc_render_kernel<A, K>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state, draw_rank, \
+#define OC_LAUNCH_RENDER(A, K, WD)                                                                               \
+    hipLaunchKernelGGL((oc_render_kernel<A, K, WD>), grid, dim3(kBlock), 0, st, R, (const uint8_t*)state, draw_rank, \
                        atlas, background, out)
-    OC_DISPATCH(h->A, h->K, OC_LAUNCH_RENDER)
+    OC_DISPATCH_W(h, OC_LAUNCH_RENDER)
     return hip_check("oc_render launch");
 }
 

@@ -11,15 +11,20 @@
 // The reachability graph of the static level (world.py:67-108) is precomputed by
 // build_roll_level() as a compact all-pairs distance table (u8, 0xFF = no path).  The static
 // tables of a level (tile classes, graph node ids, Cutboard / Delivery lists, distances) form
-// one byte blob that the kernels stage in LDS, sized per level (kBlob*Off + nnodes^2 bytes):
-// a 7x7 kitchen's blob is ~7 KB, the largest (kMaxNodes nodes) ~152 KB, which the kernels get
-// as dynamic LDS past the default 64 KB (gfx950 has 160 KB per CU).  Distances and bounds are
-// exact in fp32 (integers and halves < 2^9).
+// one byte blob, sized per level (the tables + nnodes^2 distance bytes).  A narrow level's
+// kernels stage all of it in LDS: a 7x7 kitchen's blob is ~7 KB, the largest (kMaxNodes nodes)
+// ~152 KB, which they get as dynamic LDS past the default 64 KB (gfx950 has 160 KB per CU).  A
+// wide level (more than 255 cells) stages the tables in front of the distances only and reads
+// the distance table from device memory (L2), so its graph may have up to kMaxNodesWide nodes
+// (a 1,024-cell kitchen's 5,120 approach nodes at most, 26 MB).  Distances and bounds are exact
+// in fp32 (integers and halves < 2^9).
 //
 // The includer defines __host__ / __device__ (HIP, or empty for the host test harness).
 #pragma once
 
 #include <stdint.h>
+
+#include <vector>
 
 // Every row function is force-inlined: a GPU call spills the caller's live registers to
 // scratch (the bound walk was being emitted as s_swappc calls with ~100 B of scratch per lane).
@@ -43,6 +48,7 @@ constexpr int kMaxCellsWide = 1024;  // wide levels (more than 255 cells): u16 c
 // block's LDS (blob + 64 configurations + the kernels' own) within the 160 KB of a gfx950 CU;
 // distances are bytes (0xFF = no path), so a graph whose BFS distances reach 255 is refused too
 constexpr int kMaxNodes = 390;
+constexpr int kMaxNodesWide = 5 * kMaxCellsWide;  // wide levels: the distances stay in device memory
 constexpr uint8_t kNone = 0xFF;
 constexpr uint16_t kNoNode = 0xFFFF;
 constexpr int kFloor = 0, kCounter = 1, kCutboard = 2, kDelivery = 3;  // OC_TILE_*
@@ -55,13 +61,10 @@ constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NA
 //   node_off   u16 [C * 5] graph node of (cell, approach), approach 4 = (0, 0)
 //   cut_off    Cutboard cells in scan order (L.ncut; u8 narrow, u16 wide)
 //   deliv_off  Delivery cells in scan order (L.ndeliv; u8 narrow, u16 wide)
-//   dist_off   [nnodes][nnodes] BFS distances
 //   dmin_off   [2][nnodes] the distance from a node to the nearest Cutboard (row 0) / Delivery
 //              (row 1) approach node, 0xFF = none reachable
-// A narrow level's offsets are fixed: 0, 256, 2816, 3072, 3328.
-constexpr int kNarrowDistOff = 256 + 2 * 256 * 5 + 256 + 256;
-constexpr int kWideTablesMax = kMaxCellsWide * (1 + 10 + 2 + 2);
-constexpr int kBlobMax = kWideTablesMax + kMaxNodes * kMaxNodes + 2 * kMaxNodes + 4;
+//   dist_off   [nnodes][nnodes] BFS distances (last: a wide level stages the blob up to here)
+// A narrow level's first offsets are fixed: 0, 256, 2816, 3072, then dmin at 3328.
 
 struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t W, H, perimeter, nnodes;
@@ -71,6 +74,7 @@ struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t tile_off, node_off, cut_off, deliv_off, dist_off;
     int32_t wide;      // u16 cell ids (W * H > 255)
     int32_t blob_bytes;  // the blob's size (a multiple of 4)
+    int32_t lds_bytes;   // what the kernels stage in LDS: all of it (narrow), up to dist_off (wide)
 };
 
 // The environment step's level constants (the scalar step of wide levels, RowOps::env_step).
@@ -162,10 +166,10 @@ OC_RH bool has_u16(uint64_t w, uint32_t v) {
 
 // ---- host: level tables ----------------------------------------------------------------------
 // Builds the reachability graph of make_reachability_graph (world.py:67-108) and its BFS
-// distances into `blob` (kBlobMax bytes).  Returns the node count, or -1 when the level has
-// more cells than its layout takes (255 narrow, kMaxCellsWide wide), the graph more than
-// kMaxNodes nodes, or a BFS distance past 254.
-inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uint8_t* tiles, int enc) {
+// distances into `blob_v` (resized to the blob).  Returns the node count, or -1 when the level
+// has more cells than its layout takes (255 narrow, kMaxCellsWide wide), the graph more nodes
+// than its kernels take (kMaxNodes narrow, kMaxNodesWide wide), or a BFS distance past 254.
+inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, int H, const uint8_t* tiles, int enc) {
     L.W = W;
     L.enc = enc;
     L.H = H;
@@ -176,11 +180,14 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
     L.wide = cells > kMaxCells ? 1 : 0;
     if (cells > kMaxCellsWide) return -1;
     const int C = L.wide ? (cells + 3) & ~3 : 256, lb = L.wide ? 2 : 1;  // table cells, list entry bytes
+    const int max_nodes = L.wide ? kMaxNodesWide : kMaxNodes;
     L.tile_off = 0;
     L.node_off = C;
     L.cut_off = L.node_off + 2 * C * 5;
     L.deliv_off = L.cut_off + lb * C;
-    L.dist_off = L.deliv_off + lb * C;
+    L.dmin_off = L.deliv_off + lb * C;
+    blob_v.assign((size_t)L.dmin_off, 0);  // grown below once the node count is known
+    uint8_t* blob = blob_v.data();
     uint8_t* tile = blob + L.tile_off;
     uint16_t* node = (uint16_t*)(blob + L.node_off);
     auto put_list = [&](int off, int i, int c) {
@@ -200,13 +207,13 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
         const int x = c % W, y = c / W;
         const bool coll = tiles[c] != kFloor;
         if (!coll) {
-            if (n >= kMaxNodes) return -1;
+            if (n >= max_nodes) return -1;
             node[c * 5 + 4] = (uint16_t)n++;
         }
         for (int d = 0; d < 4; ++d) {
             const int nc = clampy(y + kDY[d]) * W + clampx(x + kDX[d]);
             if (coll && tiles[nc] == kFloor) {
-                if (n >= kMaxNodes) return -1;
+                if (n >= max_nodes) return -1;
                 node[c * 5 + d] = (uint16_t)n++;
             }
         }
@@ -214,14 +221,15 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
     // adjacency (undirected): floor-floor, and a collidable square's approach node with the
     // floor it is approached from
     static const int opp[4] = {1, 0, 3, 2};
-    static uint16_t adj[kMaxNodes][8];
-    int deg[kMaxNodes] = {0};
+    std::vector<uint16_t> adj_v((size_t)n * 8);
+    std::vector<int> deg((size_t)n, 0), q((size_t)n);
+    auto adj = [&](int u, int k) -> uint16_t& { return adj_v[(size_t)u * 8 + k]; };
     auto link = [&](int u, int v) {
         if (u == kNoNode || v == kNoNode || u == v) return;
         for (int k = 0; k < deg[u]; ++k)
-            if (adj[u][k] == v) return;
-        adj[u][deg[u]++] = (uint16_t)v;
-        adj[v][deg[v]++] = (uint16_t)u;
+            if (adj(u, k) == v) return;
+        adj(u, deg[u]++) = (uint16_t)v;
+        adj(v, deg[v]++) = (uint16_t)u;
     };
     for (int c = 0; c < cells; ++c) {
         const int x = c % W, y = c / W;
@@ -234,17 +242,22 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
             else if (!coll && !ncoll) link(node[c * 5 + 4], node[nc * 5 + 4]);
         }
     }
+    L.dist_off = (L.dmin_off + 2 * n + 3) & ~3;
+    blob_v.resize((size_t)L.dist_off + (size_t)n * n + 4, 0);
+    blob = blob_v.data();
+    tile = blob + L.tile_off;
+    node = (uint16_t*)(blob + L.node_off);
     uint8_t* dist = blob + L.dist_off;
     for (int s = 0; s < n; ++s) {
-        uint8_t* row = dist + s * n;
+        uint8_t* row = dist + (size_t)s * n;
         for (int t = 0; t < n; ++t) row[t] = kNone;
-        int q[kMaxNodes], qh = 0, qt = 0;
+        int qh = 0, qt = 0;
         row[s] = 0;
         q[qt++] = s;
         while (qh < qt) {
             const int u = q[qh++];
             for (int k = 0; k < deg[u]; ++k) {
-                const int v = adj[u][k];
+                const int v = adj(u, k);
                 if (row[v] == kNone) {
                     if (row[u] + 1 >= kNone) return -1;  // a distance the byte table cannot hold
                     row[v] = (uint8_t)(row[u] + 1);
@@ -256,7 +269,6 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
     // Chop and Deliver have a static B side (every Cutboard / every Delivery square, from any
     // side it is approached from): the single-agent bound's min over B of dist(A node, B node)
     // is this per-node table (world.py:175-189 evaluated once per level)
-    L.dmin_off = L.dist_off + n * n;
     for (int side = 0; side < 2; ++side) {
         const int off = side == 0 ? L.cut_off : L.deliv_off;
         const int nc = side == 0 ? L.ncut : L.ndeliv;
@@ -268,7 +280,7 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
                 for (int d = 0; d < 4; ++d) {
                     const int b = node[cell * 5 + d];
                     if (b == kNoNode) continue;
-                    const int dd = dist[v * n + b];
+                    const int dd = dist[(size_t)v * n + b];
                     if (dd != kNone && dd < best) best = dd;
                 }
             }
@@ -276,7 +288,9 @@ inline int build_roll_level(RollLevel& L, uint8_t* blob, int W, int H, const uin
         }
     }
     L.nnodes = n;
-    L.blob_bytes = (L.dmin_off + 2 * n + 3) & ~3;
+    L.blob_bytes = (int32_t)((L.dist_off + (size_t)n * n + 3) & ~(size_t)3);
+    L.lds_bytes = L.wide ? L.dist_off : L.blob_bytes;
+    blob_v.resize((size_t)L.blob_bytes, 0);
     return n;
 }
 
@@ -289,12 +303,14 @@ struct RowOps {
     static constexpr AcT kNoAc = ~(AcT)0;
     const RollLevel& L;
     const uint8_t* T;       // the level's table blob (LDS on the device)
+    const uint8_t* D;       // its distance table: in T (narrow), in device memory (wide)
     AcT ac = kNoAc;         // AgentCounter cells of this row's Level-0 view, one per byte (narrow) or
                             // u16 field (wide), all ones = none
     uint32_t active = 0;    // bit a: agent a is a subtask agent
     uint32_t blockers = 0;  // bit a: agent a's cell may not be moved into (get_single_actions)
 
-    OC_RH RowOps(const RollLevel& l, const uint8_t* blob) : L(l), T(blob) {}
+    OC_RH RowOps(const RollLevel& l, const uint8_t* blob) : L(l), T(blob), D(blob + l.dist_off) {}
+    OC_RH RowOps(const RollLevel& l, const uint8_t* blob, const uint8_t* dist) : L(l), T(blob), D(dist) {}
 
     OC_RH int static_tile(int cell) const { return T[L.tile_off + cell]; }
     OC_RH bool is_ac(int cell) const {
@@ -471,7 +487,7 @@ struct RowOps {
         // branch-free: a missing node reads entry (0, 0) and is masked, so every lane of a
         // wave issues the same table reads
         const bool none = u == kNoNode || v == kNoNode;
-        const int d = T[L.dist_off + (none ? 0 : u * L.nnodes + v)];
+        const int d = D[none ? 0 : u * L.nnodes + v];
         return none || d == kNone ? -1 : d;
     }
 

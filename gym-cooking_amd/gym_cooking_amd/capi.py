@@ -216,8 +216,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 
 
 class LevelError(RuntimeError):
-    """OC_ELEVEL: the level is outside an entry point's envelope (e.g. a reachability graph of
-    more than 390 nodes for the planner entry points)."""
+    """OC_ELEVEL: the level is outside an entry point's envelope (e.g. for the planner entry
+    points a reachability graph of more than 390 nodes on a level of at most 255 cells, whose
+    distance table the kernels keep in LDS; a wide level's graph may have up to 5,120)."""
 
 
 def check(rc: int) -> None:

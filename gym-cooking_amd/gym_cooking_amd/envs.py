@@ -735,7 +735,7 @@ class _Single:
         try:
             node_of, dist = batch.reachability()
             self.reach = ReachabilityGraph(batch.level.width, node_of, dist)
-        except capi.LevelError:  # graph past the planner tables' 390 nodes: stepping still works
+        except capi.LevelError:  # graph past the planner tables' envelope: stepping still works
             self.reach = None
 
     def _download(self, buf) -> np.ndarray:

@@ -86,14 +86,21 @@ def _draw_obj(screen, spr, mask, x, y, held, enc=0):
 
 
 def render_env(level, env_bytes, A, K, spr=None, channels="reference", order=None):
-    """One env's image from its state bytes (ax[A] ay[A] ah[A] loc[K] mask[K] t_lo t_hi flags).
+    """One env's image from its state bytes (ax[A] ay[A] ah[A] loc[K] mask[K] t_lo t_hi flags;
+    a level of more than 255 cells: loc_lo[K] loc_hi[K] mask[K], u16 cells, 0xFFFF dead).
     `order`: the slots in the order the objects are drawn (the reference's world.objects
     order, game.py:62-74); default slot order."""
     spr = _sprites() if spr is None else spr
     W, H = level.width, level.height
     b = [int(v) for v in env_bytes]
     ax, ay, ah = b[0:A], b[A:2 * A], b[2 * A:3 * A]
-    loc, mask = b[3 * A:3 * A + K], b[3 * A + K:3 * A + 2 * K]
+    if len(b) == 3 * A + 3 * K + 3:  # wide layout
+        loc = [b[3 * A + j] | b[3 * A + K + j] << 8 for j in range(K)]
+        dead = [c == 0xFFFF for c in loc]
+        mask = b[3 * A + 2 * K:3 * A + 3 * K]
+    else:
+        loc, mask = b[3 * A:3 * A + K], b[3 * A + K:3 * A + 2 * K]
+        dead = [c == 0xFF for c in loc]
     screen = np.empty((H * SCALE, W * SCALE, 3), np.uint8)
     screen[...] = FLOOR
     for c, kind in enumerate(level.tiles):
@@ -114,7 +121,7 @@ def render_env(level, env_bytes, A, K, spr=None, channels="reference", order=Non
             _blit(screen, spr["cutboard@80"], x * SCALE, y * SCALE)
     held = {h for h in ah if h < K}
     for j in (range(K) if order is None else order):
-        if loc[j] != 0xFF and j not in held:
+        if not dead[j] and j not in held:
             _draw_obj(screen, spr, mask[j], loc[j] % W, loc[j] // W, False, level.encoding)
     for a in range(A):
         _blit(screen, spr["agent-%s@80" % COLORS[a]], ax[a] * SCALE, ay[a] * SCALE)

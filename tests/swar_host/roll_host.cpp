@@ -2,6 +2,7 @@
 // so its logic can be checked against the CPU oracle and the reference rows without a GPU.
 // The loop mirrors oc_rollout_kernel's plane loads and stores; the product library never
 // contains this file.
+#include <vector>
 #include <math.h>
 #include <stdint.h>
 
@@ -36,9 +37,10 @@ static ocro::RowT<K, W> load(const uint8_t* sin, int64_t P, int64_t e) {
 template <int A, int K, bool W>
 static void run(const oc_level_desc* lv, const uint8_t* sin, uint8_t* sout, const uint8_t* act, const uint8_t* alloc,
                 const oc_subtask* subs, int nsub, uint8_t* flags, float* lb, int64_t B, int64_t P) {
-    static uint8_t blob[ocro::kBlobMax];
+    std::vector<uint8_t> blob_v;
     ocro::RollLevel L;
-    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
+    if (ocro::build_roll_level(L, blob_v, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
+    const uint8_t* blob = blob_v.data();
     using Pl = PL<A, K, W>;
     for (int64_t e = 0; e < B; ++e) {
         ocro::RowT<K, W> r = load<A, K, W>(sin, P, e);
@@ -75,9 +77,10 @@ template <int A, int K, bool W>
 static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* taken_p, const uint8_t* alloc,
                 const oc_subtask* subs, int nsub, int self_agent, double beta, double nap, double* out, uint8_t* flags,
                 int64_t B, int64_t P) {
-    static uint8_t blob[ocro::kBlobMax];
+    std::vector<uint8_t> blob_v;
     ocro::RollLevel L;
-    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
+    if (ocro::build_roll_level(L, blob_v, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
+    const uint8_t* blob = blob_v.data();
     for (int64_t e = 0; e < B; ++e) {
         const int ai = alloc ? alloc[e] : 0;
         double v = 0.0;
@@ -131,9 +134,10 @@ extern "C" int roll_host(const oc_level_desc* lv, int A, int K, const uint8_t* s
 template <int A, int K, bool W>
 static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask* subs, int nsub, float* lb,
                    uint8_t* doable, int64_t B, int64_t P) {
-    static uint8_t blob[ocro::kBlobMax];
+    std::vector<uint8_t> blob_v;
     ocro::RollLevel L;
-    if (ocro::build_roll_level(L, blob, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
+    if (ocro::build_roll_level(L, blob_v, lv->width, lv->height, lv->tiles, lv->encoding) < 0) return;
+    const uint8_t* blob = blob_v.data();
     for (int64_t e = 0; e < B; ++e) {
         const ocro::RowT<K, W> r = load<A, K, W>(sin, P, e);
         ocro::RowOps<A, K, W> ops(L, blob);

@@ -90,6 +90,28 @@ def _fixture_states(name, max_per_group=48):
         yield g.level, g.A, K, pitch, s, B
 
 
+def test_oracle_reads_the_wide_layout():
+    """render_oracle on the wide layout (u16 item cells, lo then hi planes) draws what it draws
+    from the same state in the narrow layout: random-play states of a 7x7 kitchen re-laid out."""
+    lv = levels.load_level("full-divider_salad")
+    A = 3
+    ob = oracle.OracleBatch(lv, A, 100, 64)
+    s, s2, act = ob.new_state(), ob.new_state(), ob.new_actions()
+    ob.reset(s)
+    for t in range(40):
+        ob.gen_actions(act, 0, t, 7)
+        ob.step(s, s2, act)
+        s, s2 = s2, s
+    K = ob.K
+    ev = tl.env_view(s, A, K, ob.pitch, 64)
+    for b in range(0, 64, 5):
+        n = ev[:, b]
+        w = np.concatenate([n[:3 * A], n[3 * A:3 * A + K], np.where(n[3 * A:3 * A + K] == 0xFF, 0xFF, 0).astype(np.uint8),
+                            n[3 * A + K:]])
+        assert len(w) == 3 * A + 3 * K + 3
+        assert np.array_equal(render_oracle.render_env(lv, w, A, K), render_oracle.render_env(lv, n, A, K)), b
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fixture", ["greedy.npz", "streams.npz"])
 def test_render_kernel_matches_oracle(fixture):

@@ -4,8 +4,8 @@ files).  oc_step replays the recorded episodes; oc_step_n (the scalar wide kerne
 CPU oracle on every step's outputs, the in-launch totals and the checksum; oc_reset against the
 template; oc_subtask_bounds and oc_rollout against the reference's rows; rollout, bounds and
 likelihood rows against the oracle on random states; the gym shim replays the episodes; the
-navigation planner over oc_rollout decides as the same search over the oracle's rows; the
-renderer refuses these levels (OC_ELEVEL)."""
+navigation planner over oc_rollout decides as the same search over the oracle's rows; oc_render
+draws them as the numpy restatement of the reference's blits does."""
 import os
 import types
 
@@ -184,12 +184,35 @@ def test_shim_replays_wide_level_episodes():
     assert checked > 500
 
 
-def test_wide_level_render_refused():
-    lv = levels.load_level(tw._path("wide-17x17_salad"))
-    eb = _batch(lv, 2, 8)
+@pytest.mark.parametrize("name,A", [("wide-17x17_salad", 4), ("wide-23x13_tl", 3), ("widegraph-24x24_salad", 2),
+                                    ("wide64", 3)])
+def test_wide_level_render_matches_oracle(name, A):
+    """oc_render on levels of more than 255 cells (u16 item cells; up to 64 columns) against the
+    numpy restatement of the reference's blits (oracle/render_oracle.py, pinned to the
+    reference's own screenshots and GIF frames in tests/test_render.py), after random play;
+    65 columns are refused with OC_ELEVEL while stepping works."""
+    import test_render as tr
     from gym_cooking_amd.render import Renderer
-    with pytest.raises(capi.LevelError):
-        Renderer(eb).render(eb.reset(eb.new_state()))
+    lv = tr._wide_kitchen(64) if name == "wide64" else levels.load_level(tw._path(name))
+    assert capi.is_wide(lv)
+    eb = _batch(lv, A, 24)
+    s, s2 = eb.new_state(), eb.new_state()
+    eb.reset(s)
+    a = eb.new_actions()
+    for t in range(70):
+        eb.gen_actions(a, t, 9)
+        eb.step(s, s2, a)
+        s, s2 = s2, s
+    img = Renderer(eb).render(s, channels="rgb").cpu().numpy()
+    assert img.shape[1:] == (lv.height * 80, lv.width * 80, 3)
+    ev = tl.env_view(s.cpu().numpy(), A, eb.K, eb.pitch, eb.B)
+    from oracle import render_oracle
+    for b in range(eb.B):
+        assert np.array_equal(img[b], render_oracle.render_env(lv, ev[:, b], A, eb.K, channels="rgb")), b
+    if name == "wide64":
+        wider = _batch(tr._wide_kitchen(65), 2, 8)
+        with pytest.raises(capi.LevelError, match="width"):
+            Renderer(wider).render(wider.reset(wider.new_state()))
 
 
 @pytest.mark.parametrize("name,A,sub,agents", [("wide-17x17_salad", 2, ("Chop", "Tomato"), ("agent-1",)),
