@@ -1,0 +1,140 @@
+"""A kitchen whose reachability graph has more than the 390 nodes a narrow level's planner
+tables hold in LDS: widegraph-24x24_salad, 576 cells and 605 nodes, whose
+planner kernels read the distance table from device memory (oc_rollout.h, RollLevel.lds_bytes).
+Pinned on the CPU to the reference's own runs of the level file (tests/golden/gen_widegraph.py):
+
+* the parser and the engine's graph (node count, and the BFS distance of 400 random node pairs
+  against the reference's nx.shortest_path_length);
+* the CPU oracle and oc_cpu_step against the recorded episodes (2-4 agents);
+* the host build of the planner rows and the oracle against the reference's subtask-bound and
+  rollout rows, and against each other on random rows."""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oc_testlib as tl
+import test_bounds_host as tb
+import test_rollout_host as th
+import test_widelevels as tw
+from gym_cooking_amd import capi, levels, recipes
+
+from oracle import oracle
+
+NAME = "widegraph-24x24_salad"
+
+
+def _info():
+    with open(os.path.join(tl.GOLDEN, "widegraph.json")) as f:
+        return json.load(f)[NAME]
+
+
+def _graph(lv):
+    """The engine's graph (oc_reachability): node count, node_of [cells * 5], dist [n * n]."""
+    lib = capi.load_library()
+    d = capi.level_desc(lv, 2)
+    h = ctypes.c_void_p()
+    capi.check(lib.oc_create(ctypes.byref(d), 2, 100, 0, ctypes.byref(h)))
+    try:
+        n = ctypes.c_int32()
+        capi.check(lib.oc_reachability(h, ctypes.byref(n), None, 0, None, 0))
+        node_of = np.zeros(lv.ncells * 5, np.uint16)
+        dist = np.zeros(n.value * n.value, np.uint8)
+        capi.check(lib.oc_reachability(h, ctypes.byref(n), node_of.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
+                                       len(node_of), dist.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), len(dist)))
+    finally:
+        lib.oc_destroy(h)
+    return n.value, node_of, dist.reshape(n.value, n.value)
+
+
+_NAV = {(0, 1): 0, (0, -1): 1, (-1, 0): 2, (1, 0): 3, (0, 0): 4}  # World.NAV_ACTIONS order + (0, 0)
+
+
+def test_widegraph_level_matches_reference_graph():
+    ref = _info()
+    lv = levels.load_level(tw._path(NAME))
+    assert (lv.width, lv.height) == (ref["width"], ref["height"]) and capi.is_wide(lv)
+    assert lv.tiles == ref["tiles"]
+    assert sorted(str(s) for s in recipes.all_subtasks(lv)) == sorted(ref["all_subtasks"])
+    n, node_of, dist = _graph(lv)
+    assert n == ref["graph_nodes"] > 390
+    checked = 0
+    for (ux, uy), ud, (vx, vy), vd, d in ref["dist_pairs"]:
+        u = int(node_of[(uy * lv.width + ux) * 5 + _NAV[tuple(ud)]])
+        v = int(node_of[(vy * lv.width + vx) * 5 + _NAV[tuple(vd)]])
+        assert u != 0xFFFF and v != 0xFFFF
+        got = int(dist[u, v])
+        assert (got if got != 0xFF else -1) == d, ((ux, uy), ud, (vx, vy), vd, got, d)
+        checked += 1
+    assert checked == 400
+
+
+@pytest.mark.parametrize("impl", ["oracle", "cpu_step"])
+def test_widegraph_episodes_match_reference(impl):
+    fx = tl.load_fixture("widegraph.npz")
+    groups = tl.episode_groups(fx)
+    assert sum(g.B for g in groups) == len(fx["ep_T"]) >= 6
+    for g in groups:
+        ob = oracle.OracleBatch(g.level, g.A, g.max_T, g.B)
+        s = ob.new_state()
+        ob.reset(s)
+        g.relocate(s, ob.pitch)
+        if impl == "oracle":
+            from test_oracle_golden import _oracle_step_fn
+            fn = _oracle_step_fn(ob)
+        else:
+            from gym_cooking_amd.engine import CpuStepper
+            fn = tw._cpu_step_fn(CpuStepper(g.level, g.A, g.B, g.max_T, nthreads=2))
+        errs = tl.compare_group(g, fn, s, ob.pitch, g.level.width)
+        assert not errs, "%s A=%d: %s" % (g.level.name, g.A, "\n".join(errs[:10]))
+
+
+@pytest.mark.parametrize("impl", ["oracle", "host"])
+def test_widegraph_bounds_match_reference_rows(impl):
+    rows = tl.BoundRows(tl.load_fixture("bounds_widegraph.npz"), 0)
+    assert rows.B > 0
+    ob = oracle.OracleBatch(rows.level, rows.A, 100, rows.B)
+    st = rows.state(ob.pitch)
+    for c0 in range(0, len(rows.subtasks), capi.MAX_SUBTASKS):
+        subs = rows.subtasks[c0:c0 + capi.MAX_SUBTASKS]
+        lb, ok = tb.host_bounds(ob, st, subs) if impl == "host" else ob.subtask_bounds(st, subs)
+        errs = rows.compare(lb, ok, sub0=c0)
+        assert not errs, "\n".join(errs[:20])
+
+
+@pytest.mark.parametrize("impl", ["oracle", "host"])
+def test_widegraph_rollout_matches_reference_rows(impl):
+    fx = tl.load_fixture("rollout_widegraph.npz")
+    n = 0
+    for rows in tl.RolloutRows(fx, 0).split(capi.MAX_SUBTASKS):
+        ob = oracle.OracleBatch(rows.level, rows.A, 100, rows.B)
+        sin = tl.state_from_canonical(rows.level, rows.A, ob.K, ob.pitch, rows.agents, rows.items, rows.t)
+        alloc = np.zeros(ob.pitch, np.uint8)
+        alloc[:rows.B] = rows.alloc
+        if impl == "oracle":
+            sout = ob.new_state()
+            flags, lb = ob.rollout(sin, sout, rows.actions(ob.pitch), rows.subtasks, alloc)
+        else:
+            sout, flags, lb = th.host_rollout(ob, sin, rows.actions(ob.pitch), rows.subtasks, alloc)
+        errs = rows.compare(sout, flags, lb, ob.pitch)
+        assert not errs, "\n".join(errs[:20])
+        n += rows.B
+    assert n == len(fx["cfg"]) > 0
+
+
+@pytest.mark.parametrize("A", [2, 4])
+def test_widegraph_host_rows_match_oracle_random(A):
+    B = 1200
+    ob, s, acts, subs, alloc = th.random_rollout_case(tw._path(NAME), A, B, seed=B + 7 * A, planner_levels=(0, 1))
+    o_out = ob.new_state()
+    o_fl, o_lb = ob.rollout(s, o_out, acts, subs, alloc)
+    h_out, h_fl, h_lb = th.host_rollout(ob, s, acts, subs, alloc)
+    assert np.array_equal(o_fl, h_fl) and np.array_equal(o_lb, h_lb)
+    assert np.array_equal(tl.env_view(o_out, A, ob.K, ob.pitch, B), tl.env_view(h_out, A, ob.K, ob.pitch, B))
+    subs0 = [capi.subtask(x.kind, list(x.agent[:x.num_agents]), list(x.start_mask), x.goal_mask, x.goal_count, 0)
+             for x in subs]
+    o_b, o_ok = ob.subtask_bounds(s, subs0)
+    h_b, h_ok = tb.host_bounds(ob, s, subs0)
+    assert np.array_equal(o_b, h_b) and np.array_equal(o_ok, h_ok)
