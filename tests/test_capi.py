@@ -68,3 +68,29 @@ def test_create_layout_and_validation_without_gpu():
 
 def capi_err(name):
     return {"EINVAL": -1, "EHIP": -2, "ELEVEL": -3}[name]
+
+
+def test_integration_stub_matches_binding():
+    """INTEGRATION.md section 3's ctypes stub (what a maintainer would paste into the reference)
+    declares the same structs, field for field and type for type, as the binding, asserts the
+    binding's ABI version, and its argtypes lines name exported entry points."""
+    import ctypes
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "INTEGRATION.md")) as f:
+        text = f.read()
+    sec = text[text.index("## 3. Direct C-ABI binding"):text.index("## 4.")]
+    code = sec[sec.index("```python") + len("```python"):sec.index("```", sec.index("```python") + 3)]
+    classes = re.findall(r"(class \w+\(ctypes.Structure\):.*?)(?=\n\S|\Z)", code, re.S)
+    ns = {"ctypes": ctypes}
+    for c in classes:
+        exec(c, ns)
+    for doc, ours in (("oc_level_desc", capi.OcLevelDesc), ("oc_layout", capi.OcLayout)):
+        a, b = ns[doc]._fields_, ours._fields_
+        assert [n for n, _ in a] == [n for n, _ in b], doc
+        assert [ctypes.sizeof(t) for _, t in a] == [ctypes.sizeof(t) for _, t in b], doc
+        assert ctypes.sizeof(ns[doc]) == ctypes.sizeof(ours)
+    assert re.search(r"oc_abi_version\(\) == (\d+)", code).group(1) == str(capi.OC_ABI_VERSION)
+    lib = capi.load_library()
+    for name in re.findall(r"lib\.(oc_\w+)\.argtypes", code):
+        assert hasattr(lib, name), name
