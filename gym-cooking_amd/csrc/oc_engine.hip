@@ -819,6 +819,196 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+#ifndef OC_LIK_COMPACT
+#define OC_LIK_COMPACT 1
+#endif
+#ifndef OC_LIK_ROUND_SCALE
+#define OC_LIK_ROUND_SCALE 1
+#endif
+// rows a wave takes per round: 8 with 32-lane groups (4 batches of 2), 16 with 8-lane groups
+constexpr int lik_rows_per_round(int G) { return (G == 32 ? 8 : 16) * OC_LIK_ROUND_SCALE; }
+// the compacted form's static LDS beyond the subtask table (8,384 B with 32-lane groups)
+constexpr int kLikCompactLds = 9 * 1024 * OC_LIK_ROUND_SCALE;
+// The likelihood with the wave's rollouts compacted (OC_LIK_COMPACT).  In the grouped form above
+// a rollout lane idles when its candidate is illegal and not the taken one, and a 32-lane group
+// idles 7 lanes always (27 on a one-agent row of a joint table).  Here a wave takes kNR rows per
+// round, in kNB batches of 64 / G rows (a G-lane group per row, as above):
+//   1. each group tests its row's candidates' legality and lists the ones that need a rollout
+//      (legal, or the taken action) in the wave's LDS item list, (row << 5) | k, by ballot;
+//      rows that need none (None subtask, a level0 raise, a bad alloc id) are written here;
+//   2. the wave's lanes take the list 64 items at a time: load the item's row, level0, one
+//      rollout (q_value), Q(s, k) and its raise bit into the row's LDS slots;
+//   3. each group reads its row's Q values back and takes the softmax as above (the same max,
+//      exp and ascending sum, so the outputs are bit-identical to the grouped form).
+template <int A, int K, int G, bool W>
+__global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs R, const uint8_t* __restrict__ sin,
+                                                                       const uint8_t* __restrict__ taken_p,
+                                                                       const uint8_t* __restrict__ alloc,
+                                                                       const uint8_t* __restrict__ blob_g,
+                                                                       int self_agent, double beta, double nap,
+                                                                       double* __restrict__ out,
+                                                                       uint8_t* __restrict__ out_flags) {
+    constexpr int kCand = G == 32 ? 25 : 5;  // candidates a row can have with this table
+    constexpr int kSlots = 32 / G;           // candidate k = lane + G * j, j < kSlots
+    constexpr int kRPB = 64 / G;             // rows per batch (one group each)
+    constexpr int kNR = lik_rows_per_round(G);  // rows per wave per round
+    constexpr int kNB = kNR / kRPB;             // batches per round
+    constexpr int kWaves = kBlock / 64;
+    constexpr uint32_t kNotPending = 0xFFFFu;
+    extern __shared__ uint32_t blob_w[];
+    __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
+    __shared__ double lq[kWaves][kNR][kCand];     // Q(s, k)
+    __shared__ uint32_t lok[kWaves][kNR];         // bit k: candidate k's rollout did not raise
+    __shared__ uint32_t llg[kWaves][kNR];         // bit k: candidate k is legal
+    __shared__ uint32_t lrow[kWaves][kNR];        // kt | ncand << 8, or kNotPending
+    __shared__ uint16_t items[kWaves][kNR * kCand];
+    stage_roll_tables(R, blob_g, blob_w, subs);
+    const uint8_t* blob = (const uint8_t*)blob_w;
+    const int64_t P = R.pitch;
+    const int wv = (int)(threadIdx.x >> 6), wl = (int)(threadIdx.x & 63), lane = wl & (G - 1), grp = wl / G;
+    const uint64_t below = (1ull << wl) - 1ull;
+    const int64_t stride = (int64_t)gridDim.x * kWaves * kNR;
+    for (int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * kNR; base < R.B; base += stride) {
+        wave_lds_sync();  // the previous round's phase 3 has read its slots
+        // ---- 1: legality, the rollout list ----
+        int n = 0;  // wave-uniform
+        for (int b = 0; b < kNB; ++b) {
+            const int rs = b * kRPB + grp;
+            const int64_t e = base + rs;
+            bool pending = false;
+            int kt = 0, ncand = 0;
+            bool need[kSlots], lgs[kSlots];
+#pragma unroll
+            for (int j = 0; j < kSlots; ++j) need[j] = lgs[j] = false;
+            if (e < R.B) {
+                const int ai = alloc != nullptr ? alloc[e] : 0;
+                int f = OC_LIK_BADALLOC;
+                double v = 0.0;
+                if (ai < R.nsub) {
+                    const ocro::Sub& s = subs[ai];
+                    ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
+                    uint32_t taken = 0;
+#pragma unroll
+                    for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
+                    ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);
+                    if (s.kind == 0) {
+                        f = 0;
+                        if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
+                    } else if (ops.level0(r, s)) {
+                        f = OC_LIK_RAISES;  // two removed agents on one square
+                    } else {
+                        const bool joint = s.n == 2;
+                        int t0 = (int)((taken >> (8 * s.agent[0])) & 0xFFu), t1 = ocro::kNoop;
+                        if (joint) t1 = (int)((taken >> (8 * s.agent[1])) & 0xFFu);
+                        t0 = t0 > ocro::kNoop ? ocro::kNoop : t0;
+                        t1 = t1 > ocro::kNoop ? ocro::kNoop : t1;
+                        ncand = joint ? 25 : 5;
+                        kt = joint ? t0 * 5 + t1 : t0;
+                        const int other =
+                            joint ? (s.agent[0] == self_agent ? 1 : (s.agent[1] == self_agent ? 0 : -1)) : -1;
+#pragma unroll
+                        for (int j = 0; j < kSlots; ++j) {
+                            const int k = lane + G * j;
+                            const int a0 = joint ? k / 5 : k, c1 = joint ? k % 5 : ocro::kNoop;
+                            bool lg = k < ncand && ops.action_legal(r, s, a0, c1);
+                            if (other == 0 && a0 != t0) lg = false;
+                            if (other == 1 && c1 != t1) lg = false;
+                            lgs[j] = lg;
+                            need[j] = lg || k == kt;
+                        }
+                        pending = true;
+                    }
+                }
+                if (!pending && lane == 0) {
+                    out[e] = f == OC_LIK_OK ? v : 0.0;
+                    out_flags[e] = (uint8_t)f;
+                }
+            }
+            uint32_t lgm = 0;
+#pragma unroll
+            for (int j = 0; j < kSlots; ++j) {
+                const uint64_t bn = __ballot(need[j]), bl = __ballot(lgs[j]);
+                if (need[j]) items[wv][n + __popcll(bn & below)] = (uint16_t)((rs << 5) | (lane + G * j));
+                n += __popcll(bn);
+                lgm |= (uint32_t)((bl >> (grp * G)) & (G == 32 ? 0xFFFFFFFFull : ((1ull << G) - 1ull))) << (G * j);
+            }
+            if (lane == 0) {
+                llg[wv][rs] = lgm;
+                lok[wv][rs] = 0u;
+                lrow[wv][rs] = pending ? (uint32_t)kt | ((uint32_t)ncand << 8) : kNotPending;
+            }
+        }
+        wave_lds_sync();
+        // ---- 2: the rollouts, 64 at a time ----
+        for (int p = 0; p < n; p += 64) {
+            if (p + wl < n) {
+                const uint32_t it = items[wv][p + wl];
+                const int rs = (int)(it >> 5), k = (int)(it & 31u);
+                const int64_t e = base + rs;
+                const int ai = alloc != nullptr ? alloc[e] : 0;
+                const ocro::Sub& s = subs[ai];
+                ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
+                ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);
+                ops.level0(r, s);
+                const bool joint = s.n == 2;
+                const int a0 = joint ? k / 5 : k, c1 = joint ? k % 5 : ocro::kNoop;
+                double q = 0.0;
+                const bool ok = ops.q_value(r, s, a0, c1, q);
+                lq[wv][rs][k] = q;
+                if (ok) atomicOr(&lok[wv][rs], 1u << k);
+            }
+        }
+        wave_lds_sync();
+        // ---- 3: each pending row's softmax (the grouped form's arithmetic) ----
+        for (int b = 0; b < kNB; ++b) {
+            const int rs = b * kRPB + grp;
+            const int64_t e = base + rs;
+            const uint32_t rw = lrow[wv][rs];
+            if (e >= R.B || rw == kNotPending) continue;  // group-uniform
+            const int kt = (int)(rw & 0xFFu), ncand = (int)(rw >> 8);
+            const uint32_t lgm = llg[wv][rs], okm = lok[wv][rs];
+            int f;
+            double v = 0.0;
+            if ((lgm & ~okm) != 0u || !((okm & lgm) >> kt & 1u)) {
+                f = OC_LIK_RAISES;
+            } else {
+                const double old_q = lq[wv][rs][kt];
+                double q[kSlots], ex[kSlots];
+                bool legal[kSlots];
+                double m = -1.0e300;
+#pragma unroll
+                for (int j = 0; j < kSlots; ++j) {
+                    const int k = lane + G * j;
+                    legal[j] = (lgm >> k) & 1u;
+                    q[j] = legal[j] ? beta * (old_q - lq[wv][rs][k < kCand ? k : 0]) : -1.0e300;
+                    m = q[j] > m ? q[j] : m;
+                }
+#pragma unroll
+                for (int off = 1; off < G; off <<= 1) {
+                    const double o = __shfl_xor(m, off, G);
+                    m = o > m ? o : m;
+                }
+                double et = 0.0;
+#pragma unroll
+                for (int j = 0; j < kSlots; ++j) {
+                    ex[j] = legal[j] ? exp(q[j] - m) : 0.0;
+                    if (lane + G * j == kt) et = ex[j];
+                }
+                double S = 0.0;  // ascending k: the reference's summation order
+#pragma unroll
+                for (int j = 0; j < kSlots; ++j)
+                    for (int c = 0; c < G && G * j + c < ncand; ++c) S += __shfl(ex[j], c, G);
+                v = __shfl(et, kt % G, G) / S;
+                f = OC_LIK_OK;
+            }
+            if (lane == 0) {
+                out[e] = v;
+                out_flags[e] = (uint8_t)f;
+            }
+        }
+    }
+}
+
 // One lane per env, every configuration of the block's chunk.  The bound is a min over the
 // env's A locations (Chop, Deliver: bound_static per location) or its (A, B) location pairs
 // (Merge: helper per pair), whose count depends on where the items are: walked per lane, lanes
@@ -2090,22 +2280,28 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     const int64_t G = any_joint ? 32 : 8;
     // grid: up to 16 blocks per CU with 32-lane groups (5 resident per CU: measured 0.35 vs
     // 0.39 ms per 2^18 C5 rows against 8 per CU), 8 per CU with 8-lane groups (3-4 resident)
-    const int64_t need = (B * G + kBlock - 1) / kBlock, cap = (int64_t)h->cus * (any_joint ? 16 : 8);
+    // the compacted form's row slots take up to kLikCompactLds more LDS: a level whose tables
+    // leave less than that runs the grouped form (same outputs)
+    const bool compact = OC_LIK_COMPACT && h->roll.lds_bytes + kLikCompactLds + (int)sizeof(ocro::Sub) * OC_MAX_SUBTASKS <= kLdsPerCu;
+    const int64_t rows_per_block = compact ? (kBlock / 64) * lik_rows_per_round((int)G) : kBlock / G;
+    const int64_t need = (B + rows_per_block - 1) / rows_per_block, cap = (int64_t)h->cus * (any_joint ? 16 : 8);
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
+#define OC_LIK_GO(KERN, A, K, GG, W)                                                                                 \
+    do {                                                                                                             \
+        if (const int rc = allow_dyn_lds((const void*)KERN<A, K, GG, W>, h->roll.lds_bytes)) return rc;              \
+        hipLaunchKernelGGL((KERN<A, K, GG, W>), grid, dim3(kBlock), h->roll.lds_bytes, st, R, (const uint8_t*)state, \
+                           taken, alloc, h->roll_blob, self_agent, beta, none_action_prob, likelihood, out_flags);   \
+    } while (0)
 #define OC_LAUNCH_LIK(A, K, W)                                                                                       \
-    if (const int rc = allow_dyn_lds(any_joint ? (const void*)oc_likelihood_kernel<A, K, 32, W>                       \
-                                               : (const void*)oc_likelihood_kernel<A, K, 8, W>,                 \
-                                     h->roll.lds_bytes))                                                             \
-        return rc;                                                                                                   \
-    if (any_joint)                                                                                                   \
-        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 32, W>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,       \
-                           (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,   \
-                           likelihood, out_flags);                                                                   \
+    if (compact && any_joint)                                                                                        \
+        OC_LIK_GO(oc_likelihood_compact_kernel, A, K, 32, W);                                                        \
+    else if (compact)                                                                                                \
+        OC_LIK_GO(oc_likelihood_compact_kernel, A, K, 8, W);                                                         \
+    else if (any_joint)                                                                                              \
+        OC_LIK_GO(oc_likelihood_kernel, A, K, 32, W);                                                                \
     else                                                                                                             \
-        hipLaunchKernelGGL((oc_likelihood_kernel<A, K, 8, W>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,        \
-                           (const uint8_t*)state, taken, alloc, h->roll_blob, self_agent, beta, none_action_prob,   \
-                           likelihood, out_flags)
+        OC_LIK_GO(oc_likelihood_kernel, A, K, 8, W)
     OC_DISPATCH_W(h, OC_LAUNCH_LIK)
     return hip_check("oc_nav_likelihood launch");
 }

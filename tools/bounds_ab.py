@@ -53,11 +53,26 @@ def child(lib):
     v = torch.empty(eb.pitch, dtype=torch.float64, device=dev)
     f = torch.empty(eb.pitch, dtype=torch.uint8, device=dev)
     ms_l = bench.time_launches(eb.nav_likelihood_launcher(s, a, table, 0, 1.3, 0.5, alloc, v, f), 40, dev)
+    # the likelihood again with the rows in random configuration order, and with a table of
+    # one-agent configurations only (8-lane groups)
+    perm = torch.randperm(eb.pitch, device=dev, generator=gen)
+    alloc_r = alloc[perm].contiguous()
+    vr = torch.empty_like(v)
+    fr = torch.empty_like(f)
+    ms_lr = bench.time_launches(eb.nav_likelihood_launcher(s, a, table, 0, 1.3, 0.5, alloc_r, vr, fr), 40, dev)
+    table1 = [capi.subtask(k, ags, st, g, 0) for (k, st, g) in bench.SALAD_SUBTASKS for ags in agent_sets
+              if len(ags) == 1][:capi.MAX_SUBTASKS]
+    alloc1 = (alloc % len(table1)).contiguous()
+    v1 = torch.empty_like(v)
+    f1 = torch.empty_like(f)
+    ms_l1 = bench.time_launches(eb.nav_likelihood_launcher(s, a, table1, 0, 1.3, 0.5, alloc1, v1, f1), 40, dev)
     torch.cuda.synchronize()
     h = hashlib.sha256()
-    for t in (lb[:, :rows], ok[:, :rows], out, flags[:rows], rlb[:rows], v[:rows], f[:rows]):
+    for t in (lb[:, :rows], ok[:, :rows], out, flags[:rows], rlb[:rows], v[:rows], f[:rows], vr[:rows], fr[:rows],
+              v1[:rows], f1[:rows]):
         h.update(t.contiguous().cpu().numpy().tobytes())
     print(json.dumps({"lib": os.path.basename(lib), "bounds_ms": ms_b, "rollout_ms": ms_r, "likelihood_ms": ms_l,
+                      "likelihood_random_ms": ms_lr, "likelihood_single_ms": ms_l1, "lik_ok": int((f[:rows] == 1).sum()),
                       "doable": int(ok[:, :rows].sum()), "digest": h.hexdigest()[:16]}), flush=True)
 
 
