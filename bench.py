@@ -162,8 +162,8 @@ def measure_likelihood(eb, states, taken, table, alloc, dev, world, reps: int = 
     ms = time_launches(eb.nav_likelihood_launcher(states, taken, table, 0, 1.3, 0.5, alloc, v, f), reps, dev)
     ok = int((f[:eb.B] == capi.LIK_OK).sum())
     return {"value": world * eb.B / (ms * 1e-3), "unit": "likelihood rows/s", "ms_per_launch": ms,
-            "kernel": "oc_likelihood_kernel<4,4>", "rows_computed": ok, "bound": "divergence + latency (a lane "
-            "per candidate rollout, up to 25 per row; profiles/r02/c5_grouped/pmc_c5.json)"}
+            "kernel": "oc_likelihood_compact_kernel<4,4>", "rows_computed": ok, "bound": "divergence + latency "
+            "(the wave's candidate rollouts one per lane, compacted; the rollouts' own paths differ; DESIGN.md 3.4)"}
 
 
 def measure_bounds(eb, states, table, dev, world, reps: int = 60) -> dict:
