@@ -13,7 +13,7 @@ import sys
 # kernel -> [(bench field, launches in the run incl. the 3 untimed)] in bench.py's order
 RUNS = {
     "oc_rollout_kernel": [("rollout.random_order", 203), ("rollout", 203)],
-    "oc_likelihood_kernel": [("rollout.likelihood", 43), ("rollout.likelihood.random_order", 43)],
+    "oc_likelihood_compact_kernel": [("rollout.likelihood", 43), ("rollout.likelihood.random_order", 43)],
     "oc_bounds_kernel": [("rollout.subtask_bounds", 63)],
 }
 

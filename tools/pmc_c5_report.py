@@ -27,7 +27,7 @@ import json
 import os
 import sys
 
-KERNELS = ("oc_rollout_kernel", "oc_bounds_kernel", "oc_likelihood_kernel", "oc_checksum_kernel",
+KERNELS = ("oc_rollout_kernel", "oc_bounds_kernel", "oc_likelihood_compact_kernel", "oc_likelihood_kernel", "oc_checksum_kernel",
            "oc_step_n_kernel", "oc_render_kernel")
 CUS, SIMDS = 256, 1024
 CHECKSUM_BYTES = 23 * (1 << 18)  # 3A + 2K + 3 planes x pitch, full-divider_salad 4 agents
