@@ -823,11 +823,13 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define OC_LIK_COMPACT 1
 #endif
 #ifndef OC_LIK_ROUND_SCALE
-#define OC_LIK_ROUND_SCALE 1
+#define OC_LIK_ROUND_SCALE 2
 #endif
-// rows a wave takes per round: 8 with 32-lane groups (4 batches of 2), 16 with 8-lane groups
+// rows a wave takes per round: 16 with 32-lane groups (8 batches of 2), 32 with 8-lane groups
+// (OC_LIK_ROUND_SCALE 2; half that: the same at C5 configuration-major, 2-5 % slower in random
+// order and on a one-agent table, profiles/r04/lik_compact/lik_ab_rounds.jsonl)
 constexpr int lik_rows_per_round(int G) { return (G == 32 ? 8 : 16) * OC_LIK_ROUND_SCALE; }
-// the compacted form's static LDS beyond the subtask table (8,384 B with 32-lane groups)
+// the compacted form's static LDS beyond the subtask table (16,768 B with 32-lane groups)
 constexpr int kLikCompactLds = 9 * 1024 * OC_LIK_ROUND_SCALE;
 // The likelihood with the wave's rollouts compacted (OC_LIK_COMPACT).  In the grouped form above
 // a rollout lane idles when its candidate is illegal and not the taken one, and a 32-lane group
