@@ -2284,7 +2284,10 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     // 0.39 ms per 2^18 C5 rows against 8 per CU), 8 per CU with 8-lane groups (3-4 resident)
     // the compacted form's row slots take up to kLikCompactLds more LDS: a level whose tables
     // leave less than that runs the grouped form (same outputs)
-    const bool compact = OC_LIK_COMPACT && h->roll.lds_bytes + kLikCompactLds + (int)sizeof(ocro::Sub) * OC_MAX_SUBTASKS <= kLdsPerCu;
+    // (OC_LIK_GROUPED set in the environment forces the grouped form: the parity test of that path)
+    static const bool force_grouped = std::getenv("OC_LIK_GROUPED") != nullptr;
+    const bool compact = OC_LIK_COMPACT && !force_grouped &&
+                         h->roll.lds_bytes + kLikCompactLds + (int)sizeof(ocro::Sub) * OC_MAX_SUBTASKS <= kLdsPerCu;
     const int64_t rows_per_block = compact ? (kBlock / 64) * lik_rows_per_round((int)G) : kBlock / G;
     const int64_t need = (B + rows_per_block - 1) / rows_per_block, cap = (int64_t)h->cus * (any_joint ? 16 : 8);
     const dim3 grid((unsigned)(need < cap ? need : cap));

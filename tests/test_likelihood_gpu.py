@@ -63,3 +63,42 @@ def test_likelihood_one_agent_tables_match_oracle(level, A, B):
         ok = o_f == capi.LIK_OK
         assert ok.sum() > 100
         np.testing.assert_allclose(g_v[ok], o_v[ok], rtol=1e-12)
+
+
+def _lik_case(kind):
+    """A seeded full-divider_salad case: the two-agent table (32-lane groups) or its one-agent
+    configurations (8-lane groups)."""
+    import test_rollout_host as th
+    ob, s, acts, subs, alloc = th.random_rollout_case("full-divider_salad", 4, 9000, seed=41)
+    if kind == "single":
+        subs = [capi.subtask(x.kind, [x.agent[0]], list(x.start_mask), x.goal_mask, x.goal_count) for x in subs]
+    return s, acts, subs, alloc
+
+
+def _lik_child(kind, out):
+    s, acts, subs, alloc = _lik_case(kind)
+    v, f = _gpu_lik("full-divider_salad", 4, 9000, s, acts, subs, alloc, 1, 1.3, 0.5)
+    np.savez(out, v=v, f=f)
+
+
+@pytest.mark.parametrize("kind", ["joint", "single"])
+def test_grouped_form_equals_compacted(kind, tmp_path):
+    """The product runs the compacted likelihood kernel; the grouped one remains for levels whose
+    tables leave too little LDS (oc_engine.hip, oc_nav_likelihood).  OC_LIK_GROUPED forces the
+    grouped form: a child process computes the same rows with it, bit for bit."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    env = dict(os.environ, OC_LIK_GROUPED="1",
+               PYTHONPATH=os.pathsep.join([here, root, os.path.join(root, "gym-cooking_amd")]))
+    out = str(tmp_path / "grouped.npz")
+    code = "import test_likelihood_gpu as t; t._lik_child(%r, %r)" % (kind, out)
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=300, cwd=here)
+    g = np.load(out)
+    s, acts, subs, alloc = _lik_case(kind)
+    v, f = _gpu_lik("full-divider_salad", 4, 9000, s, acts, subs, alloc, 1, 1.3, 0.5)
+    assert (f == capi.LIK_OK).sum() > 100
+    assert np.array_equal(f, g["f"])
+    assert np.array_equal(v.view(np.uint64), g["v"].view(np.uint64))
