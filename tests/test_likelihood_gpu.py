@@ -85,7 +85,9 @@ def _lik_child(kind, out):
 def test_grouped_form_equals_compacted(kind, tmp_path):
     """The product runs the compacted likelihood kernel; the grouped one remains for levels whose
     tables leave too little LDS (oc_engine.hip, oc_nav_likelihood).  OC_LIK_GROUPED forces the
-    grouped form: a child process computes the same rows with it, bit for bit."""
+    grouped form: a child process computes the same rows with it, bit for bit (that the switch
+    selects the grouped kernels: profiles/r04/lik_compact/lik_kernel_stats_grouped_env.csv, the
+    child's code under rocprofv3)."""
     import os
     import subprocess
     import sys
