@@ -822,9 +822,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef OC_LIK_COMPACT
 #define OC_LIK_COMPACT 1
 #endif
-#ifndef OC_LIK_ROW_LDS
-#define OC_LIK_ROW_LDS 0
-#endif
 #ifndef OC_LIK_ROUND_SCALE
 #define OC_LIK_ROUND_SCALE 2
 #endif
@@ -867,18 +864,6 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
     __shared__ uint32_t llg[kWaves][kNR];         // bit k: candidate k is legal
     __shared__ uint32_t lrow[kWaves][kNR];        // kt | ncand << 8, or kNotPending
     __shared__ uint16_t items[kWaves][kNR * kCand];
-#if OC_LIK_ROW_LDS
-    // each pending row's Level-0 view (row words and the RowOps state level0 sets), so that a
-    // rollout lane reads it from LDS instead of reloading the row and re-running level0
-    using Ops = ocro::RowOps<A, K, W>;
-    struct LikRow {
-        ocro::RowT<K, W> r;
-        typename Ops::AcT ac;
-        uint32_t active, blockers;
-    };
-    constexpr int kRowWords = (int)((sizeof(LikRow) + 7) / 8);
-    __shared__ uint64_t lview[kWaves][kNR][kRowWords];
-#endif
     stage_roll_tables(R, blob_g, blob_w, subs);
     const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
@@ -893,13 +878,12 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
             const int rs = b * kRPB + grp;
             const int64_t e = base + rs;
             bool pending = false;
-            int kt = 0, ncand = 0, ai_row = 0;
+            int kt = 0, ncand = 0;
             bool need[kSlots], lgs[kSlots];
 #pragma unroll
             for (int j = 0; j < kSlots; ++j) need[j] = lgs[j] = false;
             if (e < R.B) {
                 const int ai = alloc != nullptr ? alloc[e] : 0;
-                ai_row = ai;
                 int f = OC_LIK_BADALLOC;
                 double v = 0.0;
                 if (ai < R.nsub) {
@@ -935,16 +919,6 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
                             need[j] = lg || k == kt;
                         }
                         pending = true;
-#if OC_LIK_ROW_LDS
-                        if (lane == 0) {
-                            LikRow v0;
-                            v0.r = r;
-                            v0.ac = ops.ac;
-                            v0.active = ops.active;
-                            v0.blockers = ops.blockers;
-                            __builtin_memcpy(&lview[wv][rs][0], &v0, sizeof(LikRow));
-                        }
-#endif
                     }
                 }
                 if (!pending && lane == 0) {
@@ -963,7 +937,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
             if (lane == 0) {
                 llg[wv][rs] = lgm;
                 lok[wv][rs] = 0u;
-                lrow[wv][rs] = pending ? (uint32_t)kt | ((uint32_t)ncand << 8) | ((uint32_t)ai_row << 16) : kNotPending;
+                lrow[wv][rs] = pending ? (uint32_t)kt | ((uint32_t)ncand << 8) : kNotPending;
             }
         }
         wave_lds_sync();
@@ -972,23 +946,12 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
             if (p + wl < n) {
                 const uint32_t it = items[wv][p + wl];
                 const int rs = (int)(it >> 5), k = (int)(it & 31u);
-#if OC_LIK_ROW_LDS
-                const ocro::Sub& s = subs[lrow[wv][rs] >> 16];
-                LikRow v0;
-                __builtin_memcpy(&v0, &lview[wv][rs][0], sizeof(LikRow));
-                const ocro::RowT<K, W> r = v0.r;
-                ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);
-                ops.ac = v0.ac;
-                ops.active = v0.active;
-                ops.blockers = v0.blockers;
-#else
                 const int64_t e = base + rs;
                 const int ai = alloc != nullptr ? alloc[e] : 0;
                 const ocro::Sub& s = subs[ai];
                 ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
                 ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);
                 ops.level0(r, s);
-#endif
                 const bool joint = s.n == 2;
                 const int a0 = joint ? k / 5 : k, c1 = joint ? k % 5 : ocro::kNoop;
                 double q = 0.0;
