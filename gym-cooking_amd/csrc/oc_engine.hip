@@ -827,7 +827,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 #endif
 // rows a wave takes per round: 16 with 32-lane groups (8 batches of 2), 32 with 8-lane groups
 // (OC_LIK_ROUND_SCALE 2; half that: the same at C5 configuration-major, 2-5 % slower in random
-// order and on a one-agent table, profiles/r04/lik_compact/lik_ab_rounds.jsonl)
+// order and on a one-agent table, profiles/r04/lik_compact/lik_ab_rounds.jsonl; twice that: 10-20 %
+// slower, lik_ab_rounds4.jsonl)
 constexpr int lik_rows_per_round(int G) { return (G == 32 ? 8 : 16) * OC_LIK_ROUND_SCALE; }
 // the compacted form's static LDS beyond the subtask table (16,768 B with 32-lane groups)
 constexpr int kLikCompactLds = 9 * 1024 * OC_LIK_ROUND_SCALE;
