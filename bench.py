@@ -13,11 +13,12 @@ between the steps of a launch, SURVEY 8(d) "a multi-step launch that still write
 step's state"), with its own algorithmic bytes per env-step S*launches/K + S + 2A + 1.
 The one-launch-per-step path (oc_step in a hipGraph, 2S + 2A + 1 bytes) is reported beside it
 as "per_step_launch".  The timed region is bracketed by a barrier + synchronize on both
-sides; the per-GPU episode summaries are all-gathered (RCCL) inside it.
+sides (timed_window: the closing barrier follows the rank's clock read); the per-GPU episode
+summaries are all-gathered (RCCL) inside it, and `value` uses the max over ranks.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
-      N>1 starts N ranks itself (children of torch.distributed.run on 127.0.0.1); under an
-      external torchrun (WORLD_SIZE set) it runs as the given rank.
+      N>1 starts N ranks itself (child processes joining a TCPStore this process hosts on
+      127.0.0.1); under an external torchrun (WORLD_SIZE set) it runs as the given rank.
 """
 from __future__ import annotations
 
@@ -140,6 +141,17 @@ def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 200) -> dict:
     ms = time_rollout(alloc)
     nbytes = 55 * rows
     legal = int((flags[:rows] & capi.ROLL_LEGAL).ne(0).sum())
+    # the planner's own launch shape: planner.py / delegation.py send at most 4,096 rows per
+    # oc_rollout launch (64 waves); the first 4,096 C5 rows, configuration-major
+    small = 4096
+    eb4 = OvercookedBatch("full-divider_salad", A, small, max_T=100, device=dev)
+    NP = eb.layout.num_planes
+    s4 = s.view(NP, eb.pitch)[:, :small].contiguous().view(-1)
+    a4 = a.view(A, eb.pitch)[:, :small].contiguous().view(-1)
+    al4 = torch.sort(rnd[:small])[0].contiguous()
+    o4, f4 = eb4.new_state(), torch.empty(eb4.pitch, dtype=torch.uint8, device=dev)
+    lb4 = torch.empty(eb4.pitch, dtype=torch.float32, device=dev)
+    ms_small = time_launches(eb4.rollout_launcher(s4, o4, a4, table, al4, f4, lb4), 400, dev)
     lik = measure_likelihood(eb, s, a, table, alloc, dev, world)
     lik["random_order"] = measure_likelihood(eb, s, a, table, rnd, dev, world)["ms_per_launch"]
     bnd = measure_bounds(eb, s, table, dev, world)
@@ -150,7 +162,9 @@ def measure_rollout(dev, world, rows: int = 1 << 18, reps: int = 200) -> dict:
                         "rows configuration-major" % len(table),
             "algorithmic_bytes_per_row": 55, "achieved_GBs": nbytes / (ms * 1e-3) / 1e9,
             "frac_hbm": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "legal_rows": legal,
-            "random_order": {"ms_per_launch": ms_rnd, "value": world * rows / (ms_rnd * 1e-3)}}
+            "random_order": {"ms_per_launch": ms_rnd, "value": world * rows / (ms_rnd * 1e-3)},
+            "planner_shape": {"rows": small, "ms_per_launch": ms_small,
+                              "note": "the planner's launch size (<= 4,096 rows), back-to-back launches"}}
 
 
 def measure_likelihood(eb, states, taken, table, alloc, dev, world, reps: int = 40) -> dict:
@@ -418,35 +432,111 @@ def measure_plan_batch(dev, B: int = 1024, steps: int = 12) -> dict:
             "workload": "B random-play states of open-divider_salad after %d steps, Chop(Tomato) by agent-1" % steps}
 
 
-def measure_c3(dev, world, B: int = 1 << 20, n: int = 100, reps: int = 20) -> dict:
+def measure_c3(dev, world, B: int = 1 << 20, n: int = 100, reps: int = 6, replay_reps: int = 20) -> dict:
     """Secondary line, config C3: 3-agent full-divider_tl (the collision-heavy path), 2^20 envs
-    per GPU, one oc_step_n launch of n steps with every step's outputs written."""
+    per GPU, oc_step_n launches of n steps with every step's outputs written.
+
+    Measured the headline's way: the envs first run ten episodes and more in untimed launches
+    (each on its own action stream), so the timed launches start mid-run with timeouts and
+    auto-resets inside them; each timed launch continues from the previous one's last state
+    and reads actions written by gen_actions just before it (fresh, never replayed).  Its
+    duration is HIP events on the launch stream around it; the action generation queued just
+    ahead keeps the GPU busy, so the first event does not time the host's launch call.  The
+    round-4 figure (one launch replayed back to back from a reset) is kept beside it as
+    `replay_from_reset`."""
     from gym_cooking_amd.engine import OvercookedBatch
     eb = OvercookedBatch("full-divider_tl", 3, B, max_T=100, device=dev)
     P, A, S = eb.pitch, eb.A, eb.layout.state_bytes
     acts = torch.empty((n, A * P), dtype=torch.uint8, device=dev)
-    for i in range(n):
-        eb.gen_actions(acts[i], step=i, seed=3)
-    traj = torch.empty(n * S, dtype=torch.uint8, device=dev)
+    trajs = [torch.empty(n * S, dtype=torch.uint8, device=dev) for _ in range(2)]
     ex, coll = torch.empty(n * A * P, dtype=torch.uint8, device=dev), torch.empty(n * P, dtype=torch.uint8, device=dev)
     s, stats = eb.new_state(), eb.new_stats()
     tot = torch.zeros(5, dtype=torch.int64, device=dev)
     eb.reset(s)
     # as the headline launches it: state_out is the trajectory's last state, statistics folded
-    # in-launch; every replay starts from the same reset state
-    f = eb.step_n_launcher(s, traj[(n - 1) * S:], acts.reshape(-1), n, traj, ex, coll, stats, tot)
-    f()
-    torch.cuda.synchronize()
-    first = tot.cpu().tolist()
-    ms = time_launches(f, reps, dev)
-    tot = first
+    # in-launch; consecutive launches alternate between two trajectory buffers
+    fs = []
+    for k in range(2):
+        src = s if k == 0 else trajs[0][(n - 1) * S:]
+        fs.append(eb.step_n_launcher(src, trajs[k][(n - 1) * S:], acts.reshape(-1), n, trajs[k], ex, coll, stats, tot))
+    f_loop = eb.step_n_launcher(trajs[1][(n - 1) * S:], trajs[0][(n - 1) * S:], acts.reshape(-1), n, trajs[0], ex,
+                                coll, stats, tot)
+    stream_step = 0
+
+    def fresh():
+        nonlocal stream_step
+        for i in range(n):
+            eb.gen_actions(acts[i], step=stream_step + i, seed=3)
+        stream_step += n
+
+    warm = -(-(10 * 101 + 50) // n)  # ten episodes and more: the envs' phases spread over max_T + 1
+    # launch i reads the state launch i-1 wrote: fs[0], fs[1], f_loop, fs[1], f_loop, ...
+    order = [fs[0]] + [fs[1] if i % 2 == 1 else f_loop for i in range(1, warm + reps)]
+    for f in order[:warm]:
+        fresh()
+        f()
+    ms_l, colls = [], 0
+    for f in order[warm:]:
+        fresh()
+        stats.zero_()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        f()
+        e1.record()
+        torch.cuda.synchronize()
+        ms_l.append(e0.elapsed_time(e1))
+        colls += int(tot[3])
+    ms = ocdist.max_over_ranks(sum(ms_l) / len(ms_l) * 1e-3, dev) * 1e3
+    # round 4's measurement: one launch from a reset, replayed back to back
+    eb.reset(s)
+    fresh()
+    ms_rep = time_launches(fs[0], replay_reps, dev)
     nS = eb.layout.num_planes
     bytes_step = (nS + n * (nS + 2 * A + 1)) / n
+    gbs = bytes_step * B * n / (ms * 1e-3) / 1e9
     return {"value": world * B * n / (ms * 1e-3), "unit": "env-steps/s", "envs_per_gpu": B, "steps": n,
             "ms_per_step": ms / n, "kernel": "oc_step_n_kernel<3,4>", "algorithmic_bytes_per_env_step": bytes_step,
-            "achieved_GBs": bytes_step * B * n / (ms * 1e-3) / 1e9,
-            "frac_hbm": bytes_step * B * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "collision_pairs": int(tot[3]), "workload": "C3: full-divider_tl, 3 agents, random actions"}
+            "achieved_GBs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS, "timed_launches": len(ms_l),
+            "ms_per_launch_each": ms_l, "collision_pairs_per_launch": colls / len(ms_l),
+            "window": "mid-run after %d untimed launches, fresh actions per launch, HIP events per launch" % warm,
+            "replay_from_reset": {"ms_per_step": ms_rep / n,
+                                  "frac_hbm": bytes_step * B * n / (ms_rep * 1e-3) / 1e9 / HBM_PEAK_GBS},
+            "workload": "C3: full-divider_tl, 3 agents, random actions"}
+
+
+WIDE_LEVEL = os.path.join(ROOT, "tests", "golden", "levels", "widegraph-24x24_salad.txt")
+
+
+def measure_wide(dev, world, B: int = 1 << 20, n: int = 20, reps: int = 20) -> dict:
+    """Secondary line, SURVEY 8(f) #3: a wide level (more than 255 cells: u16 cell ids, the
+    scalar step kernel oc_step_wide_kernel), the 24x24 Salad kitchen of tests/golden/levels,
+    2 agents, 2^20 envs, one n-step oc_step_n launch with every step's outputs written (the
+    headline's launch shape), replayed back to back from a mid-run state.  Algorithmic bytes
+    per env-step: S/n + S + 2A + 1 with the wide layout's S = 3A + 3K + 3."""
+    from gym_cooking_amd.engine import OvercookedBatch
+    eb = OvercookedBatch(WIDE_LEVEL, 2, B, max_T=100, device=dev)
+    P, A, S = eb.pitch, eb.A, eb.layout.state_bytes
+    acts = torch.empty((n, A * P), dtype=torch.uint8, device=dev)
+    for i in range(n):
+        eb.gen_actions(acts[i], step=i, seed=7)
+    traj = torch.empty(n * S, dtype=torch.uint8, device=dev)
+    ex, coll = torch.empty(n * A * P, dtype=torch.uint8, device=dev), torch.empty(n * P, dtype=torch.uint8, device=dev)
+    s, stats = eb.new_state(), eb.new_stats()
+    tot = torch.zeros(5, dtype=torch.int64, device=dev)
+    eb.reset(s)
+    for _ in range(3):  # mid-run: 60 steps from the reset
+        eb.step_n(s, traj[(n - 1) * S:], acts.reshape(-1), n, traj, ex, coll, stats)
+        s.copy_(traj[(n - 1) * S:])
+    f = eb.step_n_launcher(s, traj[(n - 1) * S:], acts.reshape(-1), n, traj, ex, coll, stats, tot)
+    ms = time_launches(f, reps, dev)
+    nS = eb.layout.num_planes
+    bytes_step = (nS + n * (nS + 2 * A + 1)) / n
+    gbs = bytes_step * B * n / (ms * 1e-3) / 1e9
+    return {"value": world * B * n / (ms * 1e-3), "unit": "env-steps/s", "envs_per_gpu": B, "steps": n,
+            "ms_per_launch": ms, "ms_per_step": ms / n, "kernel": "oc_step_wide_kernel<2,%d>" % eb.K,
+            "state_bytes": nS, "algorithmic_bytes_per_env_step": bytes_step, "achieved_GBs": gbs,
+            "frac_hbm": gbs / HBM_PEAK_GBS,
+            "workload": "widegraph-24x24_salad (576 cells, u16 cell ids), 2 agents, random actions"}
 
 
 def per_step_launch(eb, acts, n_act, W, dev, world, use_graph=True) -> dict:
@@ -519,32 +609,131 @@ def host_cores() -> dict:
     return {"threads": share, "limits": limits}
 
 
+def timed_window(launches, gather, sync, barrier, clock=time.perf_counter):
+    """The timed region, shared by the headline window, the cold-actions window and the gloo
+    self-test that pins its contents (tests/test_bench_launcher.py).
+
+    Entry: barrier + synchronize (every rank starts from an idle GPU at the same moment).
+    Inside: the window's launches, the summary all-gather (RCCL, on the launch stream), and the
+    rank's closing synchronize -- nothing else.  Each rank's window ends at its own synchronize;
+    the closing barrier comes after the clock is read, so it brackets the region without being
+    timed (`value` takes the max over ranks of the windows, ocdist.max_over_ranks, so a barrier
+    inside would only add a collective round trip to every rank's window).  Returns (seconds,
+    gather's result)."""
+    barrier()
+    sync()
+    t0 = clock()
+    for f in launches:
+        f()
+    g = gather()
+    sync()
+    t1 = clock()
+    barrier()
+    return t1 - t0, g
+
+
+class WindowLog:
+    """--window-log PATH: host timestamps of the timed windows, to lay them beside a rocprofv3
+    kernel trace of the same run (tools/window_split.py itemises the window's fixed cost:
+    launch to kernel start, kernel, all-gather, completion seen by the host).  Each event is
+    (tag, CLOCK_MONOTONIC ns, CLOCK_BOOTTIME ns): the window's start and end (the timed_window
+    clock), and the moment each launch call and the all-gather call returned.  Without a path
+    nothing is wrapped or recorded."""
+
+    def __init__(self, path):
+        self.path, self.events, self.win = path, [], ""
+
+    def _mark(self, tag):
+        self.events.append((self.win + ":" + tag, time.clock_gettime_ns(time.CLOCK_MONOTONIC),
+                            time.clock_gettime_ns(time.CLOCK_BOOTTIME)))
+
+    def clock(self, win):
+        if self.path is None:
+            return time.perf_counter
+        self.win = win
+        n = [0]
+
+        def f():
+            self._mark("t0" if n[0] == 0 else "t1")
+            n[0] += 1
+            return time.perf_counter()
+        return f
+
+    def wrap(self, launches):
+        if self.path is None:
+            return launches
+
+        def w(i, fn):
+            def g():
+                fn()
+                self._mark("launch%d_returned" % i)
+            return g
+        return [w(i, fn) for i, fn in enumerate(launches)]
+
+    def dump(self, rank):
+        if self.path is not None:
+            with open("%s.rank%d.json" % (self.path, rank), "w") as f:
+                json.dump({"events": self.events}, f)
+
+
 def launch_ranks(n: int, argv) -> int:
-    """`bench.py --gpus N` outside torchrun: start the N ranks as child processes of
-    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) and exit with their
-    status.  The parent never touches the GPU, and nothing is exec'd: the ranks are fresh
-    processes, rank 0 prints the JSON line."""
-    import socket
+    """`bench.py --gpus N` outside torchrun: start the N ranks (one process per GPU) as child
+    processes and exit with their status.  The rendezvous store is a TCPStore this parent hosts
+    on 127.0.0.1, bound to port 0: the kernel picks a free port at bind time and the store keeps
+    it for the job, so no probe-then-bind race; the ranks join it as clients
+    (TORCHELASTIC_USE_AGENT_STORE, the way torchrun's agent hands its store to workers).  The
+    parent never touches the GPU, and nothing is exec'd: the ranks are fresh processes, rank 0
+    prints the JSON line.  If a rank fails, the others are terminated (by their PIDs)."""
     import subprocess
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.run(cmd, env=env).returncode
+    from torch.distributed import TCPStore
+    store = TCPStore("127.0.0.1", 0, n, is_master=True, wait_for_workers=False)
+    base = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                MASTER_PORT=str(store.port), TORCHELASTIC_USE_AGENT_STORE="True")
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                              env=dict(base, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    del store
+    return rc
 
 
 def selftest_ranks(args) -> int:
-    """--selftest-ranks: the launcher and shard/all-gather plumbing on gloo without any GPU
-    work (tests/test_bench_launcher.py): every rank reports its shard, rank 0 prints them."""
+    """--selftest-ranks: the launcher, shard and all-gather plumbing on gloo without any GPU
+    work (tests/test_bench_launcher.py).  Every rank reports its shard, and runs timed_window
+    with recording stand-ins (the launches, a real gloo all-gather of the summary row, the
+    synchronize, the barrier, the clock) so the test can check what the timed region holds;
+    rank 0 prints both."""
     rank, world, local = ocdist.world_from_env()
     ocdist.init("gloo")
     sh = ocdist.shard(args.batch, rank, world, local)
     g = ocdist.gather_summaries(torch.tensor([rank, world, sh.env_offset, sh.batch, os.getpid()]))
+    trace = []
+
+    def rec(tag, ret=None):
+        def f():
+            trace.append(tag)
+            return ret() if ret is not None else None
+        return f
+
+    row = torch.tensor([rank, 1, 2, 3, 4], dtype=torch.int64)
+    _, gathered = timed_window([rec("launch"), rec("launch")],
+                               rec("all_gather", lambda: ocdist.gather_summaries(row)),
+                               rec("synchronize"), rec("barrier", ocdist.barrier),
+                               clock=lambda: trace.append("clock") or time.perf_counter())
     if rank == 0:
-        print(json.dumps({"n_gpus": world, "ranks": g.tolist()}), flush=True)
+        print(json.dumps({"n_gpus": world, "ranks": g.tolist(), "window_trace": trace,
+                          "window_gathered": gathered.tolist()}), flush=True)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
     return 0
@@ -576,12 +765,15 @@ def main() -> int:
     ap.add_argument("--no-render", action="store_true", help="skip the secondary oc_render measurement")
     ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 (3-agent full-divider_tl) line")
     ap.add_argument("--no-planner", action="store_true", help="skip the secondary navigation-planner line")
+    ap.add_argument("--no-wide", action="store_true", help="skip the secondary wide-level (24x24) step line")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--host-wait", choices=("auto", "spin"), default="spin",
                     help="spin (default): hipSetDeviceFlags(hipDeviceScheduleSpin) before the device comes up, so "
                          "the window's closing synchronize spins on the completion signal; auto: the runtime's default "
                          "wait, which let the host see a ~90 us kernel's completion 20-40 us late in some windows "
                          "(profiles/r04/window_wait/)")
+    ap.add_argument("--window-log", default=None,
+                    help="write the timed windows' host timestamps to PATH.rankR.json (tools/window_split.py)")
     ap.add_argument("--selftest-ranks", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -699,17 +891,12 @@ def main() -> int:
     stats.zero_()
     torch.cuda.synchronize()
 
-    # ---------------- timed region ----------------
-    ocdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for f in timed:
-        f()
-    gathered = ocdist.gather_summaries(summary_row, summary_all)
-    torch.cuda.synchronize()
-    ocdist.barrier()
-    elapsed = time.perf_counter() - t0
-    # ----------------------------------------------
+    # ---------------- timed region (timed_window: launches + all-gather + synchronize) ----------
+    sync = torch.cuda.synchronize
+    wlog = WindowLog(args.window_log)
+    elapsed, gathered = timed_window(wlog.wrap(timed), lambda: ocdist.gather_summaries(summary_row, summary_all),
+                                     sync, ocdist.barrier, clock=wlog.clock("warm"))
+    # -------------------------------------------------------------------------------------------
     elapsed_max = ocdist.max_over_ranks(elapsed, dev)
     summary = ocdist.summarize(gathered)
 
@@ -751,15 +938,10 @@ def main() -> int:
     flush.fill_(1)
     stats.zero_()
     del flush
-    ocdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for f in timed:
-        f()
-    ocdist.gather_summaries(summary_row, summary_all)
-    torch.cuda.synchronize()
-    ocdist.barrier()
-    cold_max = ocdist.max_over_ranks(time.perf_counter() - t0, dev)
+    cold, _ = timed_window(wlog.wrap(timed), lambda: ocdist.gather_summaries(summary_row, summary_all), sync,
+                           ocdist.barrier, clock=wlog.clock("cold"))
+    cold_max = ocdist.max_over_ranks(cold, dev)
+    wlog.dump(rank)
     nS = eb.layout.num_planes  # state bytes per env (the u16 t counts 2)
     bytes_launch = (nS + n_per * (nS + 2 * A + 1)) * sh.batch
     bytes_env_step = bytes_launch / (n_per * sh.batch)
@@ -802,6 +984,7 @@ def main() -> int:
             "bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
             "frac_wall": bytes_env_step * sh.batch * K / elapsed_max / 1e9 / HBM_PEAK_GBS,
+            "frac_wall_cold": bytes_env_step * sh.batch * K / cold_max / 1e9 / HBM_PEAK_GBS,
             "kernel": "oc_step_n_kernel<%d,%d>" % (A, eb.K), "steps_per_launch": n_per,
             "algorithmic_bytes_per_launch": bytes_launch, "algorithmic_bytes_per_env_step": bytes_env_step,
             "kernel_ms_mean": kern_ms, "kernel_ms_source": ("HIP events around %d back-to-back replays of the timed "
@@ -823,6 +1006,8 @@ def main() -> int:
         line["render"] = measure_render(dev, world, args.level, args.agents)
     if not args.no_c3:
         line["c3"] = measure_c3(dev, world)
+    if not args.no_wide:
+        line["wide"] = measure_wide(dev, world)
     if not args.no_planner:
         line["planner"] = measure_planner(dev, world)
         line["bayes"] = measure_bayes(dev, world)
