@@ -38,6 +38,47 @@ static int get_val(PyObject* d, PyObject* k, double* out) {
     return 0;
 }
 
+/* Known-hash dict calls and _PySet_NextEntry are CPython internals: 3.10's public headers (this
+ * toolchain) still declare them, 3.13 moved them to the internal API.  From 3.13 on the public
+ * calls stand in; they hash the key again but read and write the same dicts, keys and values. */
+#if PY_VERSION_HEX >= 0x030D0000
+#define OC_DICT_GET_KH(d, k, h) PyDict_GetItemWithError((d), (k))
+#define OC_DICT_SET_KH(d, k, v, h) PyDict_SetItem((d), (k), (v))
+#define OC_DICT_HAS_KH(d, k, h) PyDict_Contains((d), (k))
+#else
+#define OC_DICT_GET_KH(d, k, h) _PyDict_GetItem_KnownHash((d), (k), (h))
+#define OC_DICT_SET_KH(d, k, v, h) _PyDict_SetItem_KnownHash((d), (k), (v), (h))
+#define OC_DICT_HAS_KH(d, k, h) _PyDict_Contains_KnownHash((d), (k), (h))
+#endif
+
+/* The smallest int in a set of ints (*out = -1 when empty); -1 on error. */
+static int set_min_index(PyObject* set, Py_ssize_t* out) {
+    *out = -1;
+#if PY_VERSION_HEX >= 0x030D0000
+    PyObject* iter = PyObject_GetIter(set);
+    if (iter == NULL) return -1;
+    PyObject* it;
+    while ((it = PyIter_Next(iter)) != NULL) {
+        const Py_ssize_t v = PyLong_AsSsize_t(it);
+        Py_DECREF(it);
+        if (v == -1 && PyErr_Occurred()) { Py_DECREF(iter); return -1; }
+        if (*out < 0 || v < *out) *out = v;
+    }
+    Py_DECREF(iter);
+    return PyErr_Occurred() ? -1 : 0;
+#else
+    Py_ssize_t pos = 0;
+    PyObject* it;
+    Py_hash_t hh;
+    while (_PySet_NextEntry(set, &pos, &it, &hh)) {
+        const Py_ssize_t v = PyLong_AsSsize_t(it);
+        if (v == -1 && PyErr_Occurred()) return -1;
+        if (*out < 0 || v < *out) *out = v;
+    }
+    return 0;
+#endif
+}
+
 static int set_val(PyObject* d, PyObject* k, double x) {
     PyObject* f = PyFloat_FromDouble(x);
     if (f == NULL) return -1;
@@ -65,7 +106,7 @@ static const char* entry_hashes(PyObject* got, Py_ssize_t n) {
 /* get_val / set_val with the key's hash known (h = NULL: hash it) */
 static int get_val_h(PyObject* d, PyObject* k, const char* h, Py_ssize_t i, double* out) {
     if (h == NULL) return get_val(d, k, out);
-    PyObject* v = _PyDict_GetItem_KnownHash(d, k, hash_at(h, i));
+    PyObject* v = OC_DICT_GET_KH(d, k, hash_at(h, i));
     if (v == NULL) {
         if (!PyErr_Occurred()) PyErr_SetObject(PyExc_KeyError, k);
         return -1;
@@ -79,14 +120,14 @@ static int set_val_h(PyObject* d, PyObject* k, const char* h, Py_ssize_t i, doub
     if (h == NULL) return set_val(d, k, x);
     PyObject* f = PyFloat_FromDouble(x);
     if (f == NULL) return -1;
-    int r = _PyDict_SetItem_KnownHash(d, k, f, hash_at(h, i));
+    int r = OC_DICT_SET_KH(d, k, f, hash_at(h, i));
     Py_DECREF(f);
     return r;
 }
 
 /* k in d, with the hash known (h = NULL: hash it); -1 on error */
 static int has_key_h(PyObject* d, PyObject* k, const char* h, Py_ssize_t i) {
-    return h == NULL ? PyDict_Contains(d, k) : _PyDict_Contains_KnownHash(d, k, hash_at(h, i));
+    return h == NULL ? PyDict_Contains(d, k) : OC_DICT_HAS_KH(d, k, hash_at(h, i));
 }
 
 /* numpy's bit-generator interface (numpy/random/bitgen.h): a legacy RandomState's
@@ -102,7 +143,10 @@ typedef struct {
 /* One uniform double from the tie-break generator (RandomState.random_sample: MT19937's
  * next_double, the variate numpy's legacy binomial reads); -1 on error.  `sample` is the bound
  * random_sample, or the generator's "BitGenerator" capsule (planner._sampler), whose
- * next_double is the very function random_sample calls: the same stream without a Python call. */
+ * next_double is the very function random_sample calls: the same stream without a Python call.
+ * The capsule path does not take the bit generator's lock (random_sample does): it assumes, as
+ * the planner guarantees, that no other thread uses the same RandomState while a search runs
+ * (each planner owns its generator; the search holds the GIL throughout). */
 static int uniform(PyObject* sample, double* u) {
     if (PyCapsule_CheckExact(sample)) {
         bitgen_t* bg = (bitgen_t*)PyCapsule_GetPointer(sample, "BitGenerator");
@@ -328,7 +372,7 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         resume = 0;
         PyObject* key = PyTuple_Pack(2, x, sk);
         if (key == NULL) goto fail;
-        PyObject* got = xh != -1 ? _PyDict_GetItem_KnownHash(succ, key, xh) : PyDict_GetItemWithError(succ, key);
+        PyObject* got = xh != -1 ? OC_DICT_GET_KH(succ, key, xh) : PyDict_GetItemWithError(succ, key);
         Py_DECREF(key);
         if (got == NULL && PyErr_Occurred()) goto fail;
         if (got == NULL) return Py_BuildValue("(iNli)", 1, x, counter, -1);
@@ -336,14 +380,8 @@ static PyObject* forward(PyObject* self, PyObject* args) {
         PyObject* crash = PyList_GET_ITEM(got, 7);
         if (PyList_GET_ITEM(got, 6) != Py_True) {
             if (crash != Py_None && PySet_GET_SIZE(crash) > 0) {  /* _init_succ raises on the first */
-                Py_ssize_t first = -1, pos = 0;
-                PyObject* it;
-                Py_hash_t hh;
-                while (_PySet_NextEntry(crash, &pos, &it, &hh)) {
-                    const Py_ssize_t v = PyLong_AsSsize_t(it);
-                    if (v == -1 && PyErr_Occurred()) goto fail;
-                    if (first < 0 || v < first) first = v;
-                }
+                Py_ssize_t first;
+                if (set_min_index(crash, &first) < 0) goto fail;
                 return Py_BuildValue("(iNli)", 2, x, counter, (int)first);
             }
             if (init_entry(got, v_l, v_u, tc) < 0) goto fail;
@@ -547,12 +585,12 @@ static PyObject* expand(PyObject* self, PyObject* args) {
         Py_XDECREF(rep);
         const Py_hash_t h1 = vk != NULL ? PyObject_Hash(vk) : -1;
         if (nk != NULL && h1 != -1 && keys != Py_None) {  /* intern */
-            PyObject* c = _PyDict_GetItem_KnownHash(keys, vk, h1);
+            PyObject* c = OC_DICT_GET_KH(keys, vk, h1);
             if (c != NULL) {
                 Py_INCREF(c);
                 Py_DECREF(vk);
                 vk = c;
-            } else if (PyErr_Occurred() || _PyDict_SetItem_KnownHash(keys, vk, vk, h1) < 0) {
+            } else if (PyErr_Occurred() || OC_DICT_SET_KH(keys, vk, vk, h1) < 0) {
                 Py_CLEAR(vk);
             }
         }

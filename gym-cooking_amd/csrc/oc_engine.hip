@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <thread>
 #include <vector>
@@ -552,7 +553,8 @@ struct RollArgs {
     ocro::RollLevel L;
     ocro::Sub subs[OC_MAX_SUBTASKS];
     int32_t nsub;
-    int32_t blob_words;  // ocro::blob_bytes(nnodes) / 4
+    int32_t blob_words;  // roll.lds_bytes / 4: the whole blob on a narrow level, the tables up to
+                         // dist_off on a wide one (its distances are read from device memory)
     int64_t pitch, B;
 };
 
@@ -790,27 +792,6 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
 // (configurations and tables in LDS).  Output [subtask][pitch], so each store instruction of a
 // wave covers 64 consecutive envs of one configuration.  Chunking the table multiplies the
 // waves of a launch: the walk is LDS-latency bound and one chunk left 4 waves per SIMD.
-#ifndef OC_BOUNDS_COMPACT
-#define OC_BOUNDS_COMPACT 0  // the wave-compacted walk below: parity-green, measured slower (off)
-#endif
-// Inclusive prefix sum over the wave: wave_sum's scan without its final read.
-__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
-    return v;
-}
-__device__ __forceinline__ uint32_t shfl32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src); }
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-    return (uint64_t)shfl32((uint32_t)v, src) | ((uint64_t)shfl32((uint32_t)(v >> 32), src) << 32);
-}
-__device__ __forceinline__ int kth_bit(uint32_t set, int k) {  // the k-th set bit (k < popcount)
-    for (int q = 0; q < k; ++q) set &= set - 1u;
-    return __builtin_ctz(set);
-}
 // LDS ordering between the lanes of one wave (its LDS operations run in order; this keeps the
 // compiler from moving them and waits for the outstanding ones)
 __device__ __forceinline__ void wave_lds_sync() {
@@ -1016,99 +997,28 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
 // env's A locations (Chop, Deliver: bound_static per location) or its (A, B) location pairs
 // (Merge: helper per pair), whose count depends on where the items are: walked per lane, lanes
 // with fewer locations idle while the others finish (0.58 of the lanes active per VALU
-// instruction, profiles/r04/c5/pmc_c5.json).  Compacted (OC_BOUNDS_COMPACT): the wave lists
-// its (env, location or pair) items with a prefix sum of the per-lane counts, and its lanes
-// take them 64 at a time: item j's lane finds the owning env by a binary search over the
-// prefix (shuffles), takes the owner's agent cells, location sets and row words by shuffle,
-// evaluates that one location or pair, and folds it into the owner's minimum with an LDS
-// atomic (the bounds are positive floats, ordered as their bit patterns).  The min is the same
-// whatever the order, so the outputs are identical (round 4, profiles/r04/bounds_compact/: the
-// same output digest, the GPU suite green on it).  It lifts the lanes active per VALU
-// instruction from 0.58 to 0.70 but runs 0.129-0.130 ms against 0.118-0.119 at C5: most
-// (env, configuration) pairs have 0 or 1 location, so the walk has little divergence to remove,
-// and the prefix sum, the owner search (shuffles) and the LDS fold cost more VALU and LDS
-// instructions per wave (925 / 98 against 869 / 65) than the idle lanes did.  So it is off.
+// instruction, profiles/r04/c5/pmc_c5.json).  A wave-compacted walk (the wave's (env, location)
+// items by a prefix sum, one per lane, folded by LDS atomics) gave the same outputs with 0.70 of
+// the lanes active but ran 0.129 ms against 0.118 at C5, where most (env, configuration) pairs
+// have 0 or 1 location; it was removed in round 5 (profiles/r04/bounds_compact/).
 template <int A, int K, bool W>
 __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                            const uint8_t* __restrict__ blob_g,
                                                            float* __restrict__ lb, uint8_t* __restrict__ doable) {
     extern __shared__ uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
-    __shared__ uint32_t minv[kBlock];
     stage_roll_tables(R, blob_g, blob_w, subs);
     const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
     const int i0 = (int)(blockIdx.y * R.nsub / gridDim.y), i1 = (int)((blockIdx.y + 1) * R.nsub / gridDim.y);
-    if (!OC_BOUNDS_COMPACT) {
-        for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-            const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
-            ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
-            for (int i = i0; i < i1; ++i) {
-                float v;
-                const bool ok = ops.full_bound(r, subs[i], v);
-                lb[i * P + e] = v;
-                doable[i * P + e] = ok ? 1 : 0;
-            }
-        }
-        return;
-    }
-    const int lane = (int)(threadIdx.x & 63u), wbase = (int)(threadIdx.x & ~63u);
-    const float per = (float)R.L.perimeter;
-    // wave-uniform env loop: every lane of the wave runs the shuffles
-    for (int64_t e0 = blockIdx.x * (int64_t)kBlock + wbase; e0 < R.B; e0 += (int64_t)gridDim.x * kBlock) {
-        const int64_t e = e0 + lane;
-        const bool valid = e < R.B;
-        const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, valid ? e : e0);
+    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
+        const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
         ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
         for (int i = i0; i < i1; ++i) {
-            const ocro::Sub& s = subs[i];
-            ops.bound_config(s);
-            int ag0, ag1;
-            float pen;
-            ops.bound_agents(r, s, ag0, ag1, pen);
-            const bool walk = valid && (s.kind == 1 || s.kind == 2 || s.kind == 3);
-            const uint32_t setA = walk ? ops.obj_set(r, s.start[0], s.kind == 3) : 0u;
-            const uint32_t setB = walk && s.kind == 2 ? ops.obj_set(r, s.start[1], false) : 0u;
-            const uint32_t cnt = s.kind == 2 ? __popc(setA) * __popc(setB) : __popc(setA);
-            const uint32_t incl = wave_scan(cnt), off = incl - cnt;
-            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-            minv[threadIdx.x] = __float_as_uint(per + 1.0f);
-            wave_lds_sync();
-            const int bl = s.kind == 1 ? R.L.cut_off : R.L.deliv_off;
-            const int nb = s.kind == 1 ? R.L.ncut : R.L.ndeliv;
-            const uint8_t* dm = blob + R.L.dmin_off + (s.kind == 1 ? 0 : R.L.nnodes);
-            for (uint32_t base = 0; base < total; base += 64u) {  // wave-uniform
-                const uint32_t j = base + (uint32_t)lane;
-                int own = 0;  // the last lane whose offset is <= j: item j's env
-#pragma unroll
-                for (int stp = 32; stp > 0; stp >>= 1) own = shfl32(off, own + stp) <= j ? own + stp : own;
-                const uint32_t t = j - shfl32(off, own);
-                const uint32_t oA = shfl32(setA, own), oB = shfl32(setB, own);
-                const int oag0 = (int)shfl32((uint32_t)ag0, own), oag1 = (int)shfl32((uint32_t)ag1, own);
-                ocro::RowT<K, W> ro;  // the owner's cells: agent x / y and item locations
-                ro.x = shfl32(r.x, own);
-                ro.y = shfl32(r.y, own);
-#pragma unroll
-                for (int q = 0; q < ocro::RowT<K, W>::NL; ++q) ro.loc[q] = shfl64(r.loc[q], own);
-                if (j < total) {
-                    float b;
-                    if (s.kind == 2) {
-                        const uint32_t ncB = (uint32_t)__popc(oB);
-                        const int Ac = ops.src_cell(ro, kth_bit(oA, (int)(t / ncB)));
-                        const int Bc = ops.src_cell(ro, kth_bit(oB, (int)(t % ncB)));
-                        b = ops.helper(s, oag0, oag1, Ac, Bc);
-                    } else {
-                        b = ops.helper_static(s, oag0, oag1, ops.src_cell(ro, kth_bit(oA, (int)t)), bl, nb, dm);
-                    }
-                    atomicMin(&minv[wbase + own], __float_as_uint(b));
-                }
-            }
-            wave_lds_sync();
-            const float d = __uint_as_float(minv[threadIdx.x]);
-            if (valid) {
-                lb[i * P + e] = d + pen;
-                doable[i * P + e] = (s.kind == 0 || d < per) ? 1 : 0;
-            }
+            float v;
+            const bool ok = ops.full_bound(r, subs[i], v);
+            lb[i * P + e] = v;
+            doable[i * P + e] = ok ? 1 : 0;
         }
     }
 }
@@ -1554,6 +1464,7 @@ __global__ __launch_bounds__(kBlock) void oc_stats_reduce_kernel(const uint64_t*
 }
 
 thread_local std::string g_last_error;
+thread_local uint64_t g_err_gen = 0;  // failures on this thread so far (ErrScope compares)
 
 int fail(int code, const char* fmt, ...) {
     char buf[512];
@@ -1562,6 +1473,7 @@ int fail(int code, const char* fmt, ...) {
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
     g_last_error = buf;
+    ++g_err_gen;
     return code;
 }
 
@@ -1597,7 +1509,24 @@ struct oc_handle {
     ocro::RollLevel step_lv;         // W, H, enc; tile_off 0 (the tile table alone)
     uint8_t* wide_tiles = nullptr;   // device: tile class per cell (W * H rounded up to 4 bytes)
     uint8_t wide_tiles_host[ocro::kMaxCellsWide];
+    int32_t lik_form = OC_LIK_FORM_AUTO;  // oc_set_likelihood_form
+    mutable std::string last_error;       // oc_get_last_error: the last failed call on this handle
 };
+
+// An entry point's failure is also recorded on its handle (oc_get_last_error): the scope sees
+// whether fail() ran on this thread while the call was in progress.
+struct ErrScope {
+    const oc_handle* h;
+    uint64_t gen;
+    explicit ErrScope(const oc_handle* hh) : h(hh), gen(g_err_gen) {}
+    ~ErrScope() {
+        if (h != nullptr && g_err_gen != gen) h->last_error = g_last_error;
+    }
+};
+
+// Device entry points refuse a host-only handle (oc_create with OC_DEVICE_HOST).
+#define OC_NEED_DEVICE(h_) \
+    if ((h_)->device < 0) return fail(OC_EINVAL, "host-only handle (OC_DEVICE_HOST): this entry point needs a device")
 
 // Statistics rows, shared by the blocks of every kernel modulo the row count; oc_step_n's
 // completion tickets follow them (ticket_base; zero between launches).
@@ -1740,6 +1669,25 @@ int oc_abi_version(void) { return OC_ABI_VERSION; }
 
 const char* oc_last_error(void) { return g_last_error.c_str(); }
 
+int oc_get_last_error(const oc_handle* h, char* buf, int64_t size) {
+    if (h == nullptr) return fail(OC_EINVAL, "bad argument");
+    const int64_t n = (int64_t)h->last_error.size();
+    if (buf != nullptr && size > 0) {
+        const int64_t c = n < size - 1 ? n : size - 1;
+        memcpy(buf, h->last_error.data(), (size_t)c);
+        buf[c] = '\0';
+    }
+    return (int)n;
+}
+
+int oc_set_likelihood_form(oc_handle* h, int32_t form) {
+    if (h == nullptr) return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    if (form != OC_LIK_FORM_AUTO && form != OC_LIK_FORM_GROUPED) return fail(OC_EINVAL, "likelihood form %d", form);
+    h->lik_form = form;
+    return OC_OK;
+}
+
 int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_t device, oc_handle** out) {
     if (lv == nullptr || out == nullptr) return fail(OC_EINVAL, "null argument");
     const int W = lv->width, H = lv->height;
@@ -1750,6 +1698,8 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     if (lv->num_items < 0 || lv->num_items > OC_MAX_ITEMS) return fail(OC_ELEVEL, "num_items %d", lv->num_items);
     if (lv->num_goals < 1 || lv->num_goals > OC_MAX_GOALS) return fail(OC_ELEVEL, "num_goals %d", lv->num_goals);
     if (max_T < 0 || max_T > 65535) return fail(OC_EINVAL, "max_T %d", max_T);
+    if (device < OC_DEVICE_HOST) return fail(OC_EINVAL, "device %d", device);
+    const bool host_only = device == OC_DEVICE_HOST;  // no HIP call at all
     const bool wide = W * H > ocro::kMaxCells;  // u16 cell ids: the scalar step (oc_step_wide_kernel)
     LevelArgs L{};
     L.W = W;
@@ -1843,7 +1793,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     h->device = device;
     h->args = L;
     h->cus = 256;  // MI355X; replaced by the device's own count when there is a device
-    {
+    if (!host_only) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
             h->cus = cus;
@@ -1856,7 +1806,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
         const int n = ocro::build_roll_level(h->roll, h->roll_blob_host, W, H, lv->tiles, lv->encoding);
         if (n < 0) {
             h->roll.nnodes = -1;
-        } else {
+        } else if (!host_only) {
             h->roll_blob_bytes = h->roll.blob_bytes;
             if (hipSetDevice(device) != hipSuccess ||
                 hipMalloc(&h->roll_blob, (size_t)h->roll_blob_bytes) != hipSuccess ||
@@ -1867,7 +1817,8 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
             }
         }
     }
-    if (wide) {
+    if (h->roll.nnodes >= 0) h->roll_blob_bytes = h->roll.blob_bytes;
+    if (wide && !host_only) {
         const size_t tb = (size_t)((W * H + 3) & ~3);
         if (hipSetDevice(device) != hipSuccess || hipMalloc(&h->wide_tiles, tb) != hipSuccess ||
             hipMemcpy(h->wide_tiles, h->wide_tiles_host, tb, hipMemcpyHostToDevice) != hipSuccess) {
@@ -1882,6 +1833,7 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
 int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, int64_t node_of_len, uint8_t* dist,
                     int64_t dist_len) {
     if (h == nullptr || num_nodes == nullptr) return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
     if (h->roll.nnodes < 0)
         return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (%d on a level of more than 255 cells) or a distance of 254", ocro::kMaxNodes, ocro::kMaxNodesWide);
     const int n = h->roll.nnodes, cells = h->level.width * h->level.height;
@@ -1906,6 +1858,7 @@ int oc_destroy(oc_handle* h) {
 
 int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
     if (h == nullptr || out == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
     const int A = h->A, K = h->K;
     out->pitch = pitch_for(B);
     out->num_agents = A;
@@ -2033,6 +1986,8 @@ static int step_wide(const oc_handle* h, const void* sin, void* sout, const uint
 
 int oc_reset(const oc_handle* h, void* state, int64_t B, void* stream) {
     if (h == nullptr || state == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    OC_NEED_DEVICE(h);
     if (B == 0) return OC_OK;
     if (h->wide) {
         WideArgs R;
@@ -2061,6 +2016,8 @@ int oc_step(const oc_handle* h, const void* state_in, void* state_out, const uin
             uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* stats, int64_t B, void* stream) {
     if (h == nullptr || state_in == nullptr || state_out == nullptr || actions == nullptr || B < 0)
         return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    OC_NEED_DEVICE(h);
     if (B == 0) return OC_OK;
     if (((uintptr_t)state_in | (uintptr_t)state_out | (uintptr_t)actions | (uintptr_t)exec_actions |
          (uintptr_t)coll_mask) & 15u)
@@ -2085,6 +2042,7 @@ int oc_cpu_step(const oc_handle* h, const void* state_in, void* state_out, const
                 uint8_t* exec_actions, uint8_t* coll_mask, uint64_t* totals, int64_t B, int32_t nthreads) {
     if (h == nullptr || state_in == nullptr || state_out == nullptr || actions == nullptr || B < 0 || nthreads < 0)
         return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
     if (B == 0) return OC_OK;
     const int64_t P = pitch_for(B), words = (B + kEPL - 1) / kEPL;
     if (nthreads == 0) nthreads = (int32_t)std::thread::hardware_concurrency();
@@ -2109,15 +2067,30 @@ int oc_cpu_step(const oc_handle* h, const void* state_in, void* state_out, const
 #undef OC_CPU_STEP
         return OC_OK;
     };
-    int rc = OC_OK;
-    if (nt == 1) {
-        rc = run(0);
-    } else {
+    // Every range runs the same (A, K, MODE) dispatch: range 0 runs on the calling thread first,
+    // so a dispatch failure sets this thread's message; a worker's failure message is carried
+    // back to it.  Ranges whose thread cannot be started run here too.
+    int rc = run(0);
+    if (rc == OC_OK && nt > 1) {
         std::vector<std::thread> pool;
         std::vector<int> rcs((size_t)nt, OC_OK);
-        for (int64_t i = 0; i < nt; ++i) pool.emplace_back([&, i] { rcs[(size_t)i] = run(i); });
+        std::vector<std::string> msgs((size_t)nt);
+        int64_t started = 1;
+        try {
+            for (; started < nt; ++started)
+                pool.emplace_back([&, i = started] {
+                    rcs[(size_t)i] = run(i);
+                    if (rcs[(size_t)i] != OC_OK) msgs[(size_t)i] = g_last_error;
+                });
+        } catch (const std::exception&) {  // no more threads: the rest of the ranges run here
+        }
+        for (int64_t i = started; i < nt; ++i) {
+            rcs[(size_t)i] = run(i);
+            if (rcs[(size_t)i] != OC_OK) msgs[(size_t)i] = g_last_error;
+        }
         for (auto& t : pool) t.join();
-        for (int r : rcs) rc = rc != OC_OK ? rc : r;
+        for (int64_t i = 1; i < nt && rc == OC_OK; ++i)
+            if (rcs[(size_t)i] != OC_OK) rc = fail(rcs[(size_t)i], "%s", msgs[(size_t)i].c_str());
     }
     if (rc == OC_OK && totals != nullptr)
         for (int64_t i = 0; i < nt; ++i)
@@ -2130,6 +2103,8 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
               void* stream) {
     if (h == nullptr || state_in == nullptr || state_out == nullptr || actions == nullptr || B < 0 || n < 0)
         return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    OC_NEED_DEVICE(h);
     if (totals != nullptr && stats == nullptr) return fail(OC_EINVAL, "totals need the stats buffer");
     if (totals != nullptr && (uintptr_t)totals & 7u) return fail(OC_EINVAL, "totals must be 8-byte aligned");
     if (B == 0 || n == 0) return totals != nullptr && B > 0 ? oc_stats_reduce(h, stats, B, totals, stream) : OC_OK;
@@ -2249,6 +2224,8 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     if (h == nullptr || state_in == nullptr || state_out == nullptr || actions == nullptr || subtasks == nullptr ||
         out_flags == nullptr || lower_bound == nullptr || B < 0)
         return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    OC_NEED_DEVICE(h);
     if (state_in == state_out) return fail(OC_EINVAL, "oc_rollout is out of place");
     if (((uintptr_t)lower_bound & 3u) || ((uintptr_t)state_in & 1u) || ((uintptr_t)state_out & 1u))
         return fail(OC_EINVAL, "misaligned buffer");
@@ -2273,6 +2250,8 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     if (h == nullptr || state == nullptr || taken == nullptr || subtasks == nullptr || likelihood == nullptr ||
         out_flags == nullptr || B < 0)
         return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    OC_NEED_DEVICE(h);
     if (self_agent < 0 || self_agent >= h->A) return fail(OC_EINVAL, "self_agent %d", self_agent);
     if (((uintptr_t)likelihood & 7u) || ((uintptr_t)state & 1u)) return fail(OC_EINVAL, "misaligned buffer");
     RollArgs R;
@@ -2285,9 +2264,8 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     // 0.39 ms per 2^18 C5 rows against 8 per CU), 8 per CU with 8-lane groups (3-4 resident)
     // the compacted form's row slots take up to kLikCompactLds more LDS: a level whose tables
     // leave less than that runs the grouped form (same outputs)
-    // (OC_LIK_GROUPED set in the environment forces the grouped form: the parity test of that path)
-    static const bool force_grouped = std::getenv("OC_LIK_GROUPED") != nullptr;
-    const bool compact = OC_LIK_COMPACT && !force_grouped &&
+    // (oc_set_likelihood_form(h, OC_LIK_FORM_GROUPED) forces the grouped form: the parity test of that path)
+    const bool compact = OC_LIK_COMPACT && h->lik_form == OC_LIK_FORM_AUTO &&
                          h->roll.lds_bytes + kLikCompactLds + (int)sizeof(ocro::Sub) * OC_MAX_SUBTASKS <= kLdsPerCu;
     const int64_t rows_per_block = compact ? (kBlock / 64) * lik_rows_per_round((int)G) : kBlock / G;
     const int64_t need = (B + rows_per_block - 1) / rows_per_block, cap = (int64_t)h->cus * (any_joint ? 16 : 8);
@@ -2317,6 +2295,8 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
     if (h == nullptr || state == nullptr || subtasks == nullptr || lower_bound == nullptr || doable == nullptr ||
         B < 0)
         return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    OC_NEED_DEVICE(h);
     if (((uintptr_t)lower_bound & 3u) || ((uintptr_t)state & 1u)) return fail(OC_EINVAL, "misaligned buffer");
     RollArgs R;
     if (const int rc = roll_args(h, subtasks, num_subtasks, B, R)) return rc;
@@ -2351,6 +2331,8 @@ int oc_render_ordered(const oc_handle* h, const void* state, const uint8_t* draw
     if (h == nullptr || state == nullptr || atlas == nullptr || background == nullptr || desc == nullptr ||
         out == nullptr || B < 0)
         return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    OC_NEED_DEVICE(h);
     const int W = h->level.width, H = h->level.height;
     const int max_w = h->wide ? kRenderMaxWWide : kRenderMaxW;
     if (W > max_w) return fail(OC_ELEVEL, "render: width %d > %d", W, max_w);
@@ -2394,6 +2376,8 @@ int oc_render_ordered(const oc_handle* h, const void* state, const uint8_t* draw
 int oc_gen_actions(const oc_handle* h, uint8_t* actions, int64_t B, int64_t env_offset, int64_t step,
                    uint64_t seed, void* stream) {
     if (h == nullptr || actions == nullptr || B < 0 || env_offset < 0 || step < 0) return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    OC_NEED_DEVICE(h);
     if (B == 0) return OC_OK;
     const int64_t P = pitch_for(B);
     hipLaunchKernelGGL(oc_gen_actions_kernel, dim3((unsigned)(P / kBlock)), dim3(kBlock), 0, (hipStream_t)stream,
@@ -2403,6 +2387,8 @@ int oc_gen_actions(const oc_handle* h, uint8_t* actions, int64_t B, int64_t env_
 
 int oc_state_checksum(const oc_handle* h, const void* state, int64_t B, uint64_t* out, void* stream) {
     if (h == nullptr || state == nullptr || out == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    OC_NEED_DEVICE(h);
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(out, 0, sizeof(uint64_t), s) != hipSuccess) return hip_check("oc_state_checksum memset");
     if (B == 0) return OC_OK;
@@ -2442,6 +2428,7 @@ int oc_state_checksum(const oc_handle* h, const void* state, int64_t B, uint64_t
 
 int oc_stats_size(const oc_handle* h, int64_t B, int64_t* nbytes) {
     if (h == nullptr || nbytes == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
     const int64_t groups = ((int64_t)h->cus * 5 + kTicketGroup - 1) / kTicketGroup;  // oc_step_n's grid <= 5 blocks per CU
     *nbytes = (ticket_base(stats_rows(h, B)) + (1 + groups) * kTicketStride) * (int64_t)sizeof(uint64_t);
     return OC_OK;
@@ -2449,6 +2436,8 @@ int oc_stats_size(const oc_handle* h, int64_t B, int64_t* nbytes) {
 
 int oc_stats_reduce(const oc_handle* h, const uint64_t* stats, int64_t B, uint64_t* totals, void* stream) {
     if (h == nullptr || stats == nullptr || totals == nullptr || B < 0) return fail(OC_EINVAL, "bad argument");
+    ErrScope es_(h);
+    OC_NEED_DEVICE(h);
     const int64_t rows = stats_rows(h, B);
     hipLaunchKernelGGL(oc_stats_reduce_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, stats, rows, totals);
     return hip_check("oc_stats_reduce launch");

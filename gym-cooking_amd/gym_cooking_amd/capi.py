@@ -21,7 +21,9 @@ OC_MAX_NARROW_CELLS = 255   # up to this many cells: byte cell ids; more ("wide"
 OC_MAX_GOALS = 4
 OC_PITCH_ALIGN = 4096
 OC_NSTATS = 5
-OC_ABI_VERSION = 8  # include/oc_engine.h
+OC_ABI_VERSION = 9  # include/oc_engine.h
+OC_DEVICE_HOST = -1  # oc_create: a host-only handle (no HIP call)
+OC_LIK_FORM_AUTO, OC_LIK_FORM_GROUPED = 0, 1
 OC_EINVAL, OC_EHIP, OC_ELEVEL = -1, -2, -3
 
 OC_FLAG_DONE = 0x01
@@ -34,7 +36,8 @@ OC_STAT_NAMES = ("episodes", "successes", "steps", "collisions", "errors")
 EXPORTED_SYMBOLS = (
     "oc_abi_version", "oc_last_error", "oc_create", "oc_destroy", "oc_get_layout", "oc_reset",
     "oc_step", "oc_step_n", "oc_cpu_step", "oc_rollout", "oc_nav_likelihood", "oc_subtask_bounds", "oc_reachability", "oc_render", "oc_render_ordered",
-    "oc_gen_actions", "oc_state_checksum", "oc_stats_size", "oc_stats_reduce",
+    "oc_gen_actions", "oc_state_checksum", "oc_stats_size", "oc_stats_reduce", "oc_get_last_error",
+    "oc_set_likelihood_form",
 )
 
 
@@ -197,6 +200,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.oc_render.argtypes = [vp, vp, vp, vp, ctypes.POINTER(OcRenderDesc), vp, i64, vp]
     lib.oc_render_ordered.restype = ctypes.c_int
     lib.oc_render_ordered.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(OcRenderDesc), vp, i64, vp]
+    lib.oc_get_last_error.restype = ctypes.c_int
+    lib.oc_get_last_error.argtypes = [vp, ctypes.c_char_p, i64]
+    lib.oc_set_likelihood_form.restype = ctypes.c_int
+    lib.oc_set_likelihood_form.argtypes = [vp, i32]
     lib.oc_cpu_step.restype = ctypes.c_int
     lib.oc_cpu_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i32]
     lib.oc_step_n.restype = ctypes.c_int

@@ -247,6 +247,17 @@ class OvercookedBatch:
                 self._stream())
         return _bound(self.lib.oc_subtask_bounds, args)
 
+    def set_likelihood_form(self, form: int) -> None:
+        """oc_set_likelihood_form: capi.OC_LIK_FORM_AUTO (default) or OC_LIK_FORM_GROUPED (the
+        grouped likelihood kernel on any level; the same outputs, for its parity test)."""
+        capi.check(self.lib.oc_set_likelihood_form(self._h, int(form)))
+
+    def last_error(self) -> str:
+        """oc_get_last_error: the message of the last failed call on this handle."""
+        buf = ctypes.create_string_buffer(512)
+        self.lib.oc_get_last_error(self._h, buf, len(buf))
+        return buf.value.decode()
+
     def reachability(self):
         """The level's static reachability graph (oc_reachability): (node_of u16 [W*H*5] with
         0xFFFF = not a node, dist u8 [n][n] with 0xFF = no path)."""
@@ -304,7 +315,9 @@ class CpuStepper:
         self.lib = capi.load_library()
         self._desc = capi.level_desc(level, num_agents)
         h = ctypes.c_void_p()
-        capi.check(self.lib.oc_create(ctypes.byref(self._desc), num_agents, max_T, 0, ctypes.byref(h)))
+        # a host-only handle: oc_create makes no HIP call (no device query, no device tables)
+        capi.check(self.lib.oc_create(ctypes.byref(self._desc), num_agents, max_T, capi.OC_DEVICE_HOST,
+                                      ctypes.byref(h)))
         self._h = h
         lay = capi.OcLayout()
         capi.check(self.lib.oc_get_layout(self._h, self.B, ctypes.byref(lay)))

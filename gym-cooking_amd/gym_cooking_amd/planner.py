@@ -444,6 +444,11 @@ class E2E_BRTDP:
         new = object.__new__(E2E_BRTDP)
         new.__dict__ = self.__dict__.copy()
         new._tmemo = {}  # T's lru_cache is keyed by the planner object
+        # a belief update's memo belongs to the delegator's own planner and that update only
+        # (delegation.py drops it when the update ends): a copy made during an update must not
+        # keep it alive or read it later
+        if "_bayes_memo" in new.__dict__:
+            new._bayes_memo = None
         return new
 
     def _configure(self, env, subtask, subtask_agent_names, other_agent_planners=None):

@@ -17,7 +17,8 @@
  *
  * Conventions
  *  - All entry points return 0 on success and a negative OC_E* code on failure; the message
- *    of the last failure on the calling thread is available from oc_last_error().
+ *    of the last failure on the calling thread is available from oc_last_error(), and the
+ *    last failure of a call on a given handle from oc_get_last_error(h, buf, size).
  *  - Every buffer is caller-owned device memory (e.g. torch ROCm tensors); the engine never
  *    allocates in oc_step / oc_reset / oc_gen_actions, so they are hipGraph-capturable.
  *  - `stream` is a hipStream_t passed as void* (NULL = the null stream).  Calls are
@@ -35,7 +36,7 @@
 extern "C" {
 #endif
 
-#define OC_ABI_VERSION 8
+#define OC_ABI_VERSION 9
 
 #define OC_MAX_AGENTS 4
 #define OC_MAX_ITEMS 16  /* item slots: K = 4, 8 or 16 per level */
@@ -153,8 +154,17 @@ typedef struct oc_handle oc_handle;
 int oc_abi_version(void);
 const char* oc_last_error(void);
 
+/* The message of the last failed call on handle h (the same text oc_last_error() gave the
+ * calling thread then), copied NUL-terminated into buf (at most size bytes); "" when no call
+ * on h has failed.  Returns the message length. */
+int oc_get_last_error(const oc_handle* h, char* buf, int64_t size);
+
 /* Static level tables + episode settings.  max_T = --max-num-timesteps (main.py:24; 0 = no
- * limit).  device = HIP ordinal the handle's launches target (recorded, validated). */
+ * limit).  device = HIP ordinal the handle's launches target (recorded, validated), or
+ * OC_DEVICE_HOST: a host-only handle that makes no HIP call at all (no device query, no
+ * device tables); only the host entry points (oc_get_layout, oc_cpu_step, oc_reachability,
+ * oc_stats_size) take it, the device ones return OC_EINVAL. */
+#define OC_DEVICE_HOST (-1)
 int oc_create(const oc_level_desc* level, int32_t num_agents, int32_t max_T, int32_t device,
               oc_handle** out);
 int oc_destroy(oc_handle* h);
@@ -327,6 +337,14 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
 int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* taken, const uint8_t* alloc,
                       const oc_subtask* subtasks, int32_t num_subtasks, int32_t self_agent, double beta,
                       double none_action_prob, double* likelihood, uint8_t* out_flags, int64_t B, void* stream);
+
+/* Which kernel oc_nav_likelihood runs on handle h: OC_LIK_FORM_AUTO (the default: the
+ * compacted form, whose rollouts are spread over the wave, where the level's tables leave it
+ * the LDS; else the grouped form) or OC_LIK_FORM_GROUPED (the grouped form always).  The two
+ * give the same bits; this exists so a test can run the grouped form on any level. */
+#define OC_LIK_FORM_AUTO 0
+#define OC_LIK_FORM_GROUPED 1
+int oc_set_likelihood_form(oc_handle* h, int32_t form);
 
 /* The level's static reachability graph, World.make_reachability_graph (utils/world.py:67-108),
  * as built by oc_create: nodes are (cell, approach) with approach 0..3 = World.NAV_ACTIONS (the

@@ -94,3 +94,58 @@ def test_integration_stub_matches_binding():
     lib = capi.load_library()
     for name in re.findall(r"lib\.(oc_\w+)\.argtypes", code):
         assert hasattr(lib, name), name
+
+
+def test_host_only_handle_and_handle_errors():
+    """oc_create(..., OC_DEVICE_HOST) makes a host-only handle: no HIP call at all (oc_create
+    skips the device query and the device tables).  Its device entry points refuse it with
+    OC_EINVAL before touching HIP, its host ones work, and each failure is also recorded on the
+    handle (oc_get_last_error)."""
+    if not os.path.isfile(capi.LIB_PATH):
+        pytest.skip("liboc_engine.so not built")
+    lib = capi.load_library()
+    lv = levels.load_level("partial-divider_salad")
+    d = capi.level_desc(lv, 2)
+    h = ctypes.c_void_p()
+    assert lib.oc_create(ctypes.byref(d), 2, 100, capi.OC_DEVICE_HOST, ctypes.byref(h)) == 0
+    buf = ctypes.create_string_buffer(256)
+    assert lib.oc_get_last_error(h, buf, len(buf)) == 0 and buf.value == b""
+    lay = capi.OcLayout()
+    assert lib.oc_get_layout(h, 4096, ctypes.byref(lay)) == 0
+    s = (ctypes.c_uint8 * lay.state_bytes)()
+    a = (ctypes.c_uint8 * (2 * lay.pitch))()
+    assert lib.oc_step(h, s, s, a, None, None, None, 4096, None) == capi_err("EINVAL")
+    assert b"host-only handle" in lib.oc_last_error()
+    n = lib.oc_get_last_error(h, buf, len(buf))
+    assert n > 0 and buf.value == lib.oc_last_error()
+    small = ctypes.create_string_buffer(8)  # truncated, NUL-terminated; the full length returned
+    assert lib.oc_get_last_error(h, small, len(small)) == n and len(small.value) == 7
+    for call in (lambda: lib.oc_reset(h, s, 4096, None),
+                 lambda: lib.oc_gen_actions(h, a, 4096, 0, 0, 0, None),
+                 lambda: lib.oc_state_checksum(h, s, 4096, s, None)):
+        assert call() == capi_err("EINVAL") and b"host-only handle" in lib.oc_last_error()
+    nn = ctypes.c_int32()
+    assert lib.oc_reachability(h, ctypes.byref(nn), None, 0, None, 0) == 0 and nn.value > 0
+    assert lib.oc_set_likelihood_form(h, 7) == capi_err("EINVAL")
+    assert lib.oc_get_last_error(h, buf, len(buf)) > 0 and b"likelihood form 7" in buf.value
+    assert lib.oc_set_likelihood_form(h, capi.OC_LIK_FORM_GROUPED) == 0
+    assert lib.oc_destroy(h) == 0
+    assert lib.oc_create(ctypes.byref(d), 2, 100, -2, ctypes.byref(h)) == capi_err("EINVAL")
+
+
+def test_cpu_stepper_on_host_only_handle():
+    """engine.CpuStepper steps on a host-only handle (oc_cpu_step), threaded, and its handle
+    refuses a device call."""
+    if not os.path.isfile(capi.LIB_PATH):
+        pytest.skip("liboc_engine.so not built")
+    import numpy as np
+    from gym_cooking_amd.engine import CpuStepper
+    cs = CpuStepper("partial-divider_salad", 2, 70000, nthreads=4)
+    s0 = cs.new_state()
+    s1 = np.empty_like(s0)
+    act = np.full(2 * cs.pitch, 3, np.uint8)
+    tot = np.zeros(5, np.uint64)
+    cs.step(s0, s1, act, totals=tot)
+    assert not np.array_equal(s0, s1)
+    lib = cs.lib
+    assert lib.oc_reset(cs._h, s1.ctypes.data, cs.B, None) == capi_err("EINVAL")

@@ -11,9 +11,11 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_lik(level, A, B, s, taken, subs, alloc, self_agent, beta, nap):
+def _gpu_lik(level, A, B, s, taken, subs, alloc, self_agent, beta, nap, form=None):
     from gym_cooking_amd.engine import OvercookedBatch
     eb = OvercookedBatch(level, A, B, max_T=100, device="cuda:0")
+    if form is not None:
+        eb.set_likelihood_form(form)
     a = torch.from_numpy(alloc).cuda() if alloc is not None else None
     v, f = eb.nav_likelihood(torch.from_numpy(s).cuda(), torch.from_numpy(taken).cuda(), subs, self_agent, beta, nap, a)
     torch.cuda.synchronize()
@@ -75,32 +77,16 @@ def _lik_case(kind):
     return s, acts, subs, alloc
 
 
-def _lik_child(kind, out):
-    s, acts, subs, alloc = _lik_case(kind)
-    v, f = _gpu_lik("full-divider_salad", 4, 9000, s, acts, subs, alloc, 1, 1.3, 0.5)
-    np.savez(out, v=v, f=f)
-
-
 @pytest.mark.parametrize("kind", ["joint", "single"])
-def test_grouped_form_equals_compacted(kind, tmp_path):
+def test_grouped_form_equals_compacted(kind):
     """The product runs the compacted likelihood kernel; the grouped one remains for levels whose
-    tables leave too little LDS (oc_engine.hip, oc_nav_likelihood).  OC_LIK_GROUPED forces the
-    grouped form: a child process computes the same rows with it, bit for bit (that the switch
-    selects the grouped kernels: profiles/r04/lik_compact/lik_kernel_stats_grouped_env.csv, the
-    child's code under rocprofv3)."""
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    root = os.path.dirname(here)
-    env = dict(os.environ, OC_LIK_GROUPED="1",
-               PYTHONPATH=os.pathsep.join([here, root, os.path.join(root, "gym-cooking_amd")]))
-    out = str(tmp_path / "grouped.npz")
-    code = "import test_likelihood_gpu as t; t._lik_child(%r, %r)" % (kind, out)
-    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=300, cwd=here)
-    g = np.load(out)
+    tables leave too little LDS (oc_engine.hip, oc_nav_likelihood).  oc_set_likelihood_form
+    (OC_LIK_FORM_GROUPED) forces the grouped form on a handle: the same rows with it, bit for bit
+    (that the switch selects the grouped kernels: profiles/r04/lik_compact/
+    lik_kernel_stats_grouped_env.csv, measured with the round-4 switch)."""
     s, acts, subs, alloc = _lik_case(kind)
+    g = _gpu_lik("full-divider_salad", 4, 9000, s, acts, subs, alloc, 1, 1.3, 0.5, form=capi.OC_LIK_FORM_GROUPED)
     v, f = _gpu_lik("full-divider_salad", 4, 9000, s, acts, subs, alloc, 1, 1.3, 0.5)
     assert (f == capi.LIK_OK).sum() > 100
-    assert np.array_equal(f, g["f"])
-    assert np.array_equal(v.view(np.uint64), g["v"].view(np.uint64))
+    assert np.array_equal(f, g[1])
+    assert np.array_equal(v.view(np.uint64), g[0].view(np.uint64))
