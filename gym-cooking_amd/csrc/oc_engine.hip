@@ -626,26 +626,49 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
                                                             float* __restrict__ lb) {
     extern __shared__ uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
-    stage_roll_tables(R, blob_g, blob_w, subs);
-    const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
     using PL = Planes<A, K, W>;
-    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-        ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
-        const uint16_t t = ((const uint16_t*)(sin + PL::T * P))[e];
-        const uint8_t fl_in = sin[PL::F * P + e];
-        const int ai = alloc != nullptr ? alloc[e] : 0;
+    // a row's inputs: its state, t, flags, alloc id and every agent's action (the subtask's
+    // agents are known only after the configuration is read from LDS)
+    struct In {
+        ocro::RowT<K, W> r;
+        uint32_t t, fl, ai, aw;
+    };
+    auto load = [&](int64_t e) {
+        In d;
+        d.r = load_row<A, K, W>(sin, P, e);
+        d.t = ((const uint16_t*)(sin + PL::T * P))[e];
+        d.fl = sin[PL::F * P + e];
+        d.ai = alloc != nullptr ? alloc[e] : 0u;
+        d.aw = 0u;
+#pragma unroll
+        for (int a = 0; a < A; ++a) d.aw |= (uint32_t)act[a * P + e] << (8 * a);
+        return d;
+    };
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    // the first row's loads go out before the tables are staged: their latencies overlap
+    // (tools/rolltl.hip, round 5)
+    In d;
+    if (e < R.B) d = load(e);
+    stage_roll_tables(R, blob_g, blob_w, subs);
+    const uint8_t* blob = (const uint8_t*)blob_w;
+    for (; e < R.B; e += stride) {
+        ocro::RowT<K, W> r = d.r;
         float bound = 0.0f;
         int f = OC_ROLL_BADALLOC;  // an alloc id past num_subtasks: the row is copied unchanged
-        if (ai < R.nsub) {
-            const ocro::Sub& s = subs[ai];
-            const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
+        if ((int)d.ai < R.nsub) {
+            const ocro::Sub& s = subs[d.ai];
+            const int c0 = (int)((d.aw >> (8 * s.agent[0])) & 0xFFu);
+            const int c1 = s.n == 2 ? (int)((d.aw >> (8 * s.agent[1])) & 0xFFu) : ocro::kNoop;
             ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             f = ops.run(r, s, c0, c1, bound);
         }
+        const uint32_t t = d.t, fl_in = d.fl;
+        if (e + stride < R.B) d = load(e + stride);
         store_row<A, K, W>(sout, P, e, r);
-        ((uint16_t*)(sout + PL::T * P))[e] = t;
-        sout[PL::F * P + e] = fl_in;
+        ((uint16_t*)(sout + PL::T * P))[e] = (uint16_t)t;
+        sout[PL::F * P + e] = (uint8_t)fl_in;
         out_flags[e] = (uint8_t)f;
         lb[e] = bound;
     }
@@ -1038,6 +1061,11 @@ struct WideArgs {
 // n steps of every env (oc_step: n = 1, no trajectory): the state stays in registers between
 // the steps; step r's state goes to traj[r] (when given), its executed actions and collision
 // mask to exec_out / coll_out at r * A * pitch / r * pitch; the final state to sout.
+// Round 5: four envs per lane, every plane read and written one dword per lane (256 B per wave
+// instruction, as the narrow kernels; round 4 moved one byte per lane, 64 B per instruction),
+// through buffer resources (an absent output's stores are dropped by its num_records = 0, so
+// every store is unconditional), nt stores, and the next step's action words loaded before the
+// current step runs.  The four envs step one after another through the scalar env_step.
 template <int A, int K>
 __global__ __launch_bounds__(kBlock) void oc_step_wide_kernel(WideArgs R, const uint8_t* __restrict__ tiles_g,
                                                               const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
@@ -1049,40 +1077,131 @@ __global__ __launch_bounds__(kBlock) void oc_step_wide_kernel(WideArgs R, const 
     for (int i = threadIdx.x; i < R.tile_words; i += kBlock) tiles_w[i] = ((const uint32_t*)tiles_g)[i];
     __syncthreads();
     using PL = Planes<A, K, true>;
-    const int64_t P = R.pitch;
+    using Row = ocro::RowT<K, true>;
+    const uint32_t P = (uint32_t)R.pitch;
+    const uint32_t nlanes = (uint32_t)((R.B + kEPL - 1) / kEPL);
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(sin, (int64_t)PL::NP * P);
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(sout ? (const void*)sout : (const void*)sin, sout ? (int64_t)PL::NP * P : 0);
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(act, (int64_t)n * A * P);
+    const __amdgpu_buffer_rsrc_t rt = make_rsrc(traj ? (const void*)traj : (const void*)sin, traj ? (int64_t)n * PL::NP * P : 0);
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(exec_out ? (const void*)exec_out : (const void*)sin,
+                                                exec_out ? (int64_t)n * A * P : 0);
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(coll_out ? (const void*)coll_out : (const void*)sin,
+                                                coll_out ? (int64_t)n * P : 0);
+    ocro::RowOps<A, K, true> ops(R.L, (const uint8_t*)tiles_w);
     StepStats st;
-    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-        ocro::RowT<K, true> r = load_row<A, K, true>(sin, P, e);
-        uint32_t t = ((const uint16_t*)(sin + PL::T * P))[e], fl = sin[PL::F * P + e];
-        ocro::RowOps<A, K, true> ops(R.L, (const uint8_t*)tiles_w);
-        for (int q = 0; q < n; ++q) {
-            uint32_t a = 0, ex, cm;
+    typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+    for (uint32_t g = blockIdx.x * (uint32_t)kBlock + threadIdx.x; g < nlanes; g += gridDim.x * (uint32_t)kBlock) {
+        const uint32_t vo = g * 4u;
+        uint32_t X[A], Y[A], H[A], LO[K], HI[K], M[K], wa[A], nx[A];
 #pragma unroll
-            for (int i = 0; i < A; ++i) a |= (uint32_t)act[((int64_t)q * A + i) * P + e] << (8 * i);
-            const uint32_t f = ops.env_step(r, t, fl, a, R.S, ex, cm);
-            if ((f & 1u) && !(fl & 1u)) {  // an episode ended (DONE newly set)
-                st.eps += 1u;
-                st.succ += (f >> 1) & 1u;
-                st.err += (f >> 2) & 1u;
-                st.steps += t;
-            }
-            st.coll += __popc(cm);
-            fl = f;
-            if (traj != nullptr) {
-                uint8_t* o = traj + (int64_t)q * PL::NP * P;
-                store_row<A, K, true>(o, P, e, r);
-                ((uint16_t*)(o + PL::T * P))[e] = (uint16_t)t;
-                o[PL::F * P + e] = (uint8_t)fl;
-            }
-            if (exec_out != nullptr) {
-#pragma unroll
-                for (int i = 0; i < A; ++i) exec_out[((int64_t)q * A + i) * P + e] = (uint8_t)(ex >> (8 * i));
-            }
-            if (coll_out != nullptr) coll_out[(int64_t)q * P + e] = (uint8_t)cm;
+        for (int a = 0; a < A; ++a) {
+            X[a] = bld32(rs, vo, a * P);
+            Y[a] = bld32(rs, vo, (PL::Y + a) * P);
+            H[a] = bld32(rs, vo, (PL::H + a) * P);
+            wa[a] = bld32(ra, vo, a * P);
         }
-        store_row<A, K, true>(sout, P, e, r);
-        ((uint16_t*)(sout + PL::T * P))[e] = (uint16_t)t;
-        sout[PL::F * P + e] = (uint8_t)fl;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            LO[j] = bld32(rs, vo, (PL::L + j) * P);
+            HI[j] = bld32(rs, vo, (PL::LH + j) * P);
+            M[j] = bld32(rs, vo, (PL::M + j) * P);
+        }
+        const auto tw0 = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(g * 8u), (int)(PL::T * P), 0);
+        uint32_t T[2] = {tw0[0], tw0[1]}, F = bld32(rs, vo, PL::F * P);
+        const int64_t rem = R.B - (int64_t)g * kEPL;
+        for (int q = 0; q < n; ++q) {
+#pragma unroll
+            for (int a = 0; a < A; ++a) nx[a] = q + 1 < n ? bld32(ra, vo, (uint32_t)((q + 1) * A + a) * P) : 0u;
+            uint32_t EX[A], CM = 0u;
+#pragma unroll
+            for (int a = 0; a < A; ++a) EX[a] = 0u;
+#pragma unroll
+            for (int k = 0; k < kEPL; ++k) {  // the lane's four envs, one after another
+                const int sh = 8 * k;
+                Row r;
+#pragma unroll
+                for (int a = 0; a < A; ++a) {
+                    r.x |= ((X[a] >> sh) & 0xFFu) << (8 * a);
+                    r.y |= ((Y[a] >> sh) & 0xFFu) << (8 * a);
+                    r.h |= ((H[a] >> sh) & 0xFFu) << (8 * a);
+                }
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const uint64_t c = ((LO[j] >> sh) & 0xFFu) | (((HI[j] >> sh) & 0xFFu) << 8);
+                    r.loc[j / Row::LPW] |= c << (Row::kLocBits * (j % Row::LPW));
+                    r.mask[j >> 3] |= (uint64_t)((M[j] >> sh) & 0xFFu) << (8 * (j & 7));
+                }
+                uint32_t t = (T[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                const uint32_t fl = (F >> sh) & 0xFFu;
+                uint32_t av = 0u, ex, cm;
+#pragma unroll
+                for (int a = 0; a < A; ++a) av |= ((wa[a] >> sh) & 0xFFu) << (8 * a);
+                const uint32_t f = ops.env_step(r, t, fl, av, R.S, ex, cm);
+                if (k < rem) {  // statistics over the batch's envs only
+                    if ((f & 1u) && !(fl & 1u)) {  // an episode ended (DONE newly set)
+                        st.eps += 1u;
+                        st.succ += (f >> 1) & 1u;
+                        st.err += (f >> 2) & 1u;
+                        st.steps += t;
+                    }
+                    st.coll += __popc(cm);
+                }
+                const uint32_t keep = ~(0xFFu << sh);
+#pragma unroll
+                for (int a = 0; a < A; ++a) {
+                    X[a] = (X[a] & keep) | ((uint32_t)r.ax(a) << sh);
+                    Y[a] = (Y[a] & keep) | ((uint32_t)r.ay(a) << sh);
+                    H[a] = (H[a] & keep) | ((uint32_t)r.ah(a) << sh);
+                    EX[a] |= ((ex >> (8 * a)) & 0xFFu) << sh;
+                }
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const uint32_t c = (uint32_t)r.il(j);
+                    LO[j] = (LO[j] & keep) | ((c & 0xFFu) << sh);
+                    HI[j] = (HI[j] & keep) | ((c >> 8) << sh);
+                    M[j] = (M[j] & keep) | ((uint32_t)r.im(j) << sh);
+                }
+                T[k >> 1] = (T[k >> 1] & ~(0xFFFFu << (16 * (k & 1)))) | (t << (16 * (k & 1)));
+                F = (F & keep) | (f << sh);
+                CM |= cm << sh;
+            }
+            const uint32_t base = (uint32_t)q * PL::NP * P;
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                bst32<kCPnt>(rt, X[a], vo, base + a * P);
+                bst32<kCPnt>(rt, Y[a], vo, base + (PL::Y + a) * P);
+                bst32<kCPnt>(rt, H[a], vo, base + (PL::H + a) * P);
+                bst32<kCPnt>(rx, EX[a], vo, (uint32_t)(q * A + a) * P);
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                bst32<kCPnt>(rt, LO[j], vo, base + (PL::L + j) * P);
+                bst32<kCPnt>(rt, HI[j], vo, base + (PL::LH + j) * P);
+                bst32<kCPnt>(rt, M[j], vo, base + (PL::M + j) * P);
+            }
+            const u32x2 tv = {T[0], T[1]};
+            __builtin_amdgcn_raw_buffer_store_b64(tv, rt, (int)(g * 8u), (int)(base + PL::T * P), kCPnt);
+            bst32<kCPnt>(rt, F, vo, base + PL::F * P);
+            bst32<kCPnt>(rc, CM, vo, (uint32_t)q * P);
+#pragma unroll
+            for (int a = 0; a < A; ++a) wa[a] = nx[a];
+        }
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            bst32<kCPnt>(ro, X[a], vo, a * P);
+            bst32<kCPnt>(ro, Y[a], vo, (PL::Y + a) * P);
+            bst32<kCPnt>(ro, H[a], vo, (PL::H + a) * P);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            bst32<kCPnt>(ro, LO[j], vo, (PL::L + j) * P);
+            bst32<kCPnt>(ro, HI[j], vo, (PL::LH + j) * P);
+            bst32<kCPnt>(ro, M[j], vo, (PL::M + j) * P);
+        }
+        const u32x2 tv = {T[0], T[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(tv, ro, (int)(g * 8u), (int)(PL::T * P), kCPnt);
+        bst32<kCPnt>(ro, F, vo, PL::F * P);
     }
     if (stats != nullptr) {
         const uint32_t v[OC_NSTATS] = {wave_sum(st.eps), wave_sum(st.succ), wave_sum(st.steps), wave_sum(st.coll),
@@ -1142,9 +1261,12 @@ struct RenderArgs {
     int64_t pitch;
     uint8_t food_sprite[128];
 };
-// columns a render block lists (one lane per column): 32 for a narrow level, 64 for a wide one
-// (u16 item cells; its lists take twice the LDS, which only wide levels pay)
-constexpr int kRenderMaxW = 32, kRenderMaxWWide = 64, kRenderMaxDraw = 2 * OC_MAX_ITEMS + 3 * OC_MAX_AGENTS;
+// A render block lists the draws of its cell row (one lane per column, so a row of up to 255
+// columns: every width a level may have) in one compact list: a cell row holds every object at
+// most once, so it draws at most kRenderMaxDraw sprites (a plate and a food per item, an agent
+// and its held item's two), whatever its width.  Round 4's per-column lists (kRenderMaxDraw
+// entries for each of 32 or 64 columns) capped the width at 32 (narrow) / 64 (wide) columns.
+constexpr int kRenderMaxW = 255, kRenderMaxDraw = 2 * OC_MAX_ITEMS + 3 * OC_MAX_AGENTS;
 constexpr int kRenderPx = 16;  // pixels per lane and iteration: 48 output bytes, three 16-byte stores
 
 // SDL 1.2 per-pixel alpha blit of an RGBA source pixel onto an RGB destination pixel
@@ -1175,33 +1297,35 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
                                                            const uint32_t* __restrict__ bg,
                                                            uint8_t* __restrict__ out) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    constexpr int kCols = WIDE ? kRenderMaxWWide : kRenderMaxW;
-    __shared__ uint32_t dl_off[kCols][kRenderMaxDraw];
-    __shared__ uint32_t dl_geo[kCols][kRenderMaxDraw];  // size | offset << 16
-    __shared__ int32_t dl_n[kCols];
-    // per wave: its 1,024 pixels while it blends, then its 3 KB of packed output
+    __shared__ uint32_t dl_off[kRenderMaxDraw];
+    __shared__ uint32_t dl_geo[kRenderMaxDraw];    // size | offset << 16
+    __shared__ uint16_t col_start[kBlock + 1];     // column c's draws: [col_start[c], col_start[c + 1])
+    __shared__ uint32_t wave_tot[kBlock / 64];
     __shared__ u32x4 pix4[kBlock / 64][64 * kRenderPx / 4];
-    __shared__ uint32_t work[kBlock / 64][64];  // listed lane | row << 6 | cell column << 16 | x in cell << 22
+    __shared__ uint32_t work[kBlock / 64][64];  // listed lane | row << 6 | cell column << 16 | (x in cell) / 16 << 24
     const uint32_t part = blockIdx.x % (uint32_t)R.parts, strip = blockIdx.x / (uint32_t)R.parts;
     const int64_t e = strip / (uint32_t)R.H;
     const int ty = (int)(strip % (uint32_t)R.H);
     const int W = R.W, tile = R.tile;
     // planes: a wide level's item cells are u16, low bytes then high bytes, before the masks
     constexpr int kPX = 0, kPY = A, kPH = 2 * A, kPL = 3 * A, kPLH = 3 * A + K, kPM = 3 * A + (WIDE ? 2 : 1) * K;
-    if ((int)threadIdx.x < W) {
-        const int tx = threadIdx.x, cell = ty * W + tx;
-        const uint8_t* s = state + e;
-        const int64_t P = R.pitch;
+    // The cell row's draw list: every column lane counts its draws, a block prefix sum places
+    // them, and the lanes write them in the same order (draw order within a column).
+    const int tx = (int)threadIdx.x, cell = ty * W + tx;
+    const uint8_t* s = state + e;
+    const int64_t P = R.pitch;
+    auto column = [&](bool write, int n) -> int {  // this column's draws from slot n on; returns the end
         uint32_t held = 0u;
 #pragma unroll
         for (int a = 0; a < A; ++a) {
             const uint32_t h = s[(kPH + a) * P];
             if (h < (uint32_t)K) held |= 1u << h;
         }
-        int n = 0;
         auto push = [&](int32_t off, int cls) {
-            dl_off[tx][n] = (uint32_t)off;
-            dl_geo[tx][n] = (uint32_t)R.size[cls] | ((uint32_t)R.offset[cls] << 16);
+            if (write) {
+                dl_off[n] = (uint32_t)off;
+                dl_geo[n] = (uint32_t)R.size[cls] | ((uint32_t)R.offset[cls] << 16);
+            }
             ++n;
         };
         // an item: a plate first, its contents at the container class; else the food itself
@@ -1249,8 +1373,23 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
             const uint32_t h = s[(kPH + a) * P];
             if (h < (uint32_t)K) push_item(s[(kPM + h) * P], 2, 3, 1);
         }
-        dl_n[tx] = n;
+        return n;
+    };
+    const int cnt = tx < W ? column(false, 0) : 0;
+    int incl = cnt;  // inclusive scan over the wave, then over the block's waves
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if ((tx & 63) >= off) incl += o;
     }
+    if ((tx & 63) == 63) wave_tot[tx >> 6] = (uint32_t)incl;
+    __syncthreads();
+    int before = 0;
+    for (int w = 0; w < (tx >> 6); ++w) before += (int)wave_tot[w];
+    const int start = before + incl - cnt;
+    col_start[tx] = (uint16_t)start;
+    if (tx == kBlock - 1) col_start[kBlock] = (uint16_t)(start + cnt);
+    if (tx < W) column(true, start);
     __syncthreads();
     const int row_px = W * tile, G = row_px / kRenderPx;  // 16-pixel groups per image row
     // this block's share of the strip's 16-pixel groups: whole waves of them
@@ -1289,9 +1428,9 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
                 p[4 * q + 2] = v.z;
                 p[4 * q + 3] = v.w;
             }
-            const int n = dl_n[tx];
-            for (int d = 0; d < n; ++d) {
-                const uint32_t geo = dl_geo[tx][d];
+            const int d1 = col_start[tx + 1];
+            for (int d = col_start[tx]; d < d1; ++d) {
+                const uint32_t geo = dl_geo[d];
                 const int sz = (int)(geo & 0xFFFFu), o = (int)(geo >> 16);
                 need |= (unsigned)(r - o) < (unsigned)sz && lx0 + kRenderPx > o && lx0 < o + sz;
             }
@@ -1304,22 +1443,22 @@ __global__ __launch_bounds__(kBlock) void oc_render_kernel(RenderArgs R, const u
                     pix4[wave][4 * lane + q] = u32x4{p[4 * q], p[4 * q + 1], p[4 * q + 2], p[4 * q + 3]};
                 const uint32_t slot =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                work[wave][slot] = (uint32_t)lane | ((uint32_t)r << 6) | ((uint32_t)tx << 16) | ((uint32_t)lx0 << 22);
+                work[wave][slot] = (uint32_t)lane | ((uint32_t)r << 6) | ((uint32_t)tx << 16) | ((uint32_t)(lx0 >> 4) << 24);
             }
             __builtin_amdgcn_wave_barrier();  // LDS is in order within a wave; keep the compiler from moving reads up
             const int npx = kRenderPx * __popcll(mask);
             for (int t = lane; t < npx; t += 64) {
                 const uint32_t ent = work[wave][t >> 4];
                 const int k = t & (kRenderPx - 1), gl = (int)(ent & 63u);
-                const int rr = (int)((ent >> 6) & 0x3FFu), ctx = (int)((ent >> 16) & 63u), lx = (int)(ent >> 22) + k;
+                const int rr = (int)((ent >> 6) & 0x3FFu), ctx = (int)((ent >> 16) & 0xFFu), lx = (int)(ent >> 24) * 16 + k;
                 uint32_t dpx = pix[kRenderPx * gl + k];
-                const int n = dl_n[ctx];
-                for (int d = 0; d < n; ++d) {
-                    const uint32_t geo = dl_geo[ctx][d];
+                const int d1 = col_start[ctx + 1];
+                for (int d = col_start[ctx]; d < d1; ++d) {
+                    const uint32_t geo = dl_geo[d];
                     const int sz = (int)(geo & 0xFFFFu), o = (int)(geo >> 16);
                     const int dy = rr - o, dx = lx - o;
                     if ((unsigned)dy < (unsigned)sz && (unsigned)dx < (unsigned)sz)
-                        dpx = sdl_blend(dpx, atlas[dl_off[ctx][d] + dy * sz + dx]);
+                        dpx = sdl_blend(dpx, atlas[dl_off[d] + dy * sz + dx]);
                 }
                 pix[kRenderPx * gl + k] = dpx;
             }
@@ -1834,17 +1973,24 @@ int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, i
                     int64_t dist_len) {
     if (h == nullptr || num_nodes == nullptr) return fail(OC_EINVAL, "bad argument");
     ErrScope es_(h);
-    if (h->roll.nnodes < 0)
-        return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (%d on a level of more than 255 cells) or a distance of 254", ocro::kMaxNodes, ocro::kMaxNodesWide);
+    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "no reachability graph for this level");
     const int n = h->roll.nnodes, cells = h->level.width * h->level.height;
     *num_nodes = n;
     if (node_of != nullptr) {
         if (node_of_len < (int64_t)cells * 5) return fail(OC_EINVAL, "node_of needs %d entries", cells * 5);
-        memcpy(node_of, h->roll_blob_host.data() + h->roll.node_off, (size_t)cells * 5 * sizeof(uint16_t));
+        const uint32_t* hd = (const uint32_t*)(h->roll_blob_host.data() + h->roll.node_off);
+        for (int i = 0; i < cells * 5; ++i) node_of[i] = (uint16_t)(hd[i] & 0xFFFFu);  // kNoHandle -> 0xFFFF
     }
     if (dist != nullptr) {
-        if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %d bytes", n * n);
-        memcpy(dist, h->roll_blob_host.data() + h->roll.dist_off, (size_t)n * n);
+        if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %lld bytes", (long long)n * n);
+        if (h->roll.max_dist > 254)
+            return fail(OC_ELEVEL, "a node distance of %d does not fit the u8 table (the planner entry points take it)",
+                        h->roll.max_dist);
+        // the node table the Floor distances define (oc_rollout.h), built for the export
+        ocro::RollLevel L2;
+        std::vector<uint8_t> blob2, dist_v;
+        ocro::build_roll_level(L2, blob2, h->level.width, h->level.height, h->level.tiles, h->level.encoding, &dist_v);
+        memcpy(dist, dist_v.data(), (size_t)n * n);
     }
     return OC_OK;
 }
@@ -1972,15 +2118,36 @@ static int step_wide(const oc_handle* h, const void* sin, void* sout, const uint
     R.tile_words = (h->level.width * h->level.height + 3) / 4;
     R.pitch = pitch_for(B);
     R.B = B;
-    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
+    // one lane per 4 envs; up to 8 blocks per CU (grid-stride past that)
+    const int64_t need = ((B + kEPL - 1) / kEPL + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
     const dim3 grid((unsigned)(need < cap ? need : cap));
     const uint32_t rows = (uint32_t)stats_rows(h, B);
     hipStream_t st = (hipStream_t)stream;
+    // launches of at most `per` steps, so a launch's buffer offsets (trajectory, actions) stay
+    // < 2 GiB; each starts from the previous one's final state (as oc_step_n's narrow path)
+    const int64_t NP = 3 * h->A + 3 * h->K + 3, P = R.pitch;
+    if (NP * P >= (1ll << 31)) return fail(OC_EINVAL, "batch too large for one launch (state must be < 2 GiB)");
+    int64_t per = ((1ll << 31) - 1) / (NP * P);
+    if (per > 4096) per = 4096;
+    per = (n + (n + per - 1) / per - 1) / ((n + per - 1) / per);  // equal launches
+    const uint8_t* last_slot = traj ? (const uint8_t*)traj + (int64_t)(n - 1) * NP * P : nullptr;
+    const bool out_is_last = traj != nullptr && (const uint8_t*)sout == last_slot;
+    const uint8_t* src = (const uint8_t*)sin;
+    for (int64_t r0 = 0; r0 < n; r0 += per) {
+        const int m = (int)(n - r0 < per ? n - r0 : per);
+        const bool last = r0 + m >= n;
+        uint8_t* tr = traj ? (uint8_t*)traj + r0 * NP * P : nullptr;
+        uint8_t* so = (traj != nullptr && !last) || (out_is_last && last) ? nullptr : (uint8_t*)sout;
+        uint8_t* e_ = ex ? ex + r0 * h->A * P : nullptr;
+        uint8_t* c_ = coll ? coll + r0 * P : nullptr;
+        const uint8_t* a_ = act + r0 * h->A * P;
 #define OC_LAUNCH_WSTEP(A, K)                                                                                  \
-    hipLaunchKernelGGL((oc_step_wide_kernel<A, K>), grid, dim3(kBlock), 0, st, R, h->wide_tiles,                 \
-                       (const uint8_t*)sin, (uint8_t*)sout, act, (uint8_t*)traj, ex, coll, stats, rows, n)
-    OC_DISPATCH(h->A, h->K, OC_LAUNCH_WSTEP)
-    if (const int rc = hip_check("oc_step (wide) launch")) return rc;
+    hipLaunchKernelGGL((oc_step_wide_kernel<A, K>), grid, dim3(kBlock), 0, st, R, h->wide_tiles, src, so, a_,  \
+                       tr, e_, c_, stats, rows, m)
+        OC_DISPATCH(h->A, h->K, OC_LAUNCH_WSTEP)
+        if (const int rc = hip_check("oc_step (wide) launch")) return rc;
+        src = traj != nullptr ? tr + (int64_t)(m - 1) * NP * P : (const uint8_t*)sout;
+    }
     return totals != nullptr ? oc_stats_reduce(h, stats, B, totals, stream) : OC_OK;
 }
 
@@ -2172,7 +2339,7 @@ static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num
         if (subtasks[i].level != OC_LEVEL0 && !level1_ok)
             return fail(OC_EINVAL, "subtask %d: only oc_rollout takes OC_LEVEL1", i);
     if (num_subtasks < 1 || num_subtasks > OC_MAX_SUBTASKS) return fail(OC_EINVAL, "num_subtasks %d", num_subtasks);
-    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (%d on a level of more than 255 cells) or a distance of 254", ocro::kMaxNodes, ocro::kMaxNodesWide);
+    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "no reachability graph for this level");
     if (h->roll_blob == nullptr) return fail(OC_EHIP, "rollout tables not on the device");
     R.L = h->roll;
     R.nsub = num_subtasks;
@@ -2334,8 +2501,7 @@ int oc_render_ordered(const oc_handle* h, const void* state, const uint8_t* draw
     ErrScope es_(h);
     OC_NEED_DEVICE(h);
     const int W = h->level.width, H = h->level.height;
-    const int max_w = h->wide ? kRenderMaxWWide : kRenderMaxW;
-    if (W > max_w) return fail(OC_ELEVEL, "render: width %d > %d", W, max_w);
+    if (W > kRenderMaxW) return fail(OC_ELEVEL, "render: width %d > %d", W, kRenderMaxW);  // oc_create caps it at 255
     if (desc->tile < kRenderPx || desc->tile % kRenderPx != 0 || desc->tile > 1024)
         return fail(OC_EINVAL, "render: tile %d (a multiple of %d)", desc->tile, kRenderPx);
     for (int c = 0; c < OC_RENDER_SIZES; ++c)

@@ -223,9 +223,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 
 
 class LevelError(RuntimeError):
-    """OC_ELEVEL: the level is outside an entry point's envelope (e.g. for the planner entry
-    points a reachability graph of more than 390 nodes on a level of at most 255 cells, whose
-    distance table the kernels keep in LDS; a wide level's graph may have up to 5,120)."""
+    """OC_ELEVEL: the level is outside an entry point's envelope (oc_create's validation: more
+    than 1,024 cells, a 17th object or a 4th of one food; oc_reachability's export: a node
+    distance of 255 or more)."""
 
 
 def check(rc: int) -> None:

@@ -44,10 +44,16 @@ ROLL_CONFIGS = [("widegraph-24x24_salad", 2, 1, 9200)]
 
 
 def main():
+    generate(LEVELS, BOUND_CONFIGS, ROLL_CONFIGS, "widegraph", pair_seed=605, gid0=12700)
+
+
+def generate(LEVELS, BOUND_CONFIGS, ROLL_CONFIGS, prefix, pair_seed, gid0):
+    """Record <prefix>.json (tables, graph size, 400 reference BFS distances), <prefix>.npz
+    (episodes), bounds_<prefix>.npz and rollout_<prefix>.npz for the kitchens LEVELS."""
     ref = gg.load_reference()
     gg.MAXK = 8
     gr.canon = gd.canon_k
-    scratch = tempfile.mkdtemp(prefix="oc_widegraph_")
+    scratch = tempfile.mkdtemp(prefix="oc_%s_" % prefix)
     os.makedirs(os.path.join(scratch, "utils", "levels"))
     for name in LEVELS:
         shutil.copy(os.path.join(HERE, "levels", name + ".txt"), os.path.join(scratch, "utils", "levels"))
@@ -58,7 +64,7 @@ def main():
     _, nav_utils, _ = ref
 
     info = {name: gd.level_info(gg.RefEnv(ref, name, 4, 100), nav_utils) for name in LEVELS}
-    rng = random.Random(605)
+    rng = random.Random(pair_seed)
     for name in LEVELS:
         env = gg.RefEnv(ref, name, 4, 100)
         g = env.env.world.reachability_graph
@@ -74,12 +80,12 @@ def main():
             # a node is ((x, y), (dx, dy)): the square and the side it is approached from
             pairs.append([list(u[0]), list(u[1]), list(v[0]), list(v[1]), d])
         info[name]["dist_pairs"] = pairs
-    with open(os.path.join(HERE, "widegraph.json"), "w") as f:
+    with open(os.path.join(HERE, prefix + ".json"), "w") as f:
         json.dump(info, f, indent=1, sort_keys=True, default=int)
 
     gg.LEVEL_NAMES = list(LEVELS)
     rec = gg.Recorder()
-    gid = 12700
+    gid = gid0
     for name in LEVELS:
         for A in (2, 3, 4):
             seed, g_ = 4800, gid
@@ -91,7 +97,7 @@ def main():
             gid += 1
             print("episodes A=%d done" % A, flush=True)
     gg.LEVEL_NAMES = ["levels/%s.txt" % n for n in LEVELS]
-    rec.save(os.path.join(HERE, "widegraph.npz"), ["uniform", "goal"])
+    rec.save(os.path.join(HERE, prefix + ".npz"), ["uniform", "goal"])
     fl = np.array(rec.S["flags"])
     print("wrote %d episodes / %d steps; done-success %d, err %d" % (
         len(rec.eps), len(rec.act), int(((fl & 3) == 3).sum()), int(((fl & 4) != 0).sum())))
@@ -102,7 +108,7 @@ def main():
         with contextlib.redirect_stdout(io.StringIO()):
             gb.record_state(rows, nav_utils, BayesianDelegator, env.env, A, si)
     states = gw.goal_states(ref, info, BOUND_CONFIGS, 15, 120, visit_bounds)
-    out = gd.save_states(os.path.join(HERE, "bounds_widegraph.npz"), BOUND_CONFIGS, states, rows)
+    out = gd.save_states(os.path.join(HERE, "bounds_" + prefix + ".npz"), BOUND_CONFIGS, states, rows)
     print("wrote %d bound rows over %d states" % (len(out["lb"]), len(states)))
 
     rrows = {k: [] for k in ("cfg", "state", "kind", "agents", "start", "goal_mask", "goal_count",
@@ -113,7 +119,7 @@ def main():
     states = gw.goal_states(ref, info, ROLL_CONFIGS, 20, 120, visit_roll)
     width = 12 + 4 * gg.MAXK
     rrows["next"] = [np.concatenate([n, np.full(width - len(n), gg.PAD, np.uint8)]) for n in rrows["next"]]
-    out = gd.save_states(os.path.join(HERE, "rollout_widegraph.npz"), ROLL_CONFIGS, states, rrows)
+    out = gd.save_states(os.path.join(HERE, "rollout_" + prefix + ".npz"), ROLL_CONFIGS, states, rrows)
     print("wrote %d rollout rows over %d states; legal %d, goal %d" % (
         len(out["lb"]), len(states), int(out["legal"].sum()), int(out["goal"].sum())))
     shutil.rmtree(scratch)

@@ -319,21 +319,25 @@ def test_render_kernel_matches_reference_pixels():
             assert gif_frame_ok(ref, name, f, imgs[f]), (name, f)
 
 
-def _wide_kitchen(width):
-    """A 5-row Salad kitchen `width` columns wide (a user level, levels.parse_level_text)."""
-    rows = ["-" * (width - 4) + "tlp-", "/" + " " * (width - 2) + "-", "*" + " " * (width - 2) + "p",
-            "-" + " " * (width - 2) + "-", "-" * width]
-    return levels.parse_level_text("\n".join(rows) + "\n\nSalad\n\n1 1\n%d 3\n3 2\n" % (width - 3), "wide-%d" % width)
+def _wide_kitchen(width, rows_=5):
+    """A Salad kitchen `width` columns wide and `rows_` (4 or 5) rows high (a user level,
+    levels.parse_level_text)."""
+    rows = ["-" * (width - 4) + "tlp-", "/" + " " * (width - 2) + "-", "*" + " " * (width - 2) + "p"]
+    rows += ["-" + " " * (width - 2) + "-"] * (rows_ - 4) + ["-" * width]
+    return levels.parse_level_text("\n".join(rows) + "\n\nSalad\n\n1 1\n%d 2\n3 2\n" % (width - 3), "wide-%d" % width)
 
 
 @pytest.mark.gpu
-def test_render_widest_level_matches_oracle():
-    """32 columns, the kernel's widest level (2,560-px rows: 160 pixel groups of 16 per row, so a
-    wave's 1,024 pixels sit inside one image row), 3 agents after random play; 33 columns is
-    refused with OC_ELEVEL while stepping it works."""
+@pytest.mark.parametrize("width", [32, 33, 51])
+def test_render_wide_narrow_levels_match_oracle(width):
+    """Narrow levels (at most 255 cells) of 32 columns and past it, up to 51 (5 x 51 = 255
+    cells), 3 agents after random play, against the numpy restatement of the reference's blits.
+    Round 4's kernel listed 32 columns per block and refused wider narrow levels; the compact
+    per-row draw list takes any width (round 5)."""
     import torch
     from gym_cooking_amd.engine import OvercookedBatch
-    lv = _wide_kitchen(32)
+    lv = _wide_kitchen(width)
+    assert not capi.is_wide(lv)
     eb = OvercookedBatch(lv, 3, 40, max_T=100)
     s, s2 = eb.new_state(), eb.new_state()
     eb.reset(s)
@@ -344,12 +348,7 @@ def test_render_widest_level_matches_oracle():
         s, s2 = s2, s
     rd = render.Renderer(eb)
     img = rd.render(s, channels="rgb").cpu().numpy()
-    assert img.shape[1:] == (5 * 80, 32 * 80, 3)
+    assert img.shape[1:] == (5 * 80, width * 80, 3)
     ev = tl.env_view(s.cpu().numpy(), 3, eb.K, eb.pitch, eb.B)
     for b in range(eb.B):
         assert np.array_equal(img[b], render_oracle.render_env(lv, ev[:, b], 3, eb.K, channels="rgb")), b
-    wide = OvercookedBatch(_wide_kitchen(33), 2, 8, max_T=100)
-    s = wide.new_state()
-    wide.reset(s)
-    with pytest.raises(capi.LevelError, match="width"):
-        render.Renderer(wide).render(s)

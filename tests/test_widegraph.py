@@ -1,7 +1,11 @@
-"""A kitchen whose reachability graph has more than the 390 nodes a narrow level's planner
-tables hold in LDS: widegraph-24x24_salad, 576 cells and 605 nodes, whose
-planner kernels read the distance table from device memory (oc_rollout.h, RollLevel.lds_bytes).
-Pinned on the CPU to the reference's own runs of the level file (tests/golden/gen_widegraph.py):
+"""Kitchens whose reachability graph has more than 390 nodes, the limit the
+round-4 engine had on a narrow level (its all-pairs node distances in LDS):
+  * widegraph-24x24_salad: 576 cells (wide: u16 cell ids), a 605-node graph;
+  * dense-15x17_salad: 255 cells (narrow: byte cell ids), a 417-node graph (round 5).
+Since round 5 the planner tables keep only the distances between Floor squares (oc_rollout.h:
+an approach node is a leaf one edge from its Floor), in LDS on a narrow level and in device
+memory on a wide one.  Pinned on the CPU to the reference's own runs of the level files
+(tests/golden/gen_widegraph.py, gen_densegraph.py):
 
 * the parser and the engine's graph (node count, and the BFS distance of 400 random node pairs
   against the reference's nx.shortest_path_length);
@@ -24,19 +28,22 @@ from gym_cooking_amd import capi, levels, recipes
 from oracle import oracle
 
 NAME = "widegraph-24x24_salad"
+# kitchen -> (fixture prefix, wide layout)
+KITCHENS = {"widegraph-24x24_salad": ("widegraph", True), "dense-15x17_salad": ("densegraph", False)}
 
 
-def _info():
-    with open(os.path.join(tl.GOLDEN, "widegraph.json")) as f:
-        return json.load(f)[NAME]
+def _info(name=NAME):
+    with open(os.path.join(tl.GOLDEN, KITCHENS[name][0] + ".json")) as f:
+        return json.load(f)[name]
 
 
 def _graph(lv):
-    """The engine's graph (oc_reachability): node count, node_of [cells * 5], dist [n * n]."""
+    """The engine's graph (oc_reachability, a host-only handle): node count, node_of
+    [cells * 5], dist [n * n]."""
     lib = capi.load_library()
     d = capi.level_desc(lv, 2)
     h = ctypes.c_void_p()
-    capi.check(lib.oc_create(ctypes.byref(d), 2, 100, 0, ctypes.byref(h)))
+    capi.check(lib.oc_create(ctypes.byref(d), 2, 100, capi.OC_DEVICE_HOST, ctypes.byref(h)))
     try:
         n = ctypes.c_int32()
         capi.check(lib.oc_reachability(h, ctypes.byref(n), None, 0, None, 0))
@@ -52,10 +59,18 @@ def _graph(lv):
 _NAV = {(0, 1): 0, (0, -1): 1, (-1, 0): 2, (1, 0): 3, (0, 0): 4}  # World.NAV_ACTIONS order + (0, 0)
 
 
-def test_widegraph_level_matches_reference_graph():
-    ref = _info()
-    lv = levels.load_level(tw._path(NAME))
-    assert (lv.width, lv.height) == (ref["width"], ref["height"]) and capi.is_wide(lv)
+KIT = pytest.mark.parametrize("name", sorted(KITCHENS))
+
+
+def _fx(name, kind=""):
+    return tl.load_fixture(kind + KITCHENS[name][0] + ".npz")
+
+
+@KIT
+def test_widegraph_level_matches_reference_graph(name):
+    ref = _info(name)
+    lv = levels.load_level(tw._path(name))
+    assert (lv.width, lv.height) == (ref["width"], ref["height"]) and capi.is_wide(lv) == KITCHENS[name][1]
     assert lv.tiles == ref["tiles"]
     assert sorted(str(s) for s in recipes.all_subtasks(lv)) == sorted(ref["all_subtasks"])
     n, node_of, dist = _graph(lv)
@@ -71,9 +86,10 @@ def test_widegraph_level_matches_reference_graph():
     assert checked == 400
 
 
+@KIT
 @pytest.mark.parametrize("impl", ["oracle", "cpu_step"])
-def test_widegraph_episodes_match_reference(impl):
-    fx = tl.load_fixture("widegraph.npz")
+def test_widegraph_episodes_match_reference(name, impl):
+    fx = _fx(name)
     groups = tl.episode_groups(fx)
     assert sum(g.B for g in groups) == len(fx["ep_T"]) >= 6
     for g in groups:
@@ -91,9 +107,10 @@ def test_widegraph_episodes_match_reference(impl):
         assert not errs, "%s A=%d: %s" % (g.level.name, g.A, "\n".join(errs[:10]))
 
 
+@KIT
 @pytest.mark.parametrize("impl", ["oracle", "host"])
-def test_widegraph_bounds_match_reference_rows(impl):
-    rows = tl.BoundRows(tl.load_fixture("bounds_widegraph.npz"), 0)
+def test_widegraph_bounds_match_reference_rows(name, impl):
+    rows = tl.BoundRows(_fx(name, "bounds_"), 0)
     assert rows.B > 0
     ob = oracle.OracleBatch(rows.level, rows.A, 100, rows.B)
     st = rows.state(ob.pitch)
@@ -104,9 +121,10 @@ def test_widegraph_bounds_match_reference_rows(impl):
         assert not errs, "\n".join(errs[:20])
 
 
+@KIT
 @pytest.mark.parametrize("impl", ["oracle", "host"])
-def test_widegraph_rollout_matches_reference_rows(impl):
-    fx = tl.load_fixture("rollout_widegraph.npz")
+def test_widegraph_rollout_matches_reference_rows(name, impl):
+    fx = _fx(name, "rollout_")
     n = 0
     for rows in tl.RolloutRows(fx, 0).split(capi.MAX_SUBTASKS):
         ob = oracle.OracleBatch(rows.level, rows.A, 100, rows.B)
@@ -124,10 +142,11 @@ def test_widegraph_rollout_matches_reference_rows(impl):
     assert n == len(fx["cfg"]) > 0
 
 
+@KIT
 @pytest.mark.parametrize("A", [2, 4])
-def test_widegraph_host_rows_match_oracle_random(A):
+def test_widegraph_host_rows_match_oracle_random(name, A):
     B = 1200
-    ob, s, acts, subs, alloc = th.random_rollout_case(tw._path(NAME), A, B, seed=B + 7 * A, planner_levels=(0, 1))
+    ob, s, acts, subs, alloc = th.random_rollout_case(tw._path(name), A, B, seed=B + 7 * A, planner_levels=(0, 1))
     o_out = ob.new_state()
     o_fl, o_lb = ob.rollout(s, o_out, acts, subs, alloc)
     h_out, h_fl, h_lb = th.host_rollout(ob, s, acts, subs, alloc)

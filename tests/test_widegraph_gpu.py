@@ -1,8 +1,10 @@
-"""The 605-node kitchen (tests/test_widegraph.py) on the GPU, through the C-ABI: its planner
-kernels stage the level's tables in LDS and read the distance table from device memory.
-oc_step replays the reference's episodes; oc_subtask_bounds and oc_rollout against the
-reference's rows; rollout, bounds and likelihood rows against the oracle on random states; the
-navigation planner over oc_rollout decides as the same search over the oracle's rows."""
+"""The kitchens of tests/test_widegraph.py (more than 390 graph nodes: the 605-node wide
+kitchen and the 417-node narrow one) on the GPU, through the C-ABI: their planner kernels
+stage the level's tables in LDS and read the Floor distance table from LDS (narrow) or device
+memory (wide).  oc_step replays the reference's episodes; oc_subtask_bounds and oc_rollout
+against the reference's rows; rollout, bounds and likelihood rows against the oracle on random
+states; the navigation planner over oc_rollout decides as the same search over the oracle's
+rows."""
 import numpy as np
 import pytest
 
@@ -19,9 +21,13 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
-def test_engine_replays_widegraph_episodes():
+KIT = twg.KIT
+
+
+@KIT
+def test_engine_replays_widegraph_episodes(name):
     import test_gpu_parity as tg
-    fx = tl.load_fixture("widegraph.npz")
+    fx = twg._fx(name)
     n = 0
     for g in tl.episode_groups(fx):
         eb = twgpu._batch(g.level, g.A, g.B, g.max_T)
@@ -35,8 +41,9 @@ def test_engine_replays_widegraph_episodes():
     assert n == len(fx["ep_T"])
 
 
-def test_widegraph_bounds_match_reference_rows():
-    rows = tl.BoundRows(tl.load_fixture("bounds_widegraph.npz"), 0)
+@KIT
+def test_widegraph_bounds_match_reference_rows(name):
+    rows = tl.BoundRows(twg._fx(name, "bounds_"), 0)
     P = capi.pitch_for(rows.B)
     s = rows.state(P)
     eb = twgpu._batch(rows.level, rows.A, rows.B)
@@ -47,8 +54,9 @@ def test_widegraph_bounds_match_reference_rows():
         assert not errs, "\n".join(errs[:20])
 
 
-def test_widegraph_rollout_matches_reference_rows():
-    fx = tl.load_fixture("rollout_widegraph.npz")
+@KIT
+def test_widegraph_rollout_matches_reference_rows(name):
+    fx = twg._fx(name, "rollout_")
     n = 0
     for rows in tl.RolloutRows(fx, 0).split(capi.MAX_SUBTASKS):
         P = capi.pitch_for(rows.B)
@@ -65,10 +73,11 @@ def test_widegraph_rollout_matches_reference_rows():
     assert n == len(fx["cfg"])
 
 
+@KIT
 @pytest.mark.parametrize("A", [2, 4])
-def test_widegraph_rows_match_oracle_random(A):
+def test_widegraph_rows_match_oracle_random(name, A):
     B = 6000
-    ob, s, acts, subs, alloc = th.random_rollout_case(tw._path(twg.NAME), A, B, seed=B + A, planner_levels=(0, 1))
+    ob, s, acts, subs, alloc = th.random_rollout_case(tw._path(name), A, B, seed=B + A, planner_levels=(0, 1))
     eb = twgpu._batch(ob.level, A, B)
     o_out = ob.new_state()
     o_fl, o_lb = ob.rollout(s, o_out, acts, subs, alloc, nthreads=16)
@@ -94,15 +103,16 @@ def test_widegraph_rows_match_oracle_random(A):
     np.testing.assert_allclose(g_v[ok], o_v[ok], rtol=1e-12)
 
 
+@KIT
 @pytest.mark.parametrize("A,sub,agents", [(2, ("Chop", "Tomato"), ("agent-1",)),
                                           (3, ("Chop", "Lettuce"), ("agent-1", "agent-3"))])
-def test_widegraph_planner_matches_host_search(A, sub, agents):
+def test_widegraph_planner_matches_host_search(name, A, sub, agents):
     """get_next_action over oc_rollout equals the same search over the CPU oracle's rows
     (which test_widegraph.py pins to the reference's rows on this kitchen)."""
     import test_planner_host as tp
     from gym_cooking_amd import recipes
     from gym_cooking_amd.planner import E2E_BRTDP, PlanEnv
-    lv = levels.load_level(tw._path(twg.NAME))
+    lv = levels.load_level(tw._path(name))
     ob = oracle.OracleBatch(lv, A, 0, 1)
     s, s2 = ob.new_state(), ob.new_state()
     ob.reset(s)

@@ -185,17 +185,22 @@ def test_shim_replays_wide_level_episodes():
 
 
 @pytest.mark.parametrize("name,A", [("wide-17x17_salad", 4), ("wide-23x13_tl", 3), ("widegraph-24x24_salad", 2),
-                                    ("wide64", 3)])
+                                    ("wide64", 3), ("wide65", 2), ("wide255", 2)])
 def test_wide_level_render_matches_oracle(name, A):
-    """oc_render on levels of more than 255 cells (u16 item cells; up to 64 columns) against the
-    numpy restatement of the reference's blits (oracle/render_oracle.py, pinned to the
-    reference's own screenshots and GIF frames in tests/test_render.py), after random play;
-    65 columns are refused with OC_ELEVEL while stepping works."""
+    """oc_render on levels of more than 255 cells (u16 item cells) against the numpy
+    restatement of the reference's blits (oracle/render_oracle.py, pinned to the reference's
+    own screenshots and GIF frames in tests/test_render.py), after random play; up to 255
+    columns, the widest grid a level may have (255 x 4 = 1,020 cells), since round 5's compact
+    per-row draw list (round 4 refused past 64 columns)."""
     import test_render as tr
     from gym_cooking_amd.render import Renderer
-    lv = tr._wide_kitchen(64) if name == "wide64" else levels.load_level(tw._path(name))
+    if name.startswith("wide") and name[4:].isdigit():
+        w = int(name[4:])
+        lv = tr._wide_kitchen(w, 4 if w * 5 > capi.OC_MAX_CELLS else 5)
+    else:
+        lv = levels.load_level(tw._path(name))
     assert capi.is_wide(lv)
-    eb = _batch(lv, A, 24)
+    eb = _batch(lv, A, 6 if lv.width > 100 else 24)
     s, s2 = eb.new_state(), eb.new_state()
     eb.reset(s)
     a = eb.new_actions()
@@ -209,10 +214,6 @@ def test_wide_level_render_matches_oracle(name, A):
     from oracle import render_oracle
     for b in range(eb.B):
         assert np.array_equal(img[b], render_oracle.render_env(lv, ev[:, b], A, eb.K, channels="rgb")), b
-    if name == "wide64":
-        wider = _batch(tr._wide_kitchen(65), 2, 8)
-        with pytest.raises(capi.LevelError, match="width"):
-            Renderer(wider).render(wider.reset(wider.new_state()))
 
 
 @pytest.mark.parametrize("name,A,sub,agents", [("wide-17x17_salad", 2, ("Chop", "Tomato"), ("agent-1",)),
