@@ -553,8 +553,8 @@ struct RollArgs {
     ocro::RollLevel L;
     ocro::Sub subs[OC_MAX_SUBTASKS];
     int32_t nsub;
-    int32_t blob_words;  // roll.lds_bytes / 4: the whole blob on a narrow level, the tables up to
-                         // dist_off on a wide one (its distances are read from device memory)
+    int32_t blob_words;  // roll.lds_bytes / 4: the whole blob, or (dist_global: a wide level, a narrow
+                         // one past kMaxNodes) the tables up to dist_off (distances in device memory)
     int64_t pitch, B;
 };
 
@@ -616,7 +616,7 @@ __device__ __forceinline__ void store_row(uint8_t* __restrict__ sout, int64_t P,
     }
 }
 
-template <int A, int K, bool W>
+template <int A, int K, bool W, bool GD>
 __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                             uint8_t* __restrict__ sout,
                                                             const uint8_t* __restrict__ act,
@@ -626,49 +626,26 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
                                                             float* __restrict__ lb) {
     extern __shared__ uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
-    const int64_t P = R.pitch;
-    using PL = Planes<A, K, W>;
-    // a row's inputs: its state, t, flags, alloc id and every agent's action (the subtask's
-    // agents are known only after the configuration is read from LDS)
-    struct In {
-        ocro::RowT<K, W> r;
-        uint32_t t, fl, ai, aw;
-    };
-    auto load = [&](int64_t e) {
-        In d;
-        d.r = load_row<A, K, W>(sin, P, e);
-        d.t = ((const uint16_t*)(sin + PL::T * P))[e];
-        d.fl = sin[PL::F * P + e];
-        d.ai = alloc != nullptr ? alloc[e] : 0u;
-        d.aw = 0u;
-#pragma unroll
-        for (int a = 0; a < A; ++a) d.aw |= (uint32_t)act[a * P + e] << (8 * a);
-        return d;
-    };
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x;
-    // the first row's loads go out before the tables are staged: their latencies overlap
-    // (tools/rolltl.hip, round 5)
-    In d;
-    if (e < R.B) d = load(e);
     stage_roll_tables(R, blob_g, blob_w, subs);
     const uint8_t* blob = (const uint8_t*)blob_w;
-    for (; e < R.B; e += stride) {
-        ocro::RowT<K, W> r = d.r;
+    const int64_t P = R.pitch;
+    using PL = Planes<A, K, W>;
+    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
+        ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
+        const uint16_t t = ((const uint16_t*)(sin + PL::T * P))[e];
+        const uint8_t fl_in = sin[PL::F * P + e];
+        const int ai = alloc != nullptr ? alloc[e] : 0;
         float bound = 0.0f;
         int f = OC_ROLL_BADALLOC;  // an alloc id past num_subtasks: the row is copied unchanged
-        if ((int)d.ai < R.nsub) {
-            const ocro::Sub& s = subs[d.ai];
-            const int c0 = (int)((d.aw >> (8 * s.agent[0])) & 0xFFu);
-            const int c1 = s.n == 2 ? (int)((d.aw >> (8 * s.agent[1])) & 0xFFu) : ocro::kNoop;
-            ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+        if (ai < R.nsub) {
+            const ocro::Sub& s = subs[ai];
+            const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
+            ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             f = ops.run(r, s, c0, c1, bound);
         }
-        const uint32_t t = d.t, fl_in = d.fl;
-        if (e + stride < R.B) d = load(e + stride);
         store_row<A, K, W>(sout, P, e, r);
-        ((uint16_t*)(sout + PL::T * P))[e] = (uint16_t)t;
-        sout[PL::F * P + e] = (uint8_t)fl_in;
+        ((uint16_t*)(sout + PL::T * P))[e] = t;
+        sout[PL::F * P + e] = fl_in;
         out_flags[e] = (uint8_t)f;
         lb[e] = bound;
     }
@@ -691,7 +668,7 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
 // 0.35 ms configuration-major, 0.55 ms random order, against 0.44 / 1.29 ms with G = 8; a
 // one-agent table 0.19 ms with G = 8, 0.41 with G = 32.  The None subtask's closed form runs
 // on the group's first lane.
-template <int A, int K, int G, bool W>
+template <int A, int K, int G, bool W, bool GD>
 __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                                const uint8_t* __restrict__ taken_p,
                                                                const uint8_t* __restrict__ alloc,
@@ -716,7 +693,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
             uint32_t taken = 0;
 #pragma unroll
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
-            ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+            ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             if (s.kind == 0) {
                 f = 0;
                 if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
@@ -847,7 +824,7 @@ constexpr int kLikCompactLds = 9 * 1024 * OC_LIK_ROUND_SCALE;
 //      rollout (q_value), Q(s, k) and its raise bit into the row's LDS slots;
 //   3. each group reads its row's Q values back and takes the softmax as above (the same max,
 //      exp and ascending sum, so the outputs are bit-identical to the grouped form).
-template <int A, int K, int G, bool W>
+template <int A, int K, int G, bool W, bool GD>
 __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                                        const uint8_t* __restrict__ taken_p,
                                                                        const uint8_t* __restrict__ alloc,
@@ -897,7 +874,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
                     uint32_t taken = 0;
 #pragma unroll
                     for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
-                    ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);
+                    ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
                     if (s.kind == 0) {
                         f = 0;
                         if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
@@ -955,7 +932,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
                 const int ai = alloc != nullptr ? alloc[e] : 0;
                 const ocro::Sub& s = subs[ai];
                 ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
-                ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);
+                ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
                 ops.level0(r, s);
                 const bool joint = s.n == 2;
                 const int a0 = joint ? k / 5 : k, c1 = joint ? k % 5 : ocro::kNoop;
@@ -1024,7 +1001,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
 // items by a prefix sum, one per lane, folded by LDS atomics) gave the same outputs with 0.70 of
 // the lanes active but ran 0.129 ms against 0.118 at C5, where most (env, configuration) pairs
 // have 0 or 1 location; it was removed in round 5 (profiles/r04/bounds_compact/).
-template <int A, int K, bool W>
+template <int A, int K, bool W, bool GD>
 __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                            const uint8_t* __restrict__ blob_g,
                                                            float* __restrict__ lb, uint8_t* __restrict__ doable) {
@@ -1036,7 +1013,7 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
     const int i0 = (int)(blockIdx.y * R.nsub / gridDim.y), i1 = (int)((blockIdx.y + 1) * R.nsub / gridDim.y);
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
         const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
-        ocro::RowOps<A, K, W> ops(R.L, blob, W ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+        ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
         for (int i = i0; i < i1; ++i) {
             float v;
             const bool ok = ops.full_bound(r, subs[i], v);
@@ -1973,24 +1950,17 @@ int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, i
                     int64_t dist_len) {
     if (h == nullptr || num_nodes == nullptr) return fail(OC_EINVAL, "bad argument");
     ErrScope es_(h);
-    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "no reachability graph for this level");
+    if (h->roll.nnodes < 0)
+        return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (a level of more than 255 cells) or a BFS distance of 255", ocro::kMaxNodesWide);
     const int n = h->roll.nnodes, cells = h->level.width * h->level.height;
     *num_nodes = n;
     if (node_of != nullptr) {
         if (node_of_len < (int64_t)cells * 5) return fail(OC_EINVAL, "node_of needs %d entries", cells * 5);
-        const uint32_t* hd = (const uint32_t*)(h->roll_blob_host.data() + h->roll.node_off);
-        for (int i = 0; i < cells * 5; ++i) node_of[i] = (uint16_t)(hd[i] & 0xFFFFu);  // kNoHandle -> 0xFFFF
+        memcpy(node_of, h->roll_blob_host.data() + h->roll.node_off, (size_t)cells * 5 * sizeof(uint16_t));
     }
     if (dist != nullptr) {
-        if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %lld bytes", (long long)n * n);
-        if (h->roll.max_dist > 254)
-            return fail(OC_ELEVEL, "a node distance of %d does not fit the u8 table (the planner entry points take it)",
-                        h->roll.max_dist);
-        // the node table the Floor distances define (oc_rollout.h), built for the export
-        ocro::RollLevel L2;
-        std::vector<uint8_t> blob2, dist_v;
-        ocro::build_roll_level(L2, blob2, h->level.width, h->level.height, h->level.tiles, h->level.encoding, &dist_v);
-        memcpy(dist, dist_v.data(), (size_t)n * n);
+        if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %d bytes", n * n);
+        memcpy(dist, h->roll_blob_host.data() + h->roll.dist_off, (size_t)n * n);
     }
     return OC_OK;
 }
@@ -2041,7 +2011,19 @@ int oc_get_layout(const oc_handle* h, int64_t B, oc_layout* out) {
         default: return fail(OC_EINVAL, "unsupported (A,K)=(%d,%d)", (A_), (K_));           \
     }
 
-// The planner kernels: narrow (byte cell ids) or wide (u16) rows.
+// The planner kernels: LAUNCH(A, K, W, GD): narrow (byte cell ids) or wide (u16) rows; the
+// distance table in LDS (GD false) or in device memory (GD: every wide level, and a narrow level
+// whose graph has more than ocro::kMaxNodes nodes).
+#define OC_DISPATCH_PLAN(h_, LAUNCH)                                                        \
+    if ((h_)->wide) {                                                                       \
+        OC_DISPATCH((h_)->A, (h_)->K, OC_PLAN_WIDE)                                         \
+    } else if ((h_)->roll.dist_global) {                                                    \
+        OC_DISPATCH((h_)->A, (h_)->K, OC_PLAN_NARROW_GD)                                    \
+    } else {                                                                                \
+        OC_DISPATCH((h_)->A, (h_)->K, OC_PLAN_NARROW)                                       \
+    }
+
+// The render kernel: narrow (byte cell ids) or wide (u16) rows.
 #define OC_DISPATCH_W(h_, LAUNCH)                                                           \
     if ((h_)->wide) {                                                                       \
         switch ((h_)->A * ((h_)->K >= 10 ? 100 : 10) + (h_)->K) {                           \
@@ -2339,11 +2321,11 @@ static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num
         if (subtasks[i].level != OC_LEVEL0 && !level1_ok)
             return fail(OC_EINVAL, "subtask %d: only oc_rollout takes OC_LEVEL1", i);
     if (num_subtasks < 1 || num_subtasks > OC_MAX_SUBTASKS) return fail(OC_EINVAL, "num_subtasks %d", num_subtasks);
-    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "no reachability graph for this level");
+    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (a level of more than 255 cells) or a BFS distance of 255", ocro::kMaxNodesWide);
     if (h->roll_blob == nullptr) return fail(OC_EHIP, "rollout tables not on the device");
     R.L = h->roll;
     R.nsub = num_subtasks;
-    R.blob_words = h->roll.lds_bytes / 4;  // staged in LDS: the whole blob, or a wide level's tables
+    R.blob_words = h->roll.lds_bytes / 4;  // staged in LDS: the whole blob, or the tables before the distances
     R.pitch = pitch_for(B);
     R.B = B;
     for (int i = 0; i < num_subtasks; ++i) {
@@ -2402,12 +2384,18 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
-#define OC_LAUNCH_ROLL(A, K, W)                                                                              \
-    if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W>, h->roll.lds_bytes)) return rc;    \
-    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,             \
-                       (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags,    \
+#define OC_LAUNCH_ROLL(A, K, W, GD)                                                                             \
+    if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W, GD>, h->roll.lds_bytes)) return rc;   \
+    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W, GD>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,            \
+                       (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags,       \
                        lower_bound)
-    OC_DISPATCH_W(h, OC_LAUNCH_ROLL)
+#define OC_PLAN_WIDE(A, K) OC_LAUNCH_ROLL(A, K, true, true)
+#define OC_PLAN_NARROW_GD(A, K) OC_LAUNCH_ROLL(A, K, false, true)
+#define OC_PLAN_NARROW(A, K) OC_LAUNCH_ROLL(A, K, false, false)
+    OC_DISPATCH_PLAN(h, OC_LAUNCH_ROLL)
+#undef OC_PLAN_WIDE
+#undef OC_PLAN_NARROW_GD
+#undef OC_PLAN_NARROW
     return hip_check("oc_rollout launch");
 }
 
@@ -2438,22 +2426,28 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     const int64_t need = (B + rows_per_block - 1) / rows_per_block, cap = (int64_t)h->cus * (any_joint ? 16 : 8);
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
-#define OC_LIK_GO(KERN, A, K, GG, W)                                                                                 \
+#define OC_LIK_GO(KERN, A, K, GG, W, GD)                                                                             \
     do {                                                                                                             \
-        if (const int rc = allow_dyn_lds((const void*)KERN<A, K, GG, W>, h->roll.lds_bytes)) return rc;              \
-        hipLaunchKernelGGL((KERN<A, K, GG, W>), grid, dim3(kBlock), h->roll.lds_bytes, st, R, (const uint8_t*)state, \
+        if (const int rc = allow_dyn_lds((const void*)KERN<A, K, GG, W, GD>, h->roll.lds_bytes)) return rc;          \
+        hipLaunchKernelGGL((KERN<A, K, GG, W, GD>), grid, dim3(kBlock), h->roll.lds_bytes, st, R, (const uint8_t*)state, \
                            taken, alloc, h->roll_blob, self_agent, beta, none_action_prob, likelihood, out_flags);   \
     } while (0)
-#define OC_LAUNCH_LIK(A, K, W)                                                                                       \
+#define OC_LAUNCH_LIK(A, K, W, GD)                                                                                   \
     if (compact && any_joint)                                                                                        \
-        OC_LIK_GO(oc_likelihood_compact_kernel, A, K, 32, W);                                                        \
+        OC_LIK_GO(oc_likelihood_compact_kernel, A, K, 32, W, GD);                                                    \
     else if (compact)                                                                                                \
-        OC_LIK_GO(oc_likelihood_compact_kernel, A, K, 8, W);                                                         \
+        OC_LIK_GO(oc_likelihood_compact_kernel, A, K, 8, W, GD);                                                     \
     else if (any_joint)                                                                                              \
-        OC_LIK_GO(oc_likelihood_kernel, A, K, 32, W);                                                                \
+        OC_LIK_GO(oc_likelihood_kernel, A, K, 32, W, GD);                                                            \
     else                                                                                                             \
-        OC_LIK_GO(oc_likelihood_kernel, A, K, 8, W)
-    OC_DISPATCH_W(h, OC_LAUNCH_LIK)
+        OC_LIK_GO(oc_likelihood_kernel, A, K, 8, W, GD)
+#define OC_PLAN_WIDE(A, K) OC_LAUNCH_LIK(A, K, true, true)
+#define OC_PLAN_NARROW_GD(A, K) OC_LAUNCH_LIK(A, K, false, true)
+#define OC_PLAN_NARROW(A, K) OC_LAUNCH_LIK(A, K, false, false)
+    OC_DISPATCH_PLAN(h, OC_LAUNCH_LIK)
+#undef OC_PLAN_WIDE
+#undef OC_PLAN_NARROW_GD
+#undef OC_PLAN_NARROW
     return hip_check("oc_nav_likelihood launch");
 }
 
@@ -2479,11 +2473,17 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
     if (chunks < 1) chunks = 1;
     const dim3 grid((unsigned)bx, (unsigned)chunks);
     hipStream_t st = (hipStream_t)stream;
-#define OC_LAUNCH_BOUNDS(A, K, W)                                                                         \
-    if (const int rc = allow_dyn_lds((const void*)oc_bounds_kernel<A, K, W>, h->roll.lds_bytes)) return rc;  \
-    hipLaunchKernelGGL((oc_bounds_kernel<A, K, W>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,           \
+#define OC_LAUNCH_BOUNDS(A, K, W, GD)                                                                         \
+    if (const int rc = allow_dyn_lds((const void*)oc_bounds_kernel<A, K, W, GD>, h->roll.lds_bytes)) return rc;  \
+    hipLaunchKernelGGL((oc_bounds_kernel<A, K, W, GD>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,           \
                        (const uint8_t*)state, h->roll_blob, lower_bound, doable)
-    OC_DISPATCH_W(h, OC_LAUNCH_BOUNDS)
+#define OC_PLAN_WIDE(A, K) OC_LAUNCH_BOUNDS(A, K, true, true)
+#define OC_PLAN_NARROW_GD(A, K) OC_LAUNCH_BOUNDS(A, K, false, true)
+#define OC_PLAN_NARROW(A, K) OC_LAUNCH_BOUNDS(A, K, false, false)
+    OC_DISPATCH_PLAN(h, OC_LAUNCH_BOUNDS)
+#undef OC_PLAN_WIDE
+#undef OC_PLAN_NARROW_GD
+#undef OC_PLAN_NARROW
     return hip_check("oc_subtask_bounds launch");
 }
 

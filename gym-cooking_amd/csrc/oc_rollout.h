@@ -9,23 +9,25 @@
 //   lower_bound()   get_lower_bound_for_subtask_given_objs  overcooked_environment.py:480-664,
 //                   World.get_lower_bound_between(_helper), check_bound  world.py:115-283
 // The reachability graph of the static level (world.py:67-108) is precomputed by
-// build_roll_level().  Its shortest paths decompose exactly over the Floor squares: a collidable
-// square's approach node has one edge, to the Floor it is approached from (world.py:96-104), so
-// it is a leaf and no shortest path passes through it.  The distance between two nodes is
-// therefore the BFS distance between their Floor squares plus one per approach node (0 for the
-// same node), and the level keeps only the Floor-to-Floor table (round 5; it kept the all-pairs
-// node table before, n^2 bytes, which capped a narrow level's graph at 390 nodes).  A narrow
-// level (at most 255 cells) has at most 255 Floor squares: its table (u8, < 64 KB) and the other
-// static tables (tile classes, node handles, Cutboard / Delivery lists, nearest-Cutboard /
-// -Delivery rows) form one blob that the kernels stage in LDS, whatever the node count.  A wide
-// level (up to 1,024 cells) keeps its Floor table (u16) in device memory (L2) and stages the
-// rest.  Distances and bounds are exact in fp32 (integers and halves < 2^12).
+// build_roll_level() as a compact all-pairs distance table (u8, 0xFF = no path).  The static
+// tables of a level (tile classes, graph node ids, Cutboard / Delivery lists, distances) form
+// one byte blob, sized per level (the tables + nnodes^2 distance bytes).  A narrow level's
+// kernels stage all of it in LDS when its graph has at most kMaxNodes nodes: a 7x7 kitchen's blob
+// is ~7 KB, the largest ~134 KB, which they get as dynamic LDS past the default 64 KB (gfx950 has
+// 160 KB per CU).  A larger graph (round 5: a narrow level of more than kMaxNodes nodes, e.g. a
+// 255-cell kitchen dense with counter islands) and every wide level (more than 255 cells) stage
+// the tables in front of the distances only and read the distance table from device memory (L2;
+// RollLevel.dist_global, the planner kernels' GD instantiation), so a narrow graph may have every
+// node its cells can make (5 x 255) and a wide one up to kMaxNodesWide (a 1,024-cell kitchen's
+// 5,120 approach nodes at most, 26 MB).  Distances and bounds are exact in fp32 (integers and
+// halves < 2^9).  (Round 5 also measured a table of the distances between Floor squares only --
+// an approach node is a leaf one edge from its Floor -- with no node limit: 10-20 % slower C5
+// kernels at the same outputs, profiles/r05/ab/; not kept.)
 //
 // The includer defines __host__ / __device__ (HIP, or empty for the host test harness).
 #pragma once
 
 #include <stdint.h>
-#include <string.h>
 
 #include <vector>
 
@@ -47,10 +49,13 @@ struct ConditionalT<false, T, F> {
 
 constexpr int kMaxCells = 255;      // narrow levels: cell ids are bytes, 0xFF = dead / none
 constexpr int kMaxCellsWide = 1024;  // wide levels (more than 255 cells): u16 cell ids, 0xFFFF dead
-// A graph node's handle (the node table's u32 entries): bits 0-15 its node id (the reference's
-// graph order, kNoNode = none), bits 16-26 the index of its Floor square in the Floor table,
-// bit 31 set for the approach node of a collidable square (one edge away from that Floor).
-constexpr uint32_t kNoHandle = 0xFFFFFFFFu;
+// compact reachability-graph node ids are u16 (kNoNode = none); at most kMaxNodes nodes keep a
+// block's LDS (blob + 64 configurations + the kernels' own) within the 160 KB of a gfx950 CU,
+// a larger graph's distances stay in device memory; distances are bytes (0xFF = no path), so a
+// graph whose BFS distances reach 255 is refused
+constexpr int kMaxNodes = 360;  // 360^2 + the other tables + the compacted likelihood's 18 KB < 160 KB
+constexpr int kMaxNodesNarrow = 5 * kMaxCells;    // narrow levels: every node 255 cells can make
+constexpr int kMaxNodesWide = 5 * kMaxCellsWide;  // wide levels: the distances stay in device memory
 constexpr uint8_t kNone = 0xFF;
 constexpr uint16_t kNoNode = 0xFFFF;
 constexpr int kFloor = 0, kCounter = 1, kCutboard = 2, kDelivery = 3;  // OC_TILE_*
@@ -60,27 +65,28 @@ constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NA
 // Static level tables, one byte blob (offsets in RollLevel, set by build_roll_level):
 //   tile_off   [C] tile class per cell (C = 256 for a narrow level: cells >= W*H read Counter;
 //              the cell count rounded up to 4 for a wide one)
-//   node_off   u32 [W * H * 5] node handle of (cell, approach), approach 4 = (0, 0); kNoHandle = none
+//   xy_off     u16 [C] x | y << 8 of each cell (the bound's Manhattan terms read it instead of
+//              dividing by W: round 5)
+//   node_off   u16 [C * 5] graph node of (cell, approach), approach 4 = (0, 0)
 //   cut_off    Cutboard cells in scan order (L.ncut; u8 narrow, u16 wide)
 //   deliv_off  Delivery cells in scan order (L.ndeliv; u8 narrow, u16 wide)
-//   dmin_off   u16 [2][nnodes] the distance from a node to the nearest Cutboard (row 0) / Delivery
-//              (row 1) approach node, 0xFFFF = none reachable
-//   dist_off   [nfloor][nfloor] BFS distances between Floor squares (u8, 0xFF = no path, narrow;
-//              u16, 0xFFFF, wide; last: a wide level stages the blob up to here)
-// A narrow level's tile table has 256 entries (the dead cell 0xFF reads Counter); a 7x7 kitchen's
-// blob is ~2.4 KB (round 4's, with the all-pairs node table: ~7 KB).
+//   dmin_off   [2][nnodes] the distance from a node to the nearest Cutboard (row 0) / Delivery
+//              (row 1) approach node, 0xFF = none reachable
+//   dist_off   [nnodes][nnodes] BFS distances (last: a wide level stages the blob up to here)
+// A narrow level's first offsets are fixed: 0, 256, 768, 3328, 3584, then dmin at 3840.
 
 struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t W, H, perimeter, nnodes;
-    int32_t nfloor;    // Floor squares: the distance table is nfloor x nfloor
     int32_t ncut, ndeliv;
     int32_t enc;       // item mask encoding (OC_ENC_*)
     int32_t dmin_off;  // blob offset of the nearest-Cutboard / nearest-Delivery distance rows
     int32_t tile_off, node_off, cut_off, deliv_off, dist_off;
+    int32_t xy_off;    // u16 x | y << 8 per cell
     int32_t wide;      // u16 cell ids (W * H > 255)
     int32_t blob_bytes;  // the blob's size (a multiple of 4)
-    int32_t lds_bytes;   // what the kernels stage in LDS: all of it (narrow), up to dist_off (wide)
-    int32_t max_dist;    // the largest finite node-to-node distance (oc_reachability's u8 table)
+    int32_t lds_bytes;   // what the kernels stage in LDS: all of it, or up to dist_off (dist_global)
+    int32_t dist_global; // the distance table is read from device memory: a wide level, or a narrow
+                         // one of more than kMaxNodes nodes (the planner kernels' GD instantiation)
 };
 
 // The environment step's level constants (the scalar step of wide levels, RowOps::env_step).
@@ -158,6 +164,16 @@ OC_RH bool wave_any(bool p) {
 #endif
 }
 
+// a * b for operands and product below 2^24: v_mul_u32_u24 (full rate) on the device, where the
+// plain 32-bit multiply is quarter rate
+OC_RH uint32_t mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul24(a, b);
+#else
+    return a * b;
+#endif
+}
+
 // byte v occurs in one of the four bytes of w
 OC_RH bool has_byte(uint32_t w, uint32_t v) {
     const uint32_t x = w ^ (v * 0x01010101u);
@@ -171,14 +187,11 @@ OC_RH bool has_u16(uint64_t w, uint32_t v) {
 }
 
 // ---- host: level tables ----------------------------------------------------------------------
-// Builds the reachability graph of make_reachability_graph (world.py:67-108) into `blob_v`
-// (resized to the blob): the node handles, the BFS distances between Floor squares, and the
-// nearest-Cutboard / -Delivery rows.  `dist_v` (optional) receives the all-pairs node distance
-// table the graph defines (u8 [n][n], 0xFF = no path, clamped at 0xFE: oc_reachability checks
-// L.max_dist).  Returns the node count, or -1 when the level has more cells than its layout
-// takes (255 narrow, kMaxCellsWide wide).
-inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, int H, const uint8_t* tiles, int enc,
-                            std::vector<uint8_t>* dist_v = nullptr) {
+// Builds the reachability graph of make_reachability_graph (world.py:67-108) and its BFS
+// distances into `blob_v` (resized to the blob).  Returns the node count, or -1 when the level
+// has more cells than its layout takes (255 narrow, kMaxCellsWide wide), or a BFS distance past
+// 254 (the byte table cannot hold it).
+inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, int H, const uint8_t* tiles, int enc) {
     L.W = W;
     L.enc = enc;
     L.H = H;
@@ -189,14 +202,17 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
     L.wide = cells > kMaxCells ? 1 : 0;
     if (cells > kMaxCellsWide) return -1;
     const int C = L.wide ? (cells + 3) & ~3 : 256, lb = L.wide ? 2 : 1;  // table cells, list entry bytes
+    const int max_nodes = L.wide ? kMaxNodesWide : kMaxNodesNarrow;
     L.tile_off = 0;
-    L.node_off = C;
-    L.cut_off = L.node_off + 4 * cells * 5;  // node handles of the level's cells only
+    L.xy_off = C;
+    L.node_off = 3 * C;
+    L.cut_off = L.node_off + 2 * C * 5;
     L.deliv_off = L.cut_off + lb * C;
     L.dmin_off = L.deliv_off + lb * C;
     blob_v.assign((size_t)L.dmin_off, 0);  // grown below once the node count is known
     uint8_t* blob = blob_v.data();
     uint8_t* tile = blob + L.tile_off;
+    uint16_t* node = (uint16_t*)(blob + L.node_off);
     auto put_list = [&](int off, int i, int c) {
         if (L.wide) ((uint16_t*)(blob + off))[i] = (uint16_t)c;
         else blob[off + i] = (uint8_t)c;
@@ -206,14 +222,9 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
         if (c < cells && tiles[c] == kCutboard) put_list(L.cut_off, L.ncut++, c);
         if (c < cells && tiles[c] == kDelivery) put_list(L.deliv_off, L.ndeliv++, c);
     }
-    // nodes in the reference's order (cell scan; a Floor's own node, then the approach sides),
-    // each with its Floor square: its own cell, or the Floor it is approached from
-    std::vector<uint32_t> handle((size_t)cells * 5, kNoHandle);
-    std::vector<int> fidx((size_t)cells, -1), node_floor;
-    std::vector<uint8_t> node_app;
-    int nf = 0;
-    for (int c = 0; c < cells; ++c)
-        if (tiles[c] == kFloor) fidx[(size_t)c] = nf++;
+    for (int i = 0; i < C * 5; ++i) node[i] = kNoNode;
+    for (int c = 0; c < C; ++c)
+        ((uint16_t*)(blob + L.xy_off))[c] = c < cells ? (uint16_t)((c % W) | ((c / W) << 8)) : (uint16_t)0;
     int n = 0;
     auto clampx = [&](int v) { return v < 0 ? 0 : (v > W - 1 ? W - 1 : v); };
     auto clampy = [&](int v) { return v < 0 ? 0 : (v > H - 1 ? H - 1 : v); };
@@ -221,62 +232,64 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
         const int x = c % W, y = c / W;
         const bool coll = tiles[c] != kFloor;
         if (!coll) {
-            handle[(size_t)c * 5 + 4] = (uint32_t)n | ((uint32_t)fidx[(size_t)c] << 16);
-            node_floor.push_back(fidx[(size_t)c]);
-            node_app.push_back(0);
-            ++n;
+            if (n >= max_nodes) return -1;
+            node[c * 5 + 4] = (uint16_t)n++;
         }
         for (int d = 0; d < 4; ++d) {
             const int nc = clampy(y + kDY[d]) * W + clampx(x + kDX[d]);
-            if (coll && tiles[nc] == kFloor) {  // world.py:96-100: its one edge, to that Floor
-                handle[(size_t)c * 5 + d] = (uint32_t)n | ((uint32_t)fidx[(size_t)nc] << 16) | 0x80000000u;
-                node_floor.push_back(fidx[(size_t)nc]);
-                node_app.push_back(1);
-                ++n;
+            if (coll && tiles[nc] == kFloor) {
+                if (n >= max_nodes) return -1;
+                node[c * 5 + d] = (uint16_t)n++;
             }
         }
     }
-    if (n > 0xFFFE) return -1;
-    memcpy(blob + L.node_off, handle.data(), handle.size() * sizeof(uint32_t));
-    // BFS between Floor squares: Floor-Floor edges only (world.py:105-107); the approach nodes
-    // are leaves (world.py:96-104) and never lie on a shortest path between other nodes
-    constexpr int kInf = 0x7FFFFFFF;
-    std::vector<int> fd((size_t)nf * nf, kInf), q((size_t)(nf > 0 ? nf : 1));
-    std::vector<int> fcell;
-    for (int c = 0; c < cells; ++c)
-        if (tiles[c] == kFloor) fcell.push_back(c);
-    for (int s0 = 0; s0 < nf; ++s0) {
-        int* row = fd.data() + (size_t)s0 * nf;
+    // adjacency (undirected): floor-floor, and a collidable square's approach node with the
+    // floor it is approached from
+    static const int opp[4] = {1, 0, 3, 2};
+    std::vector<uint16_t> adj_v((size_t)n * 8);
+    std::vector<int> deg((size_t)n, 0), q((size_t)n);
+    auto adj = [&](int u, int k) -> uint16_t& { return adj_v[(size_t)u * 8 + k]; };
+    auto link = [&](int u, int v) {
+        if (u == kNoNode || v == kNoNode || u == v) return;
+        for (int k = 0; k < deg[u]; ++k)
+            if (adj(u, k) == v) return;
+        adj(u, deg[u]++) = (uint16_t)v;
+        adj(v, deg[v]++) = (uint16_t)u;
+    };
+    for (int c = 0; c < cells; ++c) {
+        const int x = c % W, y = c / W;
+        const bool coll = tiles[c] != kFloor;
+        for (int d = 0; d < 4; ++d) {
+            const int nc = clampy(y + kDY[d]) * W + clampx(x + kDX[d]);
+            const bool ncoll = tiles[nc] != kFloor;
+            if (coll && !ncoll) link(node[c * 5 + d], node[nc * 5 + 4]);
+            else if (!coll && ncoll) link(node[c * 5 + 4], node[nc * 5 + opp[d]]);
+            else if (!coll && !ncoll) link(node[c * 5 + 4], node[nc * 5 + 4]);
+        }
+    }
+    L.dist_off = (L.dmin_off + 2 * n + 3) & ~3;
+    blob_v.resize((size_t)L.dist_off + (size_t)n * n + 4, 0);
+    blob = blob_v.data();
+    tile = blob + L.tile_off;
+    node = (uint16_t*)(blob + L.node_off);
+    uint8_t* dist = blob + L.dist_off;
+    for (int s = 0; s < n; ++s) {
+        uint8_t* row = dist + (size_t)s * n;
+        for (int t = 0; t < n; ++t) row[t] = kNone;
         int qh = 0, qt = 0;
-        row[s0] = 0;
-        q[(size_t)qt++] = s0;
+        row[s] = 0;
+        q[qt++] = s;
         while (qh < qt) {
-            const int u = q[(size_t)qh++], cu = fcell[(size_t)u], x = cu % W, y = cu / W;
-            for (int d = 0; d < 4; ++d) {
-                const int nc = clampy(y + kDY[d]) * W + clampx(x + kDX[d]);
-                const int v = fidx[(size_t)nc];
-                if (v >= 0 && row[v] == kInf) {
-                    row[v] = row[u] + 1;
-                    q[(size_t)qt++] = v;
+            const int u = q[qh++];
+            for (int k = 0; k < deg[u]; ++k) {
+                const int v = adj(u, k);
+                if (row[v] == kNone) {
+                    if (row[u] + 1 >= kNone) return -1;  // a distance the byte table cannot hold
+                    row[v] = (uint8_t)(row[u] + 1);
+                    q[qt++] = v;
                 }
             }
         }
-    }
-    // node distances: d(floor u, floor v) + one per approach node, 0 for the same node
-    auto node_dist = [&](int u, int v) -> int {
-        if (u == v) return 0;
-        const int d = fd[(size_t)node_floor[(size_t)u] * nf + node_floor[(size_t)v]];
-        return d == kInf ? -1 : d + node_app[(size_t)u] + node_app[(size_t)v];
-    };
-    L.dist_off = (L.dmin_off + 2 * 2 * n + 3) & ~3;
-    const int fbytes = L.wide ? 2 : 1;
-    L.blob_bytes = (int32_t)((L.dist_off + (size_t)nf * nf * fbytes + 3) & ~(size_t)3);
-    blob_v.resize((size_t)L.blob_bytes, 0);
-    blob = blob_v.data();
-    for (size_t i = 0; i < (size_t)nf * nf; ++i) {
-        const int d = fd[i];
-        if (L.wide) ((uint16_t*)(blob + L.dist_off))[i] = d == kInf ? (uint16_t)0xFFFF : (uint16_t)d;
-        else blob[L.dist_off + i] = d == kInf ? kNone : (uint8_t)d;  // < nf <= 255 Floor squares
     }
     // Chop and Deliver have a static B side (every Cutboard / every Delivery square, from any
     // side it is approached from): the single-agent bound's min over B of dist(A node, B node)
@@ -284,32 +297,26 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
     for (int side = 0; side < 2; ++side) {
         const int off = side == 0 ? L.cut_off : L.deliv_off;
         const int nc = side == 0 ? L.ncut : L.ndeliv;
-        uint16_t* dm = (uint16_t*)(blob + L.dmin_off) + (size_t)side * n;
+        uint8_t* dm = blob + L.dmin_off + side * n;
         for (int v = 0; v < n; ++v) {
-            int best = -1;
+            int best = kNone;
             for (int i = 0; i < nc; ++i) {
                 const int cell = L.wide ? ((const uint16_t*)(blob + off))[i] : blob[off + i];
                 for (int d = 0; d < 4; ++d) {
-                    const uint32_t b = handle[(size_t)cell * 5 + d];
-                    if (b == kNoHandle) continue;
-                    const int dd = node_dist(v, (int)(b & 0xFFFFu));
-                    if (dd >= 0 && (best < 0 || dd < best)) best = dd;
+                    const int b = node[cell * 5 + d];
+                    if (b == kNoNode) continue;
+                    const int dd = dist[(size_t)v * n + b];
+                    if (dd != kNone && dd < best) best = dd;
                 }
             }
-            dm[v] = best < 0 ? (uint16_t)0xFFFF : (uint16_t)best;
+            dm[v] = (uint8_t)best;
         }
     }
-    L.max_dist = 0;
-    if (dist_v != nullptr) dist_v->assign((size_t)n * n, kNone);
-    for (int u = 0; u < n; ++u)
-        for (int v = 0; v < n; ++v) {
-            const int d = node_dist(u, v);
-            if (d > L.max_dist) L.max_dist = d;
-            if (dist_v != nullptr && d >= 0) (*dist_v)[(size_t)u * n + v] = (uint8_t)(d < 0xFE ? d : 0xFE);
-        }
     L.nnodes = n;
-    L.nfloor = nf;
-    L.lds_bytes = L.wide ? L.dist_off : L.blob_bytes;
+    L.blob_bytes = (int32_t)((L.dist_off + (size_t)n * n + 3) & ~(size_t)3);
+    L.dist_global = L.wide || n > kMaxNodes ? 1 : 0;
+    L.lds_bytes = L.dist_global ? L.dist_off : L.blob_bytes;
+    blob_v.resize((size_t)L.blob_bytes, 0);
     return n;
 }
 
@@ -345,7 +352,8 @@ struct RowOps {
         if constexpr (WIDE) return ((const uint16_t*)(T + off))[i];
         else return T[off + i];
     }
-    OC_RH int cell(int x, int y) const { return y * L.W + x; }
+    OC_RH int cell(int x, int y) const { return (int)mul24((uint32_t)y, (uint32_t)L.W) + x; }
+    OC_RH uint32_t xy(int c) const { return ((const uint16_t*)(T + L.xy_off))[c]; }  // x | y << 8
     OC_RH int agent_cell(const Row& r, int a) const { return cell(r.ax(a), r.ay(a)); }
 
     // level0: agents outside the subtask freeze into AgentCounters; their items leave.
@@ -499,26 +507,17 @@ struct RowOps {
         return count > s.count;
     }
 
-    OC_RH uint32_t nid(int c, int d) const {  // graph node handle of (cell, approach)
-        return ((const uint32_t*)(T + L.node_off))[c * 5 + d];
+    OC_RH int nid(int c, int d) const {  // graph node of (cell, approach)
+        return ((const uint16_t*)(T + L.node_off))[mul24((uint32_t)c, 5u) + d];
     }
-    // nx.shortest_path_length between two node handles, or -1: the Floor squares' distance plus
-    // one per approach node, 0 for the same node.  Branch-free: a missing node reads entry
-    // (0, 0) and is masked, so every lane of a wave issues the same table reads.
-    OC_RH int dn(uint32_t u, uint32_t v) const {
-        const bool none = u == kNoHandle || v == kNoHandle;
-        const uint32_t i = none ? 0u : ((u >> 16) & 0x7FFu) * (uint32_t)L.nfloor + ((v >> 16) & 0x7FFu);
-        int d;
-        bool miss;
-        if constexpr (WIDE) {
-            d = ((const uint16_t*)D)[i];
-            miss = d == 0xFFFF;
-        } else {
-            d = D[i];
-            miss = d == kNone;
-        }
-        if (none || miss) return -1;
-        return u == v ? 0 : d + (int)(u >> 31) + (int)(v >> 31);
+    OC_RH int dn(int u, int v) const {  // nx.shortest_path_length between node ids, or -1
+        // branch-free: a missing node reads entry (0, 0) and is masked, so every lane of a
+        // wave issues the same table reads
+        const bool none = u == kNoNode || v == kNoNode;
+        // narrow: u * nnodes < 1275^2 < 2^24, the full-rate 24-bit multiply; wide: up to 5,120^2
+        const uint32_t i = WIDE ? (uint32_t)u * (uint32_t)L.nnodes + (uint32_t)v : mul24((uint32_t)u, (uint32_t)L.nnodes) + (uint32_t)v;
+        const int d = D[none ? 0u : i];
+        return none || d == kNone ? -1 : d;
     }
 
     // World.get_lower_bound_between_helper (world.py:148-264) with check_bound (:266-283).  The
@@ -538,10 +537,11 @@ struct RowOps {
         float lower = per + 1.0f;
         const bool Acoll = tile(Ac) != kFloor, Bcoll = tile(Bc) != kFloor;
         const int nA = wave_any(Acoll) ? 4 : 1, nB = wave_any(Bcoll) ? 4 : 1;
-        const int dx = Ac % L.W - Bc % L.W, dy = Ac / L.W - Bc / L.W;
+        const uint32_t pa = xy(Ac), pb = xy(Bc);
+        const int dx = (int)(pa & 0xFFu) - (int)(pb & 0xFFu), dy = (int)(pa >> 8) - (int)(pb >> 8);
         const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
-        const uint32_t u0 = nid(ag0, 4);
-        uint32_t vA[4], vB[4];
+        const int u0 = nid(ag0, 4);
+        int vA[4], vB[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             vA[q] = nid(Ac, Acoll ? q : 4);
@@ -562,7 +562,7 @@ struct RowOps {
             }
             return lower > 1.0f ? lower : 1.0f;
         }
-        const uint32_t u1 = nid(ag1, 4);
+        const int u1 = nid(ag1, 4);
         float b1B[4], b2B[4];
 #pragma unroll
         for (int ib = 0; ib < 4; ++ib) {
@@ -603,29 +603,30 @@ struct RowOps {
     // helper() clamps each pair's result to >= 1 and starts from perimeter + 1; both are
     // monotone, so the min over B of helper() is this with the same clamp.  Exact in fp32.
     OC_RH float helper_static(const Sub& s, int ag0, int ag1, int Ac, int bl_off, int nb,
-                              const uint16_t* dm) const {
+                              const uint8_t* dm) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
         if (nb == 0) return lower;
         const bool Acoll = tile(Ac) != kFloor;
         const int nA = wave_any(Acoll) ? 4 : 1;  // wave-uniform (a Floor A repeats its node)
-        const uint32_t u0 = nid(ag0, 4);
+        const int u0 = nid(ag0, 4);
         if (s.n == 1) {
 #pragma unroll
             for (int ia = 0; ia < 4; ++ia) {
                 if (ia >= nA) continue;
-                const uint32_t vA = nid(Ac, Acoll ? ia : 4);
-                const int a1 = dn(u0, vA), m = dm[vA == kNoHandle ? 0u : vA & 0xFFFFu];
+                const int vA = nid(Ac, Acoll ? ia : 4);
+                const int a1 = dn(u0, vA), m = dm[vA == kNoNode ? 0 : vA];
                 const float bound = (float)(a1 + m - 1);
-                lower = vA != kNoHandle && a1 >= 0 && m != 0xFFFF && bound < lower ? bound : lower;
+                lower = vA != kNoNode && a1 >= 0 && m != kNone && bound < lower ? bound : lower;
             }
         } else {
-            const uint32_t u1 = nid(ag1, 4);
-            const int ax = Ac % L.W, ay = Ac / L.W;
+            const uint32_t pa = xy(Ac);
+            const int u1 = nid(ag1, 4), ax = (int)(pa & 0xFFu), ay = (int)(pa >> 8);
             int man = 0x7FFF;
             for (int i = 0; i < nb; ++i) {
                 const int b = list_cell(bl_off, i);
-                const int dx = ax - b % L.W, dy = ay - b / L.W;
+                const uint32_t pb = xy(b);
+                const int dx = ax - (int)(pb & 0xFFu), dy = ay - (int)(pb >> 8);
                 const int m = (dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy);
                 man = m < man ? m : man;
             }
@@ -633,7 +634,7 @@ struct RowOps {
 #pragma unroll
             for (int ia = 0; ia < 4; ++ia) {
                 if (ia >= nA) continue;
-                const uint32_t vA = nid(Ac, Acoll ? ia : 4);
+                const int vA = nid(Ac, Acoll ? ia : 4);
                 int t;
                 const float b1A = (t = dn(u0, vA)) < 0 ? per : (float)t;
                 const float b2A = (t = dn(u1, vA)) < 0 ? per : (float)t;
@@ -723,7 +724,7 @@ struct RowOps {
         if (s.kind == 1 || s.kind == 3) {  // static B side: one table lookup per A approach
             const int bl = s.kind == 1 ? L.cut_off : L.deliv_off;
             const int nb = s.kind == 1 ? L.ncut : L.ndeliv;
-            const uint16_t* dm = (const uint16_t*)(T + L.dmin_off) + (s.kind == 1 ? 0 : L.nnodes);
+            const uint8_t* dm = T + L.dmin_off + (s.kind == 1 ? 0 : L.nnodes);
             visit_objs(r, s.start[0], s.kind == 3, [&](int Ac) OC_RL {
                 const float b = helper_static(s, ag0, ag1, Ac, bl, nb, dm);
                 if (b < lower) lower = b;
@@ -797,7 +798,7 @@ struct RowOps {
     OC_RH uint32_t env_step(Row& r, uint32_t& t, uint32_t fl, uint32_t act, const StepLevel& S, uint32_t& ex,
                             uint32_t& cm) {
         ac = kNoAc;
-        constexpr uint32_t kNoops = 0x04040404u & (A == 4 ? 0xFFFFFFFFu : (1u << (8 * A)) - 1u);
+        constexpr uint32_t kNoops = 0x04040404u & (A == 4 ? 0xFFFFFFFFu : (1u << (8 * (A & 3))) - 1u);
         cm = 0u;
         ex = kNoops;
         if (fl & 1u) {  // next-step auto-reset (build-defined): the level template

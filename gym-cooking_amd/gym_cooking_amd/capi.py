@@ -224,8 +224,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 
 class LevelError(RuntimeError):
     """OC_ELEVEL: the level is outside an entry point's envelope (oc_create's validation: more
-    than 1,024 cells, a 17th object or a 4th of one food; oc_reachability's export: a node
-    distance of 255 or more)."""
+    than 1,024 cells, a 17th object or a 4th of one food; the planner entry points: a
+    reachability graph with a BFS distance of 255 or more)."""
 
 
 def check(rc: int) -> None:

@@ -354,10 +354,10 @@ int oc_set_likelihood_form(oc_handle* h, int32_t form);
  *   node_of   : nullable u16 [W*H*5]: node id of (cell, approach), 0xFFFF = not a node
  *   dist      : nullable u8 [n][n]: nx.shortest_path_length between nodes, 0xFF = no path
  * World.get_lower_bound_between(_helper) (world.py:115-283) evaluates over exactly this table.
- * The planner kernels keep only the distances between Floor squares (an approach node is a leaf
- * one edge from its Floor, so every node distance is a Floor distance plus one per approach
- * node): any graph of a level of up to 1,024 cells.  Only this export refuses (OC_ELEVEL) a
- * graph with a node distance of 255 or more, which its u8 table cannot hold. */
+ * The planner kernels keep the distance table in LDS for a graph of at most 360 nodes, in device
+ * memory past that (a narrow level: every node its 255 cells can make; a wide one: up to 5,120).
+ * OC_ELEVEL (here and from the planner entry points) for a BFS distance of 255 or more, which the
+ * u8 table cannot hold. */
 int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, int64_t node_of_len, uint8_t* dist,
                     int64_t dist_len);
 

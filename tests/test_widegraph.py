@@ -1,11 +1,11 @@
-"""Kitchens whose reachability graph has more than 390 nodes, the limit the
-round-4 engine had on a narrow level (its all-pairs node distances in LDS):
+"""Kitchens whose reachability graph has more than the 360 nodes whose distance table a
+narrow level's planner kernels hold in LDS:
   * widegraph-24x24_salad: 576 cells (wide: u16 cell ids), a 605-node graph;
-  * dense-15x17_salad: 255 cells (narrow: byte cell ids), a 417-node graph (round 5).
-Since round 5 the planner tables keep only the distances between Floor squares (oc_rollout.h:
-an approach node is a leaf one edge from its Floor), in LDS on a narrow level and in device
-memory on a wide one.  Pinned on the CPU to the reference's own runs of the level files
-(tests/golden/gen_widegraph.py, gen_densegraph.py):
+  * dense-15x17_salad: 255 cells (narrow: byte cell ids), a 417-node graph (round 5; round 4
+    refused it with OC_ELEVEL).
+Their planner kernels stage the level's other tables in LDS and read the distance table from
+device memory (oc_rollout.h, RollLevel.dist_global).  Pinned on the CPU to the reference's own
+runs of the level files (tests/golden/gen_widegraph.py, gen_densegraph.py):
 
 * the parser and the engine's graph (node count, and the BFS distance of 400 random node pairs
   against the reference's nx.shortest_path_length);
@@ -74,7 +74,7 @@ def test_widegraph_level_matches_reference_graph(name):
     assert lv.tiles == ref["tiles"]
     assert sorted(str(s) for s in recipes.all_subtasks(lv)) == sorted(ref["all_subtasks"])
     n, node_of, dist = _graph(lv)
-    assert n == ref["graph_nodes"] > 390
+    assert n == ref["graph_nodes"] > 360
     checked = 0
     for (ux, uy), ud, (vx, vy), vd, d in ref["dist_pairs"]:
         u = int(node_of[(uy * lv.width + ux) * 5 + _NAV[tuple(ud)]])

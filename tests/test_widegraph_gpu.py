@@ -1,10 +1,9 @@
-"""The kitchens of tests/test_widegraph.py (more than 390 graph nodes: the 605-node wide
-kitchen and the 417-node narrow one) on the GPU, through the C-ABI: their planner kernels
-stage the level's tables in LDS and read the Floor distance table from LDS (narrow) or device
-memory (wide).  oc_step replays the reference's episodes; oc_subtask_bounds and oc_rollout
-against the reference's rows; rollout, bounds and likelihood rows against the oracle on random
-states; the navigation planner over oc_rollout decides as the same search over the oracle's
-rows."""
+"""The kitchens of tests/test_widegraph.py (more than 360 graph nodes: the 605-node wide
+kitchen and the 417-node narrow one) on the GPU, through the C-ABI: their planner kernels (the
+GD instantiation) stage the level's tables in LDS and read the distance table from device
+memory.  oc_step replays the reference's episodes; oc_subtask_bounds and oc_rollout against
+the reference's rows; rollout, bounds and likelihood rows against the oracle on random states;
+the navigation planner over oc_rollout decides as the same search over the oracle's rows."""
 import numpy as np
 import pytest
 

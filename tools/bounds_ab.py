@@ -50,6 +50,14 @@ def child(lib):
     flags = torch.empty(eb.pitch, dtype=torch.uint8, device=dev)
     rlb = torch.empty(eb.pitch, dtype=torch.float32, device=dev)
     ms_r = bench.time_launches(eb.rollout_launcher(s, out, a, table, alloc, flags, rlb), 200, dev)
+    # the planner's launch size: the first 4,096 rows (configuration-major)
+    eb4 = OvercookedBatch("full-divider_salad", A, 4096, max_T=100, device=dev)
+    NP = eb.layout.num_planes
+    s4 = s.view(NP, eb.pitch)[:, :4096].contiguous().view(-1)
+    a4 = a.view(A, eb.pitch)[:, :4096].contiguous().view(-1)
+    o4, f4 = eb4.new_state(), torch.empty(eb4.pitch, dtype=torch.uint8, device=dev)
+    l4 = torch.empty(eb4.pitch, dtype=torch.float32, device=dev)
+    ms_r4 = bench.time_launches(eb4.rollout_launcher(s4, o4, a4, table, alloc[:4096].contiguous(), f4, l4), 400, dev)
     v = torch.empty(eb.pitch, dtype=torch.float64, device=dev)
     f = torch.empty(eb.pitch, dtype=torch.uint8, device=dev)
     ms_l = bench.time_launches(eb.nav_likelihood_launcher(s, a, table, 0, 1.3, 0.5, alloc, v, f), 40, dev)
@@ -71,7 +79,8 @@ def child(lib):
     for t in (lb[:, :rows], ok[:, :rows], out, flags[:rows], rlb[:rows], v[:rows], f[:rows], vr[:rows], fr[:rows],
               v1[:rows], f1[:rows]):
         h.update(t.contiguous().cpu().numpy().tobytes())
-    print(json.dumps({"lib": os.path.basename(lib), "bounds_ms": ms_b, "rollout_ms": ms_r, "likelihood_ms": ms_l,
+    print(json.dumps({"lib": os.path.basename(lib), "bounds_ms": ms_b, "rollout_ms": ms_r, "rollout_4096_ms": ms_r4,
+                      "likelihood_ms": ms_l,
                       "likelihood_random_ms": ms_lr, "likelihood_single_ms": ms_l1, "lik_ok": int((f[:rows] == 1).sum()),
                       "doable": int(ok[:, :rows].sum()), "digest": h.hexdigest()[:16]}), flush=True)
 

@@ -31,8 +31,8 @@ constexpr int kMaxSteps = 100;
 
 __device__ __forceinline__ uint64_t now() { return wall_clock64(); }
 
-template <int A, int K, int MODE, bool LW, bool NOLOAD, bool STAMP>
-__global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void stepn_tl(LevelArgs L, const uint8_t* __restrict__ sin,
+template <int A, int K, int MODE, bool LW, bool NOLOAD, bool STAMP, int SW = 4, int LB = 5>
+__global__ __launch_bounds__(SW * 64 + (LW ? 64 : 0), LW ? LB : 1) void stepn_tl(LevelArgs L, const uint8_t* __restrict__ sin,
                                                                              uint8_t* __restrict__ sout,
                                                                              const uint8_t* __restrict__ actions,
                                                                              uint8_t* __restrict__ traj,
@@ -41,13 +41,14 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void stepn_tl(L
                                                                              uint64_t* __restrict__ tl) {
     constexpr int CP = kCPnt, LCP = 0;
     __shared__ uint32_t tbl4[64];
-    __shared__ uint32_t ring[LW ? 2 * kLwSteps * (kBlock / 64) * A * 64 : 1];
+    constexpr int kBS = SW * 64;  // stepping lanes per block
+    __shared__ uint32_t ring[LW ? 2 * kLwSteps * SW * A * 64 : 1];
     if (threadIdx.x < 64u) tbl4[threadIdx.x] = L.cls4[threadIdx.x];
     __syncthreads();
-    const bool loader = LW && threadIdx.x >= (uint32_t)kBlock;
+    const bool loader = LW && threadIdx.x >= (uint32_t)kBS;
     const uint32_t lane = threadIdx.x & 63u;
     const uint8_t* tbl = (const uint8_t*)tbl4;
-    const uint32_t P = (uint32_t)L.pitch, nlanes = P / kEPL, stride = gridDim.x * (uint32_t)kBlock;
+    const uint32_t P = (uint32_t)L.pitch, nlanes = P / kEPL, stride = gridDim.x * (uint32_t)kBS;
     constexpr int NP = 3 * A + 2 * K + 3;
     constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
     auto cls_of = [&](uint32_t cells) -> uint32_t {
@@ -63,19 +64,19 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void stepn_tl(L
     b.ex = make_rsrc(exec_out, (int64_t)n * A * P);
     b.coll = make_rsrc(coll_out, (int64_t)n * P);
     StepStats st;
-    const uint32_t gwave = (blockIdx.x * (uint32_t)kBlock + threadIdx.x) / 64u;  // stepping waves
+    const uint32_t gwave = (blockIdx.x * (uint32_t)kBS + threadIdx.x) / 64u;  // stepping waves
     const bool rec = STAMP && !loader && (gwave % kSample) == 0u && lane == 0u;
     uint64_t* out = tl + (uint64_t)(gwave / kSample) * (3 * kMaxSteps + 3);
     if (rec) out[0] = now();
     typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
-    for (uint32_t gb = blockIdx.x * (uint32_t)kBlock; gb < nlanes; gb += stride) {
+    for (uint32_t gb = blockIdx.x * (uint32_t)kBS; gb < nlanes; gb += stride) {
         if (loader) {
             auto fill = [&](int r0, int h) {
-                uint32_t w[kLwSteps][kBlock / 64][A];
+                uint32_t w[kLwSteps][SW][A];
 #pragma unroll
                 for (int q = 0; q < kLwSteps; ++q)
 #pragma unroll
-                    for (int v = 0; v < kBlock / 64; ++v)
+                    for (int v = 0; v < SW; ++v)
 #pragma unroll
                         for (int a = 0; a < A; ++a)
                             w[q][v][a] = r0 + q < n ? bld32<LCP>(b.act, (gb + 64u * v + lane) * 4u,
@@ -84,10 +85,10 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void stepn_tl(L
 #pragma unroll
                 for (int q = 0; q < kLwSteps; ++q)
 #pragma unroll
-                    for (int v = 0; v < kBlock / 64; ++v)
+                    for (int v = 0; v < SW; ++v)
 #pragma unroll
                         for (int a = 0; a < A; ++a)
-                            ring[(((h * kLwSteps + q) * (kBlock / 64) + v) * A + a) * 64 + lane] = w[q][v][a];
+                            ring[(((h * kLwSteps + q) * SW + v) * A + a) * 64 + lane] = w[q][v][a];
             };
             fill(0, 0);
             for (int r0 = 0; r0 < n; r0 += kLwSteps) {
@@ -98,6 +99,7 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void stepn_tl(L
             continue;
         }
         const uint32_t g = gb + threadIdx.x;
+        const bool live = g < nlanes;
         Chunk<A, K> c;
         load_chunk<A, K, false>(c, b, P, g);
         __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void stepn_tl(L
                 const int h = (r / kLwSteps) & 1;
 #pragma unroll
                 for (int a = 0; a < A; ++a)
-                    act[a] = ring[(((h * kLwSteps + q) * (kBlock / 64) + (threadIdx.x >> 6)) * A + a) * 64 + lane];
+                    act[a] = ring[(((h * kLwSteps + q) * SW + (threadIdx.x >> 6)) * A + a) * 64 + lane];
             }
             if (rec) {
                 __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the ring words have landed
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void stepn_tl(L
                 st.eps += __popc(ended);
             }
             if (rec) out[3 + 3 * r] = now();
-            const uint32_t base = (uint32_t)r * NP * P;
+            const uint32_t base = live ? (uint32_t)r * NP * P : 0x7FFFFFFFu;  // past num_records: dropped
 #pragma unroll
             for (int a = 0; a < A; ++a) {
                 bst32<CP>(tr, c.wx[a], vo, base + a * P);
@@ -156,11 +158,12 @@ __global__ __launch_bounds__(kBlock + (LW ? 64 : 0), LW ? 5 : 1) void stepn_tl(L
             __builtin_amdgcn_raw_buffer_store_b64(tw, tr, (int)(g * 8u), (int)(base + kPT * P), CP);
             bst32<CP>(tr, c.wf, vo, base + kPF * P);
 #pragma unroll
-            for (int a = 0; a < A; ++a) bst32<CP>(b.ex, ex[a], vo, (uint32_t)(r * A + a) * P);
-            bst32<CP>(b.coll, cm, vo, (uint32_t)r * P);
+            for (int a = 0; a < A; ++a) bst32<CP>(b.ex, ex[a], vo, live ? (uint32_t)(r * A + a) * P : 0x7FFFFFFFu);
+            bst32<CP>(b.coll, cm, vo, live ? (uint32_t)r * P : 0x7FFFFFFFu);
             if (rec) out[4 + 3 * r] = now();
         }
         if (LW) lds_barrier();
+        if (!live) continue;
 #pragma unroll
         for (int a = 0; a < A; ++a) {
             bst32<CP>(b.sout, c.wx[a], vo, a * P);
@@ -204,7 +207,7 @@ int main(int argc, char** argv) {
     const int64_t rec_words = 3 * kMaxSteps + 3;
     CK(hipMalloc(&s0, S)); CK(hipMalloc(&sout, S)); CK(hipMalloc(&acts, (int64_t)n * 3 * P));
     CK(hipMalloc(&traj, (int64_t)n * S)); CK(hipMalloc(&ex, (int64_t)n * 3 * P)); CK(hipMalloc(&coll, (int64_t)n * P));
-    CK(hipMalloc(&tl, nrec * rec_words * 8));
+    CK(hipMalloc(&tl, (nrec + 8) * rec_words * 8));
     // mid-run start state: 1,050 steps from a reset
     uint8_t* s1;
     CK(hipMalloc(&s1, S));
@@ -221,20 +224,21 @@ int main(int argc, char** argv) {
     const int64_t need = P / kEnvsPerBlock;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    auto launch = [&](auto kern, bool lw) {
-        const int64_t cap = (int64_t)h->cus * (lw ? 4 : 5);
-        hipLaunchKernelGGL(kern, dim3((unsigned)(need < cap ? need : cap)), dim3(kBlock + (lw ? 64 : 0)), 0, nullptr, L,
-                           s0, sout, acts, traj, ex, coll, n, tl);
+    auto launch = [&](auto kern, bool lw, int sw = 4, int per_cu = 0) {
+        const int64_t lanes_pb = 64 * sw, blocks = (nlanes + lanes_pb - 1) / lanes_pb;
+        const int64_t cap = (int64_t)h->cus * (per_cu ? per_cu : (lw ? 4 : 5));
+        hipLaunchKernelGGL(kern, dim3((unsigned)(blocks < cap ? blocks : cap)), dim3(64 * sw + (lw ? 64 : 0)), 0, nullptr,
+                           L, s0, sout, acts, traj, ex, coll, n, tl);
     };
-    auto time = [&](const char* name, auto kern, bool lw) {
-        for (int i = 0; i < 3; ++i) launch(kern, lw);
+    auto time = [&](const char* name, auto kern, bool lw, int sw = 4, int per_cu = 0) {
+        for (int i = 0; i < 3; ++i) launch(kern, lw, sw, per_cu);
         CK(hipEventRecord(e0));
-        for (int i = 0; i < 10; ++i) launch(kern, lw);
+        for (int i = 0; i < 10; ++i) launch(kern, lw, sw, per_cu);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
-        printf("%-34s %8.3f us/step  (%.1f us per 100-step launch)\n", name, ms * 1e3 / 10 / n, ms * 1e3 / 10);
+        printf("%-44s %8.3f us/step  (%.1f us per 100-step launch)\n", name, ms * 1e3 / 10 / n, ms * 1e3 / 10);
     };
     auto report = [&](const char* name) {
         std::vector<uint64_t> v(nrec * rec_words);
@@ -277,6 +281,13 @@ int main(int argc, char** argv) {
     time("lw (product form)", stepn_tl<3, 4, 0, true, false, false>, true);
     time("lw + stamps", stepn_tl<3, 4, 0, true, false, true>, true);
     report("lw");
+    CK(hipMemset(tl, 0, nrec * rec_words * 8));
+    time("lw, 3 stepping waves + loader per block", stepn_tl<3, 4, 0, true, false, false, 3, 5>, true, 3, 5);
+    time("lw3 + stamps", stepn_tl<3, 4, 0, true, false, true, 3, 5>, true, 3, 5);
+    report("lw3");
+    time("lw, launch bounds 6 waves per SIMD", stepn_tl<3, 4, 0, true, false, false, 4, 6>, true);
+    time("lw6 + stamps", stepn_tl<3, 4, 0, true, false, true, 4, 6>, true);
+    report("lw6");
     time("noload (no loads, no barrier)", stepn_tl<3, 4, 0, false, true, false>, false);
     time("noload + stamps", stepn_tl<3, 4, 0, false, true, true>, false);
     report("noload");

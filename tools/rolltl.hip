@@ -131,6 +131,79 @@ __global__ __launch_bounds__(kBlock) void roll_var(RollArgs R, const uint8_t* __
     }
 }
 
+// The product row (RowOps::run) split into its phases, a stamp after each (lane 0 of every wave
+// records; the drains make each phase's LDS reads land inside it)
+template <int A, int K>
+__global__ __launch_bounds__(kBlock) void roll_phases(RollArgs R, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
+                                                     const uint8_t* __restrict__ act, const uint8_t* __restrict__ alloc,
+                                                     const uint8_t* __restrict__ blob_g, uint8_t* __restrict__ out_flags,
+                                                     float* __restrict__ lb, uint64_t* __restrict__ tl) {
+    extern __shared__ uint32_t blob_w[];
+    __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
+    const int64_t P = R.pitch;
+    using PL = Planes<A, K, false>;
+    const int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    const bool live = e < R.B;
+    const int64_t ee = live ? e : 0;
+    ocro::RowT<K, false> r = load_row<A, K, false>(sin, P, ee);
+    const uint32_t t = ((const uint16_t*)(sin + PL::T * P))[ee], fl_in = sin[PL::F * P + ee];
+    const int ai = alloc[ee];
+    uint32_t aw = 0;
+#pragma unroll
+    for (int a = 0; a < A; ++a) aw |= (uint32_t)act[a * P + ee] << (8 * a);
+    stage_roll_tables(R, blob_g, blob_w, subs);
+    const uint8_t* blob = (const uint8_t*)blob_w;
+    uint64_t ts[7];
+    ts[0] = stamp(true);
+    float bound = 0.0f;
+    int f = OC_ROLL_BADALLOC;
+    if (ai < R.nsub) {
+        const ocro::Sub& s = subs[ai];
+        int c0 = (aw >> (8 * s.agent[0])) & 0xFF, c1 = s.n == 2 ? (aw >> (8 * s.agent[1])) & 0xFF : ocro::kNoop;
+        ocro::RowOps<A, K, false> ops(R.L, blob, blob + R.L.dist_off);
+        const ocro::RowT<K, false> r_in = r;
+        const bool raised = ops.level0(r, s);
+        ts[1] = stamp(true);
+        if (raised) {
+            r = r_in;
+            f = 8;
+            ts[2] = ts[3] = ts[4] = ts[5] = stamp(true);
+        } else {
+            if (s.kind == 0) c0 = c1 = ocro::kNoop;
+            c0 = c0 > ocro::kNoop ? ocro::kNoop : c0;
+            c1 = c1 > ocro::kNoop ? ocro::kNoop : c1;
+            int fl = ops.action_legal(r, s, c0, c1) ? 1 : 0;
+            ts[2] = stamp(true);
+            ops.interact(r, s.agent[0], c0);
+            if (s.n == 2) ops.interact(r, s.agent[1], c1);
+            ts[3] = stamp(true);
+            const bool asserted = s.n == 2 && ops.agent_cell(r, s.agent[0]) == ops.agent_cell(r, s.agent[1]);
+            if (asserted) fl |= 4;
+            else if (ops.is_goal(r, s)) fl |= 2;
+            ts[4] = stamp(true);
+            bound = ops.lower_bound(r, s);
+            ts[5] = stamp(true);
+            f = fl;
+        }
+    } else {
+        ts[1] = ts[2] = ts[3] = ts[4] = ts[5] = stamp(true);
+    }
+    if (live) {
+        store_row<A, K, false>(sout, P, e, r);
+        ((uint16_t*)(sout + PL::T * P))[e] = (uint16_t)t;
+        sout[PL::F * P + e] = (uint8_t)fl_in;
+        out_flags[e] = (uint8_t)f;
+        lb[e] = bound;
+    }
+    ts[6] = stamp(true);
+    if ((threadIdx.x & 63) == 0) {
+        const int64_t w = (blockIdx.x * (int64_t)kBlock + threadIdx.x) / 64;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) tl[w * 8 + k] = ts[k];
+        tl[w * 8 + 7] = (uint64_t)ai;
+    }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -300,6 +373,35 @@ int main(int argc, char** argv) {
         auto v_utl = VAR3(true, true, true);
         time("uni_tl", v_utl);
         timeline("uni");
+        {  // the row's phases, per wave; waves grouped by their first row's configuration kind
+            auto v_ph = [&](int v) {
+                hipLaunchKernelGGL((roll_phases<4, 4>), grid, dim3(kBlock), lds, nullptr, R, s0, out[v], acts, alloc,
+                                   h->roll_blob, fl[v], lbd[v], tl);
+            };
+            time("phases: the row's phases stamped", v_ph);
+            product(0); v_ph(1);
+            printf("  outputs %s\n", same() ? "identical" : "DIFFER");
+            std::vector<uint64_t> h_tl(nwaves * 8);
+            CK(hipMemcpy(h_tl.data(), tl, h_tl.size() * 8, hipMemcpyDeviceToHost));
+            const char* nm[6] = {"level0", "legal", "interact", "goal", "bound", "store"};
+            for (int grpk = 0; grpk < 4; ++grpk) {  // 0: Chop 1 agent, 1: Chop 2, 2: Merge 1, 3: Merge 2
+                printf("  phases, waves of %s %s agent(s), us (p50 / p90):", grpk < 2 ? "Chop" : "Merge", grpk % 2 ? "2" : "1");
+                for (int k = 1; k < 7; ++k) {
+                    std::vector<double> d;
+                    for (int64_t w = 0; w < nwaves; ++w) {
+                        const int ai = (int)h_tl[w * 8 + 7];
+                        if (ai >= (int)subs.size()) continue;
+                        const int kind = subs[ai].kind, na = subs[ai].num_agents;
+                        if (kind == 3 || (kind == 1) != (grpk < 2) || (na == 2) != (grpk % 2 == 1)) continue;
+                        d.push_back((h_tl[w * 8 + k] - h_tl[w * 8 + k - 1]) * 0.01);
+                    }
+                    if (d.empty()) continue;
+                    std::sort(d.begin(), d.end());
+                    printf("  %s %.2f/%.2f", nm[k - 1], d[d.size() / 2], d[d.size() * 9 / 10]);
+                }
+                printf("\n");
+            }
+        }
         if (B > 4096 && argc > 1) {  // every row of one configuration: the cost of each configuration's path
             std::vector<uint8_t> one(P, 0);
             for (int c = 0; c < (int)subs.size(); ++c) {
