@@ -1014,9 +1014,10 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
         const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
         ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+        const auto br = ops.template bound_row<true>(r);  // the row's agent nodes, slot sets: once for its configurations
         for (int i = i0; i < i1; ++i) {
             float v;
-            const bool ok = ops.full_bound(r, subs[i], v);
+            const bool ok = ops.full_bound(br, r, subs[i], v);
             lb[i * P + e] = v;
             doable[i * P + e] = ok ? 1 : 0;
         }

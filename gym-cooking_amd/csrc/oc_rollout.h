@@ -70,10 +70,12 @@ constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NA
 //   node_off   u16 [C * 5] graph node of (cell, approach), approach 4 = (0, 0)
 //   cut_off    Cutboard cells in scan order (L.ncut; u8 narrow, u16 wide)
 //   deliv_off  Delivery cells in scan order (L.ndeliv; u8 narrow, u16 wide)
+//   man_off    u16 [2][C] Manhattan distance from a cell to the nearest Cutboard (row 0) /
+//              Delivery (row 1) square (the two-agent static bound's B term; round 6)
 //   dmin_off   [2][nnodes] the distance from a node to the nearest Cutboard (row 0) / Delivery
 //              (row 1) approach node, 0xFF = none reachable
 //   dist_off   [nnodes][nnodes] BFS distances (last: a wide level stages the blob up to here)
-// A narrow level's first offsets are fixed: 0, 256, 768, 3328, 3584, then dmin at 3840.
+// A narrow level's first offsets are fixed: 0, 256, 768, 3328, 3584, 3840, then dmin at 4864.
 
 struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t W, H, perimeter, nnodes;
@@ -82,7 +84,9 @@ struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t dmin_off;  // blob offset of the nearest-Cutboard / nearest-Delivery distance rows
     int32_t tile_off, node_off, cut_off, deliv_off, dist_off;
     int32_t xy_off;    // u16 x | y << 8 per cell
-    int32_t wide;      // u16 cell ids (W * H > 255)
+    int32_t man_off;   // u16 [2][C]: Manhattan distance from a cell to the nearest Cutboard (row 0) /
+                       // Delivery (row 1) square
+    int32_t wide;     // u16 cell ids (W * H > 255)
     int32_t blob_bytes;  // the blob's size (a multiple of 4)
     int32_t lds_bytes;   // what the kernels stage in LDS: all of it, or up to dist_off (dist_global)
     int32_t dist_global; // the distance table is read from device memory: a wide level, or a narrow
@@ -208,7 +212,8 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
     L.node_off = 3 * C;
     L.cut_off = L.node_off + 2 * C * 5;
     L.deliv_off = L.cut_off + lb * C;
-    L.dmin_off = L.deliv_off + lb * C;
+    L.man_off = L.deliv_off + lb * C;
+    L.dmin_off = L.man_off + 2 * 2 * C;
     blob_v.assign((size_t)L.dmin_off, 0);  // grown below once the node count is known
     uint8_t* blob = blob_v.data();
     uint8_t* tile = blob + L.tile_off;
@@ -225,6 +230,22 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
     for (int i = 0; i < C * 5; ++i) node[i] = kNoNode;
     for (int c = 0; c < C; ++c)
         ((uint16_t*)(blob + L.xy_off))[c] = c < cells ? (uint16_t)((c % W) | ((c / W) << 8)) : (uint16_t)0;
+    // min over a static B side of manhattan(A, B) (world.py:215, 242-244: the two-agent bound's
+    // B term), per A cell; 0x7FFF where the side is empty (the bound returns before reading it)
+    for (int side = 0; side < 2; ++side) {
+        const int off = side == 0 ? L.cut_off : L.deliv_off, nb = side == 0 ? L.ncut : L.ndeliv;
+        uint16_t* man = (uint16_t*)(blob + L.man_off) + side * C;
+        for (int c = 0; c < C; ++c) {
+            int best = 0x7FFF;
+            for (int i = 0; c < cells && i < nb; ++i) {
+                const int b = L.wide ? ((const uint16_t*)(blob + off))[i] : blob[off + i];
+                const int dx = c % W - b % W, dy = c / W - b / W;
+                const int m = (dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy);
+                best = m < best ? m : best;
+            }
+            man[c] = (uint16_t)best;
+        }
+    }
     int n = 0;
     auto clampx = [&](int v) { return v < 0 ? 0 : (v > W - 1 ? W - 1 : v); };
     auto clampy = [&](int v) { return v < 0 ? 0 : (v > H - 1 ? H - 1 : v); };
@@ -532,7 +553,7 @@ struct RowOps {
     // matter: the result is a min.  (Per-lane trip counts of 1 or 4 per side left 0.56 of the
     // lanes active per VALU instruction in oc_bounds_kernel, with more SALU than VALU
     // instructions, profiles/r03/c5_static_b2/pmc_c5.json.)
-    OC_RH float helper(const Sub& s, int ag0, int ag1, int Ac, int Bc) const {
+    OC_RH float helper(const Sub& s, int u0, int u1, int Ac, int Bc) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
         const bool Acoll = tile(Ac) != kFloor, Bcoll = tile(Bc) != kFloor;
@@ -540,7 +561,6 @@ struct RowOps {
         const uint32_t pa = xy(Ac), pb = xy(Bc);
         const int dx = (int)(pa & 0xFFu) - (int)(pb & 0xFFu), dy = (int)(pa >> 8) - (int)(pb >> 8);
         const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
-        const int u0 = nid(ag0, 4);
         int vA[4], vB[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -562,34 +582,39 @@ struct RowOps {
             }
             return lower > 1.0f ? lower : 1.0f;
         }
-        const int u1 = nid(ag1, 4);
-        float b1B[4], b2B[4];
+        // Two agents.  Per pair (ia, ib) the reference takes mA = min(b1A, b2A), mB = min(b1B,
+        // b2B), doubles both when one agent is nearest on both sides (a tie counts for both), and
+        // bounds max(mA, mB) + (man - 1) / 2.  Round 6 takes the min over the 16 pairs by side:
+        // each approach is of type 0 (agent 1 strictly nearer), 1 (agent 2 strictly nearer) or 2
+        // (a tie), and over a product of two approach sets min max(mA, mB) = max(min mA, min
+        // mB); so the min is over six type combinations of the per-type minima, doubled unless
+        // the types are (0, 1) or (1, 0).  Integers (distances, or the perimeter for an
+        // unreachable node) until the last add: the same value as the pair loop, exactly.
+        constexpr int kInf = 0x3FFFFFFF;
+        int MA[3] = {kInf, kInf, kInf}, MB[3] = {kInf, kInf, kInf};
+        auto side = [&](const int (&v)[4], int n, int (&M)[3]) OC_RL {
 #pragma unroll
-        for (int ib = 0; ib < 4; ++ib) {
-            int t;
-            b1B[ib] = b2B[ib] = per;
-            if (ib >= nB) continue;
-            b1B[ib] = (t = dn(u0, vB[ib])) < 0 ? per : (float)t;
-            b2B[ib] = (t = dn(u1, vB[ib])) < 0 ? per : (float)t;
-        }
-#pragma unroll
-        for (int ia = 0; ia < 4; ++ia) {
-            if (ia >= nA) continue;
-            int t;
-            const float b1A = (t = dn(u0, vA[ia])) < 0 ? per : (float)t;
-            const float b2A = (t = dn(u1, vA[ia])) < 0 ? per : (float)t;
-#pragma unroll
-            for (int ib = 0; ib < 4; ++ib) {
-                if (ib >= nB) continue;
-                float mA = b1A < b2A ? b1A : b2A, mB = b1B[ib] < b2B[ib] ? b1B[ib] : b2B[ib];
-                if ((b1A == mA && b1B[ib] == mB) || (b2A == mA && b2B[ib] == mB)) {
-                    mA *= 2.0f;
-                    mB *= 2.0f;
-                }
-                const float bound = (mA > mB ? mA : mB) + (man - 1.0f) * 0.5f;
-                lower = bound < lower ? bound : lower;
+            for (int q = 0; q < 4; ++q) {
+                if (q >= n) continue;  // wave-uniform
+                int t;
+                const int b1 = (t = dn(u0, v[q])) < 0 ? L.perimeter : t;
+                const int b2 = (t = dn(u1, v[q])) < 0 ? L.perimeter : t;
+                const int m = b1 < b2 ? b1 : b2;
+                M[0] = b1 < b2 && m < M[0] ? m : M[0];
+                M[1] = b2 < b1 && m < M[1] ? m : M[1];
+                M[2] = b1 == b2 && m < M[2] ? m : M[2];
             }
-        }
+        };
+        side(vA, nA, MA);
+        side(vB, nB, MB);
+        auto mx = [](int x, int y) OC_RL { return x > y ? x : y; };
+        auto mn = [](int x, int y) OC_RL { return x < y ? x : y; };
+        const int single = mn(mx(MA[0], MB[1]), mx(MA[1], MB[0]));
+        const int dbl = mn(mn(mx(MA[0], MB[0]), mx(MA[1], MB[1])),
+                           mn(mx(MA[2], mn(mn(MB[0], MB[1]), MB[2])), mx(mn(mn(MA[0], MA[1]), MA[2]), MB[2])));
+        const int best = mn(single, 2 * dbl);
+        const float bound = (float)best + (man - 1.0f) * 0.5f;
+        lower = bound < lower ? bound : lower;
         return lower > 1.0f ? lower : 1.0f;
     }
 
@@ -602,14 +627,13 @@ struct RowOps {
     //    approach node.
     // helper() clamps each pair's result to >= 1 and starts from perimeter + 1; both are
     // monotone, so the min over B of helper() is this with the same clamp.  Exact in fp32.
-    OC_RH float helper_static(const Sub& s, int ag0, int ag1, int Ac, int bl_off, int nb,
-                              const uint8_t* dm) const {
+    OC_RH float helper_static(const Sub& s, int u0, int u1, int Ac, int nb, const uint8_t* dm,
+                              const uint16_t* man_t) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
         if (nb == 0) return lower;
         const bool Acoll = tile(Ac) != kFloor;
         const int nA = wave_any(Acoll) ? 4 : 1;  // wave-uniform (a Floor A repeats its node)
-        const int u0 = nid(ag0, 4);
         if (s.n == 1) {
 #pragma unroll
             for (int ia = 0; ia < 4; ++ia) {
@@ -620,16 +644,7 @@ struct RowOps {
                 lower = vA != kNoNode && a1 >= 0 && m != kNone && bound < lower ? bound : lower;
             }
         } else {
-            const uint32_t pa = xy(Ac);
-            const int u1 = nid(ag1, 4), ax = (int)(pa & 0xFFu), ay = (int)(pa >> 8);
-            int man = 0x7FFF;
-            for (int i = 0; i < nb; ++i) {
-                const int b = list_cell(bl_off, i);
-                const uint32_t pb = xy(b);
-                const int dx = ax - (int)(pb & 0xFFu), dy = ay - (int)(pb >> 8);
-                const int m = (dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy);
-                man = m < man ? m : man;
-            }
+            const int man = man_t[Ac];  // min over the side's squares (the level's table)
             float mA = per;
 #pragma unroll
             for (int ia = 0; ia < 4; ++ia) {
@@ -647,67 +662,107 @@ struct RowOps {
         return lower > 1.0f ? lower : 1.0f;
     }
 
+    // The row's facts that every configuration's bound reads, gathered once per row (round 6:
+    // oc_bounds_kernel evaluates up to 64 configurations on one row, and each one re-derived
+    // them; the rollout and likelihood rows build it once per bound).
+    struct BoundRow {
+        AcT cells = 0;         // agent a's cell: byte a (narrow), u16 field a (wide)
+        uint32_t nodes[2] = {0u, 0u};  // HOIST: agent a's graph node (approach 4), u16 field a % 2 of word a / 2
+        uint32_t held = 0;     // agent a's held item's mask in byte a (0 where a holds nothing)
+        uint32_t avail = 0;    // bit k < K: slot k is live and held by no agent; bit K + a: agent a holds one
+        uint32_t deliv = 0;    // HOIST: bit k < K: slot k lies on a Delivery square; bit K + a: agent a
+                               // stands on one
+    };
+    // HOIST (oc_bounds_kernel): the agents' graph nodes and the Delivery bits too, read once for
+    // all configurations; a single bound (rollout, likelihood) reads the ones it needs.
+    template <bool HOIST>
+    OC_RH BoundRow bound_row(const Row& r) const {
+        BoundRow b;
+        uint32_t heldslots = 0;
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            const int c = agent_cell(r, a), h = r.ah(a);
+            if constexpr (WIDE) b.cells |= (AcT)c << (16 * a);
+            else b.cells |= (AcT)c << (8 * a);
+            if (HOIST) b.nodes[a >> 1] |= (uint32_t)nid(c, 4) << (16 * (a & 1));
+            if (h != kNone) {
+                heldslots |= 1u << (h & 31);
+                b.held |= (uint32_t)r.im(h) << (8 * a);
+                b.avail |= 1u << (K + a);
+            }
+            if (HOIST) b.deliv |= static_tile(c) == kDelivery ? 1u << (K + a) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int c = r.il(k);
+            b.avail |= c != kDead && !((heldslots >> k) & 1u) ? 1u << k : 0u;
+            if (HOIST) b.deliv |= c != kDead && static_tile(c) == kDelivery ? 1u << k : 0u;
+        }
+        return b;
+    }
+    OC_RH int brow_cell(const BoundRow& b, int a) const {
+        if constexpr (WIDE) return (int)((b.cells >> (16 * a)) & 0xFFFFu);
+        else return (int)((b.cells >> (8 * a)) & 0xFFu);
+    }
+
     // Locations of `m` as get_AB_locs_given_objs lists them, as a set of sources: bit k < K an
     // un-held item in slot k, bit K + a a subtask agent a holding one; `skip_deliv` drops
     // Delivery squares (Deliver's A_locs).  Built branch-free over every source, so the lanes
     // of a wave only part ways in the walk over the set bits (usually 0 or 1 per side).
-    OC_RH uint32_t obj_set(const Row& r, int m, bool skip_deliv) const {
-        uint32_t held = 0;
-#pragma unroll
-        for (int a = 0; a < A; ++a) {
-            const int h = r.ah(a);
-            held |= h != kNone ? 1u << (h & 31) : 0u;
-        }
+    template <bool HOIST>
+    OC_RH uint32_t obj_set(const BoundRow& b, const Row& r, int m, bool skip_deliv) const {
         uint32_t set = 0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int c = r.il(k);
-            const bool ok = c != kDead && r.im(k) == m && !((held >> k) & 1u) &&
-                            !(skip_deliv && static_tile(c == kDead ? 0 : c) == kDelivery);
-            set |= ok ? 1u << k : 0u;
-        }
+        for (int k = 0; k < K; ++k) set |= r.im(k) == m ? 1u << k : 0u;
 #pragma unroll
-        for (int a = 0; a < A; ++a) {
-            const int h = r.ah(a);
-            const bool ok = ((active >> a) & 1u) && h != kNone && r.im(h) == m &&
-                            !(skip_deliv && static_tile(agent_cell(r, a)) == kDelivery);
-            set |= ok ? 1u << (K + a) : 0u;
-        }
-        return set;
+        for (int a = 0; a < A; ++a) set |= ((b.held >> (8 * a)) & 0xFFu) == (uint32_t)m ? 1u << (K + a) : 0u;
+        set &= b.avail & (((1u << K) - 1u) | (active << K));
+        if (HOIST || !skip_deliv) return skip_deliv ? set & ~b.deliv : set;
+        uint32_t dl = 0;  // the members' squares only
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            dl |= ((set >> k) & 1u) && static_tile(r.il(k) == kDead ? 0 : r.il(k)) == kDelivery ? 1u << k : 0u;
+#pragma unroll
+        for (int a = 0; a < A; ++a)
+            dl |= ((set >> (K + a)) & 1u) && static_tile(brow_cell(b, a)) == kDelivery ? 1u << (K + a) : 0u;
+        return set & ~dl;
     }
-    OC_RH int src_cell(const Row& r, int k) const { return k < K ? r.il(k) : agent_cell(r, k - K); }
+    OC_RH int src_cell(const BoundRow& b, const Row& r, int k) const { return k < K ? r.il(k) : brow_cell(b, k - K); }
 
     // f(cell) for every location of obj_set (slot order, then agents); one rolled loop with one
     // call site: f (a bound walk) is inlined once, not K + A times
-    template <class F>
-    OC_RH void visit_objs(const Row& r, int m, bool skip_deliv, F&& f) const {
+    template <bool HOIST, class F>
+    OC_RH void visit_objs(const BoundRow& b, const Row& r, int m, bool skip_deliv, F&& f) const {
 #pragma unroll 1
-        for (uint32_t set = obj_set(r, m, skip_deliv); set != 0u; set &= set - 1u) f(src_cell(r, __builtin_ctz(set)));
+        for (uint32_t set = obj_set<HOIST>(b, r, m, skip_deliv); set != 0u; set &= set - 1u) f(src_cell(b, r, __builtin_ctz(set)));
     }
 
     // get_lower_bound_for_subtask_given_objs (overcooked_environment.py:594-664)
     OC_RH float lower_bound(const Row& r, const Sub& s) const {
         float pen;
-        const float d = lower_bound_parts(r, s, pen);
+        const float d = lower_bound_parts<false>(bound_row<false>(r), r, s, pen);
         return d + pen;
     }
 
     // The same, split: returns World.get_lower_bound_between's distance (world.py:115-146) and
     // sets `pen` to the holding penalty (overcooked_environment.py:611-640).
-    // Its head: the subtask agents' cells (ag0 the first active agent's, ag1 the second's) and
-    // the holding penalty.
-    OC_RH void bound_agents(const Row& r, const Sub& s, int& ag0, int& ag1, float& pen) const {
+    // Its head: the subtask agents' graph nodes (u0 the first active agent's, u1 the second's)
+    // and the holding penalty.
+    template <bool HOIST>
+    OC_RH void bound_agents(const BoundRow& b, const Sub& s, int& u0, int& u1, float& pen) const {
         pen = 0.0f;
-        ag0 = ag1 = 0;
-        int na = 0;
+        int ag0 = 0, ag1 = 0, na = 0;
 #pragma unroll
         for (int a = 0; a < A; ++a) {
             if (!((active >> a) & 1u)) continue;
-            if (na == 0) ag0 = agent_cell(r, a); else ag1 = agent_cell(r, a);
+            const int v = HOIST ? (int)((b.nodes[a >> 1] >> (16 * (a & 1))) & 0xFFFFu) : brow_cell(b, a);
+            if (na == 0) ag0 = v; else ag1 = v;
             ++na;
-            const int h = r.ah(a);
-            if (h != kNone && s.kind != 2 && r.im(h) != s.start[0] && r.im(h) != s.goal) pen = 1.0f;
+            const int hm = (int)((b.held >> (8 * a)) & 0xFFu);
+            if (((b.avail >> (K + a)) & 1u) && s.kind != 2 && hm != s.start[0] && hm != s.goal) pen = 1.0f;
         }
+        u0 = HOIST ? ag0 : nid(ag0, 4);
+        u1 = HOIST || s.n != 2 ? ag1 : nid(ag1, 4);  // read by the two-agent bounds only
     }
     // full_bound's configuration of this object: no Level-0 view, the subtask agents active
     OC_RH void bound_config(const Sub& s) {
@@ -717,22 +772,24 @@ struct RowOps {
         blockers = active;
     }
 
-    OC_RH float lower_bound_parts(const Row& r, const Sub& s, float& pen) const {
-        int ag0, ag1;
-        bound_agents(r, s, ag0, ag1, pen);
+    template <bool HOIST>
+    OC_RH float lower_bound_parts(const BoundRow& br, const Row& r, const Sub& s, float& pen) const {
+        int u0, u1;
+        bound_agents<HOIST>(br, s, u0, u1, pen);
         float lower = (float)L.perimeter + 1.0f;
         if (s.kind == 1 || s.kind == 3) {  // static B side: one table lookup per A approach
-            const int bl = s.kind == 1 ? L.cut_off : L.deliv_off;
             const int nb = s.kind == 1 ? L.ncut : L.ndeliv;
             const uint8_t* dm = T + L.dmin_off + (s.kind == 1 ? 0 : L.nnodes);
-            visit_objs(r, s.start[0], s.kind == 3, [&](int Ac) OC_RL {
-                const float b = helper_static(s, ag0, ag1, Ac, bl, nb, dm);
+            const int C = L.wide ? (L.W * L.H + 3) & ~3 : 256;
+            const uint16_t* man_t = (const uint16_t*)(T + L.man_off) + (s.kind == 1 ? 0 : C);
+            visit_objs<HOIST>(br, r, s.start[0], s.kind == 3, [&](int Ac) OC_RL {
+                const float b = helper_static(s, u0, u1, Ac, nb, dm, man_t);
                 if (b < lower) lower = b;
             });
         } else if (s.kind == 2) {
-            visit_objs(r, s.start[0], false, [&](int Ac) OC_RL {
-                visit_objs(r, s.start[1], false, [&](int Bc) OC_RL {
-                    const float b = helper(s, ag0, ag1, Ac, Bc);
+            visit_objs<HOIST>(br, r, s.start[0], false, [&](int Ac) OC_RL {
+                visit_objs<HOIST>(br, r, s.start[1], false, [&](int Bc) OC_RL {
+                    const float b = helper(s, u0, u1, Ac, Bc);
                     if (b < lower) lower = b;
                 });
             });
@@ -742,14 +799,16 @@ struct RowOps {
 
     // oc_subtask_bounds on a full state (no Level-0 view): lb = get_lower_bound_for_subtask_
     // given_objs; returns BayesianDelegator.subtask_alloc_is_doable (bayesian_delegator.py:98-156):
-    // None -> true, else the distance < world.perimeter.
-    OC_RH bool full_bound(const Row& r, const Sub& s, float& lb) {
+    // None -> true, else the distance < world.perimeter.  `br` = bound_row<true>(r), built once
+    // for all of the row's configurations.
+    OC_RH bool full_bound(const BoundRow& br, const Row& r, const Sub& s, float& lb) {
         bound_config(s);
         float pen;
-        const float d = lower_bound_parts(r, s, pen);
+        const float d = lower_bound_parts<true>(br, r, s, pen);
         lb = d + pen;
         return s.kind == 0 || d < (float)L.perimeter;
     }
+    OC_RH bool full_bound(const Row& r, const Sub& s, float& lb) { return full_bound(bound_row<true>(r), r, s, lb); }
 
     // The whole row: returns OC_ROLL_* flags; r becomes the Level-0 next state (unchanged when
     // the configuration raises).

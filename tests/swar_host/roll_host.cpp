@@ -141,12 +141,13 @@ static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask
     for (int64_t e = 0; e < B; ++e) {
         const ocro::RowT<K, W> r = load<A, K, W>(sin, P, e);
         ocro::RowOps<A, K, W> ops(L, blob);
+        const auto br = ops.template bound_row<true>(r);  // as the kernel: once per row
         for (int i = 0; i < nsub; ++i) {
             const oc_subtask& o = subs[i];
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
                         {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
             float v;
-            doable[i * P + e] = ops.full_bound(r, s, v) ? 1 : 0;
+            doable[i * P + e] = ops.full_bound(br, r, s, v) ? 1 : 0;
             lb[i * P + e] = v;
         }
     }
