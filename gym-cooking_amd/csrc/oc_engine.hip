@@ -561,7 +561,10 @@ struct RollArgs {
 // Stage the level's table blob and the subtask configurations in LDS.
 __device__ __forceinline__ void stage_roll_tables(const RollArgs& R, const uint8_t* blob_g, uint32_t* blob_w,
                                                   ocro::Sub* subs) {
-    for (int i = threadIdx.x; i < R.blob_words; i += kBlock) blob_w[i] = ((const uint32_t*)blob_g)[i];
+    // 16-byte loads (a quarter of the load instructions; round 6), then the last < 4 words
+    const int n16 = R.blob_words >> 2;
+    for (int i = threadIdx.x; i < n16; i += kBlock) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
+    for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += kBlock) blob_w[i] = ((const uint32_t*)blob_g)[i];
     constexpr int kSubWords = (int)(sizeof(ocro::Sub) / 4);
     for (int i = threadIdx.x; i < R.nsub * kSubWords; i += kBlock)
         ((uint32_t*)subs)[i] = ((const uint32_t*)R.subs)[i];
@@ -624,22 +627,47 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
                                                             const uint8_t* __restrict__ blob_g,
                                                             uint8_t* __restrict__ out_flags,
                                                             float* __restrict__ lb) {
-    extern __shared__ uint32_t blob_w[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
-    stage_roll_tables(R, blob_g, blob_w, subs);
-    const uint8_t* blob = (const uint8_t*)blob_w;
     const int64_t P = R.pitch;
     using PL = Planes<A, K, W>;
-    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
-        ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
-        const uint16_t t = ((const uint16_t*)(sin + PL::T * P))[e];
-        const uint8_t fl_in = sin[PL::F * P + e];
-        const int ai = alloc != nullptr ? alloc[e] : 0;
+    // A lane's row: its state, t, flags, allocation id and every agent's action (the subtask's
+    // agents are known only once the configuration table is in LDS).  The first row's loads are
+    // issued before the table staging, so their latency overlaps it (round 6).
+    struct In {
+        ocro::RowT<K, W> r;
+        uint16_t t;
+        uint8_t fl;
+        int ai;
+        uint32_t acts;  // agent a's action in byte a
+    };
+    auto load_in = [&](int64_t e) {
+        In v;
+        v.r = load_row<A, K, W>(sin, P, e);
+        v.t = ((const uint16_t*)(sin + PL::T * P))[e];
+        v.fl = sin[PL::F * P + e];
+        v.ai = alloc != nullptr ? alloc[e] : 0;
+        v.acts = 0u;
+#pragma unroll
+        for (int a = 0; a < A; ++a) v.acts |= (uint32_t)act[a * P + e] << (8 * a);
+        return v;
+    };
+    int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    In in;
+    if (e < R.B) in = load_in(e);
+    stage_roll_tables(R, blob_g, blob_w, subs);
+    const uint8_t* blob = (const uint8_t*)blob_w;
+    for (bool first = true; e < R.B; e += (int64_t)gridDim.x * kBlock, first = false) {
+        if (!first) in = load_in(e);
+        ocro::RowT<K, W> r = in.r;
+        const uint16_t t = in.t;
+        const uint8_t fl_in = in.fl;
+        const int ai = in.ai;
         float bound = 0.0f;
         int f = OC_ROLL_BADALLOC;  // an alloc id past num_subtasks: the row is copied unchanged
         if (ai < R.nsub) {
             const ocro::Sub& s = subs[ai];
-            const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
+            const int c0 = (in.acts >> (8 * s.agent[0])) & 0xFFu, c1 = s.n == 2 ? (in.acts >> (8 * s.agent[1])) & 0xFFu : ocro::kNoop;
             ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             f = ops.run(r, s, c0, c1, bound);
         }
@@ -675,7 +703,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
                                                                const uint8_t* __restrict__ blob_g, int self_agent,
                                                                double beta, double nap, double* __restrict__ out,
                                                                uint8_t* __restrict__ out_flags) {
-    extern __shared__ uint32_t blob_w[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
     stage_roll_tables(R, blob_g, blob_w, subs);
     const uint8_t* blob = (const uint8_t*)blob_w;
@@ -693,7 +721,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
             uint32_t taken = 0;
 #pragma unroll
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
-            ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+            ocro::RowOps<A, K, W, true> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             if (s.kind == 0) {
                 f = 0;
                 if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
@@ -839,7 +867,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
     constexpr int kNB = kNR / kRPB;             // batches per round
     constexpr int kWaves = kBlock / 64;
     constexpr uint32_t kNotPending = 0xFFFFu;
-    extern __shared__ uint32_t blob_w[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
     __shared__ double lq[kWaves][kNR][kCand];     // Q(s, k)
     __shared__ uint32_t lok[kWaves][kNR];         // bit k: candidate k's rollout did not raise
@@ -874,7 +902,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
                     uint32_t taken = 0;
 #pragma unroll
                     for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
-                    ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
+                    ocro::RowOps<A, K, W, true> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
                     if (s.kind == 0) {
                         f = 0;
                         if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
@@ -932,7 +960,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
                 const int ai = alloc != nullptr ? alloc[e] : 0;
                 const ocro::Sub& s = subs[ai];
                 ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
-                ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
+                ocro::RowOps<A, K, W, true> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
                 ops.level0(r, s);
                 const bool joint = s.n == 2;
                 const int a0 = joint ? k / 5 : k, c1 = joint ? k % 5 : ocro::kNoop;
@@ -1005,7 +1033,7 @@ template <int A, int K, bool W, bool GD>
 __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                            const uint8_t* __restrict__ blob_g,
                                                            float* __restrict__ lb, uint8_t* __restrict__ doable) {
-    extern __shared__ uint32_t blob_w[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t blob_w[];
     __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
     stage_roll_tables(R, blob_g, blob_w, subs);
     const uint8_t* blob = (const uint8_t*)blob_w;

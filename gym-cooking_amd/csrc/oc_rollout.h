@@ -342,7 +342,10 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
 }
 
 // ---- row logic ----------------------------------------------------------------------------
-template <int A, int K, bool WIDE = false>
+// LEAN (the likelihood kernels, whose compacted form sits at 122 of the 128 VGPRs that keep 4
+// waves per SIMD): the bound walk reads a square's tile before its approach nodes, as before
+// round 6, instead of all five node reads at once (which keeps more values live).
+template <int A, int K, bool WIDE = false, bool LEAN = false>
 struct RowOps {
     using Row = RowT<K, WIDE>;
     using AcT = typename ConditionalT<WIDE, uint64_t, uint32_t>::type;
@@ -433,13 +436,33 @@ struct RowOps {
     OC_RH int merged(int a, int b) const { return L.enc ? a + b : a | b; }        // Object.merge
     OC_RH int chopped(int m) const { return L.enc ? m & 0x7F : m | ((m << 4) & 0x70); }  // Object.chop
 
+    // The square agent a's action points at, clamped to the grid (interact's and get_single_
+    // actions' World.inbounds), and its tile in the Level-0 view.  single_legal and interact
+    // read the same square (interact moves no other agent and the AgentCounters are fixed), so
+    // a row reads each subtask agent's tile once, all agents' reads together (round 6).
+    struct Target {
+        int x, y, c, t;
+    };
+    OC_RH Target target(const Row& r, int a, int code) const {
+        Target g;
+        const int k = code > kNoop ? kNoop : code;
+        g.x = r.ax(a) + kDX[k];
+        g.y = r.ay(a) + kDY[k];
+        g.x = g.x < 0 ? 0 : (g.x > L.W - 1 ? L.W - 1 : g.x);
+        g.y = g.y < 0 ? 0 : (g.y > L.H - 1 ? L.H - 1 : g.y);
+        g.c = cell(g.x, g.y);
+        g.t = tile(g.c);
+        return g;
+    }
+
     // interact(agent, world), play = False (utils/interact.py:4-89)
     OC_RH void interact(Row& r, int a, int code) const {
+        if (code == kNoop) return;  // before the target's read, as the reference returns first
+        interact(r, a, code, target(r, a, code));
+    }
+    OC_RH void interact(Row& r, int a, int code, const Target& g) const {
         if (code == kNoop) return;
-        int tx = r.ax(a) + kDX[code], ty = r.ay(a) + kDY[code];
-        tx = tx < 0 ? 0 : (tx > L.W - 1 ? L.W - 1 : tx);
-        ty = ty < 0 ? 0 : (ty > L.H - 1 ? L.H - 1 : ty);
-        const int tc = cell(tx, ty), t = tile(tc), h = r.ah(a);
+        const int tx = g.x, ty = g.y, tc = g.c, t = g.t, h = r.ah(a);
         if (t == kFloor) {  // move_to: the held item follows
             Row::s32(r.x, a, (uint32_t)tx);
             Row::s32(r.y, a, (uint32_t)ty);
@@ -488,13 +511,15 @@ struct RowOps {
     // nav_utils.get_single_actions membership
     OC_RH bool single_legal(const Row& r, int a, int code) const {
         if (code == kNoop) return true;
-        int nx = r.ax(a) + kDX[code], ny = r.ay(a) + kDY[code];
-        nx = nx < 0 ? 0 : (nx > L.W - 1 ? L.W - 1 : nx);
-        ny = ny < 0 ? 0 : (ny > L.H - 1 ? L.H - 1 : ny);
+        return single_legal(r, a, code, target(r, a, code));
+    }
+    OC_RH bool single_legal(const Row& r, int a, int code, const Target& g) const {
+        if (code == kNoop) return true;
+        const int nx = g.x, ny = g.y;
 #pragma unroll
         for (int b = 0; b < A; ++b)
             if (((blockers >> b) & 1u) && r.ax(b) == nx && r.ay(b) == ny) return false;
-        const int c = cell(nx, ny), t = tile(c);
+        const int c = g.c, t = g.t;
         if (t == kFloor || t == kDelivery) return true;
         const int o = item_at(r, c);
         const int h = r.ah(a);
@@ -502,11 +527,34 @@ struct RowOps {
         return h == kNone || mergeable(r.im(h), r.im(o));
     }
 
+    // The same test without branches (the rollout row: the blocker scan, the square's class and
+    // its item are all evaluated and combined with selects)
+    OC_RH bool single_legal_flat(const Row& r, int a, int code, const Target& g) const {
+        uint32_t on = 0;  // agents on the target square
+#pragma unroll
+        for (int b = 0; b < A; ++b) on |= r.ax(b) == g.x && r.ay(b) == g.y ? 1u << b : 0u;
+        const int o = item_at(r, g.c), h = r.ah(a);
+        const int hm = r.im(h == kNone ? 0 : h), om = r.im(o < 0 ? 0 : o);
+        const bool open = g.t == kFloor || g.t == kDelivery;
+        const bool item_ok = o < 0 ? h != kNone : (h == kNone || mergeable(hm, om));
+        return code == kNoop || ((on & blockers) == 0u && (open || item_ok));
+    }
+
+    // The short-cut form (the likelihood kernels: fewer registers live across the checks)
     OC_RH bool action_legal(const Row& r, const Sub& s, int c0, int c1) const {
         if (s.kind == 0) return c0 == kNoop && (s.n < 2 || c1 == kNoop);
         if (!single_legal(r, s.agent[0], c0)) return false;
         if (s.n < 2) return true;
         return single_legal(r, s.agent[1], c1) && no_collision(r, s.agent[0], s.agent[1], c0, c1);
+    }
+    // The rollout row's form: g0, g1 the subtask agents' targets (g1 unused with one agent),
+    // read once for the legality and interact; the checks are all evaluated (no short cut), so
+    // their table reads issue together
+    OC_RH bool action_legal(const Row& r, const Sub& s, int c0, int c1, const Target& g0, const Target& g1) const {
+        if (s.kind == 0) return c0 == kNoop && (s.n < 2 || c1 == kNoop);
+        const bool l0 = single_legal_flat(r, s.agent[0], c0, g0);
+        if (s.n < 2) return l0;
+        return ((int)l0 & (int)single_legal_flat(r, s.agent[1], c1, g1) & (int)no_collision(r, s.agent[0], s.agent[1], c0, c1)) != 0;
     }
 
     OC_RH bool is_goal(const Row& r, const Sub& s) const {
@@ -541,6 +589,28 @@ struct RowOps {
         return none || d == kNone ? -1 : d;
     }
 
+    // A square's graph nodes as the bound walks them: its four approach nodes when it is
+    // collidable in the Level-0 view, else its own node (approach 4) four times; returns the
+    // collidability.  A square is statically collidable exactly when it has no approach-4 node
+    // (only Floor squares get one, world.py:67-108), so the five node reads issue together and
+    // no tile read comes first (round 6).
+    OC_RH bool approaches(int c, int (&v)[4]) const {
+        if constexpr (LEAN) {
+            const bool coll = tile(c) != kFloor;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = nid(c, coll ? q : 4);
+            return coll;
+        }
+        const int n4 = nid(c, 4);
+        const bool coll = n4 == kNoNode || is_ac(c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int nq = nid(c, q);
+            v[q] = coll ? nq : n4;
+        }
+        return coll;
+    }
+
     // World.get_lower_bound_between_helper (world.py:148-264) with check_bound (:266-283).  The
     // agents' node ids are looked up once, the A-side distances once per A approach and (two
     // agents) the B-side distances once per B approach, out of the pair loop; the arithmetic
@@ -556,17 +626,12 @@ struct RowOps {
     OC_RH float helper(const Sub& s, int u0, int u1, int Ac, int Bc) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
-        const bool Acoll = tile(Ac) != kFloor, Bcoll = tile(Bc) != kFloor;
+        int vA[4], vB[4];
+        const bool Acoll = approaches(Ac, vA), Bcoll = approaches(Bc, vB);
         const int nA = wave_any(Acoll) ? 4 : 1, nB = wave_any(Bcoll) ? 4 : 1;
         const uint32_t pa = xy(Ac), pb = xy(Bc);
         const int dx = (int)(pa & 0xFFu) - (int)(pb & 0xFFu), dy = (int)(pa >> 8) - (int)(pb >> 8);
         const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
-        int vA[4], vB[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            vA[q] = nid(Ac, Acoll ? q : 4);
-            vB[q] = nid(Bc, Bcoll ? q : 4);
-        }
         if (s.n == 1) {
 #pragma unroll
             for (int ia = 0; ia < 4; ++ia) {
@@ -632,13 +697,14 @@ struct RowOps {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
         if (nb == 0) return lower;
-        const bool Acoll = tile(Ac) != kFloor;
+        int vAs[4];
+        const bool Acoll = approaches(Ac, vAs);
         const int nA = wave_any(Acoll) ? 4 : 1;  // wave-uniform (a Floor A repeats its node)
         if (s.n == 1) {
 #pragma unroll
             for (int ia = 0; ia < 4; ++ia) {
                 if (ia >= nA) continue;
-                const int vA = nid(Ac, Acoll ? ia : 4);
+                const int vA = vAs[ia];
                 const int a1 = dn(u0, vA), m = dm[vA == kNoNode ? 0 : vA];
                 const float bound = (float)(a1 + m - 1);
                 lower = vA != kNoNode && a1 >= 0 && m != kNone && bound < lower ? bound : lower;
@@ -649,7 +715,7 @@ struct RowOps {
 #pragma unroll
             for (int ia = 0; ia < 4; ++ia) {
                 if (ia >= nA) continue;
-                const int vA = nid(Ac, Acoll ? ia : 4);
+                const int vA = vAs[ia];
                 int t;
                 const float b1A = (t = dn(u0, vA)) < 0 ? per : (float)t;
                 const float b2A = (t = dn(u1, vA)) < 0 ? per : (float)t;
@@ -822,9 +888,10 @@ struct RowOps {
         if (s.kind == 0) c0 = c1 = kNoop;
         c0 = c0 > kNoop ? kNoop : c0;
         c1 = c1 > kNoop ? kNoop : c1;
-        int fl = action_legal(r, s, c0, c1) ? 1 : 0;
-        interact(r, s.agent[0], c0);
-        if (s.n == 2) interact(r, s.agent[1], c1);
+        const Target g0 = target(r, s.agent[0], c0), g1 = s.n == 2 ? target(r, s.agent[1], c1) : g0;
+        int fl = action_legal(r, s, c0, c1, g0, g1) ? 1 : 0;
+        interact(r, s.agent[0], c0, g0);
+        if (s.n == 2) interact(r, s.agent[1], c1, g1);
         const bool asserted = s.n == 2 && agent_cell(r, s.agent[0]) == agent_cell(r, s.agent[1]);
         if (asserted) fl |= 4;
         else if (is_goal(r, s)) fl |= 2;
@@ -928,10 +995,13 @@ struct RowOps {
     // E2E_BRTDP.Q(state, action, v_l) with value_init's values (e2e_brtdp.py:736-760, :678-729);
     // false where T raises (joint co-location)
     OC_RH bool q_value(const Row& r0, const Sub& s, int c0, int c1, double& q) const {
+        return q_value(r0, s, c0, c1, target(r0, s.agent[0], c0), target(r0, s.agent[1], c1), q);
+    }
+    OC_RH bool q_value(const Row& r0, const Sub& s, int c0, int c1, const Target& g0, const Target& g1, double& q) const {
         Row r = r0;
-        interact(r, s.agent[0], c0);
+        interact(r, s.agent[0], c0, g0);
         if (s.n == 2) {
-            interact(r, s.agent[1], c1);
+            interact(r, s.agent[1], c1, g1);
             if (agent_cell(r, s.agent[0]) == agent_cell(r, s.agent[1])) return false;
         }
         double cost = 1.0;  // time_cost + action_cost per moving agent (:816-826)

@@ -92,7 +92,7 @@ static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* take
             const oc_subtask& o = subs[ai];
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
                         {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
-            ocro::RowOps<A, K, W> ops(L, blob);
+            ocro::RowOps<A, K, W, true> ops(L, blob);  // the likelihood kernels' lean flavour
             f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
         }
         out[e] = f == OC_LIK_OK ? v : 0.0;
