@@ -559,14 +559,15 @@ struct RollArgs {
 };
 
 // Stage the level's table blob and the subtask configurations in LDS.
+template <int NT = kBlock>
 __device__ __forceinline__ void stage_roll_tables(const RollArgs& R, const uint8_t* blob_g, uint32_t* blob_w,
                                                   ocro::Sub* subs) {
     // 16-byte loads (a quarter of the load instructions; round 6), then the last < 4 words
     const int n16 = R.blob_words >> 2;
-    for (int i = threadIdx.x; i < n16; i += kBlock) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
-    for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += kBlock) blob_w[i] = ((const uint32_t*)blob_g)[i];
+    for (int i = threadIdx.x; i < n16; i += NT) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
+    for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += NT) blob_w[i] = ((const uint32_t*)blob_g)[i];
     constexpr int kSubWords = (int)(sizeof(ocro::Sub) / 4);
-    for (int i = threadIdx.x; i < R.nsub * kSubWords; i += kBlock)
+    for (int i = threadIdx.x; i < R.nsub * kSubWords; i += NT)
         ((uint32_t*)subs)[i] = ((const uint32_t*)R.subs)[i];
     __syncthreads();
 }
@@ -619,8 +620,15 @@ __device__ __forceinline__ void store_row(uint8_t* __restrict__ sout, int64_t P,
     }
 }
 
+#ifndef OC_ROLL_BLOCK
+#define OC_ROLL_BLOCK 256
+#endif
+// The rollout kernel's block (one row per lane).  512- and 1,024-lane blocks (fewer blocks to
+// dispatch, each staging the tables with more lanes) measured slower at C5: 12.0-12.3 and
+// 12.2-12.4 us against 11.6 (profiles/r05/ab/ab_merge_pairs_blocks.jsonl).
+constexpr int kRollBlock = OC_ROLL_BLOCK;
 template <int A, int K, bool W, bool GD>
-__global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const uint8_t* __restrict__ sin,
+__global__ __launch_bounds__(kRollBlock) void oc_rollout_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                             uint8_t* __restrict__ sout,
                                                             const uint8_t* __restrict__ act,
                                                             const uint8_t* __restrict__ alloc,
@@ -652,12 +660,12 @@ __global__ __launch_bounds__(kBlock) void oc_rollout_kernel(RollArgs R, const ui
         for (int a = 0; a < A; ++a) v.acts |= (uint32_t)act[a * P + e] << (8 * a);
         return v;
     };
-    int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    int64_t e = blockIdx.x * (int64_t)kRollBlock + threadIdx.x;
     In in;
     if (e < R.B) in = load_in(e);
-    stage_roll_tables(R, blob_g, blob_w, subs);
+    stage_roll_tables<kRollBlock>(R, blob_g, blob_w, subs);
     const uint8_t* blob = (const uint8_t*)blob_w;
-    for (bool first = true; e < R.B; e += (int64_t)gridDim.x * kBlock, first = false) {
+    for (bool first = true; e < R.B; e += (int64_t)gridDim.x * kRollBlock, first = false) {
         if (!first) in = load_in(e);
         ocro::RowT<K, W> r = in.r;
         const uint16_t t = in.t;
@@ -2410,12 +2418,12 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     RollArgs R;
     if (const int rc = roll_args(h, subtasks, num_subtasks, B, R, true)) return rc;
     if (B == 0) return OC_OK;
-    const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
+    const int64_t need = (B + kRollBlock - 1) / kRollBlock, cap = (int64_t)h->cus * 8 * kBlock / kRollBlock;
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_ROLL(A, K, W, GD)                                                                             \
     if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W, GD>, h->roll.lds_bytes)) return rc;   \
-    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W, GD>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,            \
+    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W, GD>), grid, dim3(kRollBlock), h->roll.lds_bytes, st, R,            \
                        (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags,       \
                        lower_bound)
 #define OC_PLAN_WIDE(A, K) OC_LAUNCH_ROLL(A, K, true, true)

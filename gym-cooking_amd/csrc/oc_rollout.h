@@ -624,26 +624,37 @@ struct RowOps {
     // lanes active per VALU instruction in oc_bounds_kernel, with more SALU than VALU
     // instructions, profiles/r03/c5_static_b2/pmc_c5.json.)
     OC_RH float helper(const Sub& s, int u0, int u1, int Ac, int Bc) const {
+        const int B1[1] = {Bc};
+        return helper_n<1>(s, u0, u1, Ac, B1);
+    }
+    // min over NB B squares of helper(s, u0, u1, Ac, Bc[j]) (a repeated square is harmless):
+    // the B squares' node and distance reads issue together (round 6, two at a time for the
+    // rollout and bounds rows; two Plates make two B squares on the Salad kitchens)
+    template <int NB>
+    OC_RH float helper_n(const Sub& s, int u0, int u1, int Ac, const int (&Bc)[NB]) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
-        int vA[4], vB[4];
-        const bool Acoll = approaches(Ac, vA), Bcoll = approaches(Bc, vB);
+        int vA[4], vB[NB][4];
+        const bool Acoll = approaches(Ac, vA);
+        bool Bcoll = false;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) Bcoll |= approaches(Bc[j], vB[j]);
         const int nA = wave_any(Acoll) ? 4 : 1, nB = wave_any(Bcoll) ? 4 : 1;
-        const uint32_t pa = xy(Ac), pb = xy(Bc);
-        const int dx = (int)(pa & 0xFFu) - (int)(pb & 0xFFu), dy = (int)(pa >> 8) - (int)(pb >> 8);
-        const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
+        const uint32_t pa = xy(Ac);
         if (s.n == 1) {
 #pragma unroll
             for (int ia = 0; ia < 4; ++ia) {
                 if (ia >= nA) continue;  // wave-uniform
                 const int a1 = dn(u0, vA[ia]);
 #pragma unroll
-                for (int ib = 0; ib < 4; ++ib) {
-                    if (ib >= nB) continue;
-                    const int b2 = dn(vA[ia], vB[ib]);
-                    const float bound = (float)(a1 + b2 - 1);
-                    lower = a1 >= 0 && b2 >= 0 && bound < lower ? bound : lower;
-                }
+                for (int j = 0; j < NB; ++j)
+#pragma unroll
+                    for (int ib = 0; ib < 4; ++ib) {
+                        if (ib >= nB) continue;
+                        const int b2 = dn(vA[ia], vB[j][ib]);
+                        const float bound = (float)(a1 + b2 - 1);
+                        lower = a1 >= 0 && b2 >= 0 && bound < lower ? bound : lower;
+                    }
             }
             return lower > 1.0f ? lower : 1.0f;
         }
@@ -656,7 +667,6 @@ struct RowOps {
         // the types are (0, 1) or (1, 0).  Integers (distances, or the perimeter for an
         // unreachable node) until the last add: the same value as the pair loop, exactly.
         constexpr int kInf = 0x3FFFFFFF;
-        int MA[3] = {kInf, kInf, kInf}, MB[3] = {kInf, kInf, kInf};
         auto side = [&](const int (&v)[4], int n, int (&M)[3]) OC_RL {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -670,16 +680,24 @@ struct RowOps {
                 M[2] = b1 == b2 && m < M[2] ? m : M[2];
             }
         };
-        side(vA, nA, MA);
-        side(vB, nB, MB);
         auto mx = [](int x, int y) OC_RL { return x > y ? x : y; };
         auto mn = [](int x, int y) OC_RL { return x < y ? x : y; };
-        const int single = mn(mx(MA[0], MB[1]), mx(MA[1], MB[0]));
-        const int dbl = mn(mn(mx(MA[0], MB[0]), mx(MA[1], MB[1])),
-                           mn(mx(MA[2], mn(mn(MB[0], MB[1]), MB[2])), mx(mn(mn(MA[0], MA[1]), MA[2]), MB[2])));
-        const int best = mn(single, 2 * dbl);
-        const float bound = (float)best + (man - 1.0f) * 0.5f;
-        lower = bound < lower ? bound : lower;
+        int MA[3] = {kInf, kInf, kInf};
+        side(vA, nA, MA);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            int MB[3] = {kInf, kInf, kInf};
+            side(vB[j], nB, MB);
+            const uint32_t pb = xy(Bc[j]);
+            const int dx = (int)(pa & 0xFFu) - (int)(pb & 0xFFu), dy = (int)(pa >> 8) - (int)(pb >> 8);
+            const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
+            const int single = mn(mx(MA[0], MB[1]), mx(MA[1], MB[0]));
+            const int dbl = mn(mn(mx(MA[0], MB[0]), mx(MA[1], MB[1])),
+                               mn(mx(MA[2], mn(mn(MB[0], MB[1]), MB[2])), mx(mn(mn(MA[0], MA[1]), MA[2]), MB[2])));
+            const int best = mn(single, 2 * dbl);
+            const float bound = (float)best + (man - 1.0f) * 0.5f;
+            lower = bound < lower ? bound : lower;
+        }
         return lower > 1.0f ? lower : 1.0f;
     }
 
@@ -803,6 +821,20 @@ struct RowOps {
         for (uint32_t set = obj_set<HOIST>(b, r, m, skip_deliv); set != 0u; set &= set - 1u) f(src_cell(b, r, __builtin_ctz(set)));
     }
 
+    // The same, two locations per call (f(c1, c2); c2 = c1 for a lone last one)
+    template <bool HOIST, class F>
+    OC_RH void visit_obj_pairs(const BoundRow& b, const Row& r, int m, bool skip_deliv, F&& f) const {
+        uint32_t set = obj_set<HOIST>(b, r, m, skip_deliv);
+#pragma unroll 1
+        while (set != 0u) {
+            const int c1 = src_cell(b, r, __builtin_ctz(set));
+            set &= set - 1u;
+            const int c2 = set != 0u ? src_cell(b, r, __builtin_ctz(set)) : c1;
+            set &= set == 0u ? 0u : set - 1u;
+            f(c1, c2);
+        }
+    }
+
     // get_lower_bound_for_subtask_given_objs (overcooked_environment.py:594-664)
     OC_RH float lower_bound(const Row& r, const Sub& s) const {
         float pen;
@@ -854,10 +886,18 @@ struct RowOps {
             });
         } else if (s.kind == 2) {
             visit_objs<HOIST>(br, r, s.start[0], false, [&](int Ac) OC_RL {
-                visit_objs<HOIST>(br, r, s.start[1], false, [&](int Bc) OC_RL {
-                    const float b = helper(s, u0, u1, Ac, Bc);
-                    if (b < lower) lower = b;
-                });
+                if constexpr (LEAN) {
+                    visit_objs<HOIST>(br, r, s.start[1], false, [&](int Bc) OC_RL {
+                        const float b = helper(s, u0, u1, Ac, Bc);
+                        if (b < lower) lower = b;
+                    });
+                } else {
+                    visit_obj_pairs<HOIST>(br, r, s.start[1], false, [&](int B1, int B2) OC_RL {
+                        const int Bc[2] = {B1, B2};
+                        const float b = helper_n<2>(s, u0, u1, Ac, Bc);
+                        if (b < lower) lower = b;
+                    });
+                }
             });
         }
         return lower;
