@@ -1912,7 +1912,6 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     L.max_T = max_T;
     const int dcell[5] = {W, -W, -1, 1, 0};
     for (int c = 0; c < 5; ++c) L.dcell_lut |= (uint64_t)((dcell[c] + 128) & 0xFF) << (8 * c);
-    if (max_T > 0x7FFF) return fail(OC_EINVAL, "max_T %d > 32767", max_T);
     if (!wide)
         ocsw::build_swar_level(L.sw, W, H, L.done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x,
                                lv->spawn_y, num_agents, cell8, mask, lv->encoding, lv->tiles);
@@ -2488,6 +2487,12 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     return hip_check("oc_nav_likelihood launch");
 }
 
+// configuration chunks: enough blocks for this many per CU (round 2's sweep, 0.44 ms kernels:
+// 64 best; round 5, 0.09 ms kernels with each block staging the tables: 32 at 0.0916-0.0924 ms
+// against 0.0925-0.0938 at 64 and 0.0925-0.0931 at 24, profiles/r05/ab/ab_bounds_chunks.jsonl)
+#ifndef OC_BOUNDS_BLOCKS_PER_CU
+#define OC_BOUNDS_BLOCKS_PER_CU 32
+#endif
 int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* subtasks, int32_t num_subtasks,
                       float* lower_bound, uint8_t* doable, int64_t B, void* stream) {
     if (h == nullptr || state == nullptr || subtasks == nullptr || lower_bound == nullptr || doable == nullptr ||
@@ -2501,11 +2506,11 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
     if (B == 0) return OC_OK;
     const int64_t need = (B + kBlock - 1) / kBlock, cap = (int64_t)h->cus * 8;
     const int64_t bx = need < cap ? need : cap;
-    // configuration chunks: enough blocks for 64 per CU, at most one configuration per chunk
-    // (C5, 2^18 envs x 64 configurations: 0.75 ms unchunked, 0.53 / 0.46 / 0.44 / 0.44 ms at
-    // 16 / 32 / 64 / 128 blocks per CU, 0.47 ms at one configuration per block;
-    // profiles/r02/bounds_chunk_sweep.log)
-    int64_t chunks = ((int64_t)h->cus * 64 + bx - 1) / bx;
+    // configuration chunks: enough blocks for OC_BOUNDS_BLOCKS_PER_CU per CU, at most one
+    // configuration per chunk (round 2, C5, 2^18 envs x 64 configurations: 0.75 ms unchunked,
+    // 0.53 / 0.46 / 0.44 / 0.44 ms at 16 / 32 / 64 / 128 blocks per CU, 0.47 ms at one
+    // configuration per block; profiles/r02/bounds_chunk_sweep.log; round 5: see the macro)
+    int64_t chunks = ((int64_t)h->cus * OC_BOUNDS_BLOCKS_PER_CU + bx - 1) / bx;
     if (chunks > R.nsub) chunks = R.nsub;
     if (chunks < 1) chunks = 1;
     const dim3 grid((unsigned)bx, (unsigned)chunks);

@@ -159,8 +159,9 @@ const char* oc_last_error(void);
  * on h has failed.  Returns the message length. */
 int oc_get_last_error(const oc_handle* h, char* buf, int64_t size);
 
-/* Static level tables + episode settings.  max_T = --max-num-timesteps (main.py:24; 0 = no
- * limit).  device = HIP ordinal the handle's launches target (recorded, validated), or
+/* Static level tables + episode settings.  max_T = --max-num-timesteps (main.py:24), 0 to
+ * 65,535 (the u16 step counter; round 4 refused past 32,767); 0 = no limit, where the counter
+ * wraps after 65,535 steps (the reference's keeps counting; nothing else reads it).  device = HIP ordinal the handle's launches target (recorded, validated), or
  * OC_DEVICE_HOST: a host-only handle that makes no HIP call at all (no device query, no
  * device tables); only the host entry points (oc_get_layout, oc_cpu_step, oc_reachability,
  * oc_stats_size) take it, the device ones return OC_EINVAL. */

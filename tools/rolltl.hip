@@ -172,10 +172,12 @@ __global__ __launch_bounds__(kBlock) void roll_phases(RollArgs R, const uint8_t*
             if (s.kind == 0) c0 = c1 = ocro::kNoop;
             c0 = c0 > ocro::kNoop ? ocro::kNoop : c0;
             c1 = c1 > ocro::kNoop ? ocro::kNoop : c1;
-            int fl = ops.action_legal(r, s, c0, c1) ? 1 : 0;
+            // as RowOps::run: the agents' target squares read once, the legality without branches
+            const auto g0 = ops.target(r, s.agent[0], c0), g1 = s.n == 2 ? ops.target(r, s.agent[1], c1) : g0;
+            int fl = ops.action_legal(r, s, c0, c1, g0, g1) ? 1 : 0;
             ts[2] = stamp(true);
-            ops.interact(r, s.agent[0], c0);
-            if (s.n == 2) ops.interact(r, s.agent[1], c1);
+            ops.interact(r, s.agent[0], c0, g0);
+            if (s.n == 2) ops.interact(r, s.agent[1], c1, g1);
             ts[3] = stamp(true);
             const bool asserted = s.n == 2 && ops.agent_cell(r, s.agent[0]) == ops.agent_cell(r, s.agent[1]);
             if (asserted) fl |= 4;
