@@ -63,19 +63,20 @@ constexpr int kNoop = 4;
 constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NAV_ACTIONS + (0, 0)
 
 // Static level tables, one byte blob (offsets in RollLevel, set by build_roll_level):
-//   tile_off   [C] tile class per cell (C = 256 for a narrow level: cells >= W*H read Counter;
-//              the cell count rounded up to 4 for a wide one)
-//   xy_off     u16 [C] x | y << 8 of each cell (the bound's Manhattan terms read it instead of
-//              dividing by W: round 5)
+//   tile_off   [TC] tile class per cell (TC = 256 for a narrow level: cell ids >= W*H, the dead
+//              slot 0xFF among them, read Counter; the cell count rounded up to 4 for a wide one)
+//   xy_off     u16 [C] x | y << 8 of each cell (C = the cell count rounded up to 4; the bound's
+//              Manhattan terms read it instead of dividing by W: round 5)
 //   node_off   u16 [C * 5] graph node of (cell, approach), approach 4 = (0, 0)
-//   cut_off    Cutboard cells in scan order (L.ncut; u8 narrow, u16 wide)
-//   deliv_off  Delivery cells in scan order (L.ndeliv; u8 narrow, u16 wide)
+//   cut_off    Cutboard cells in scan order (L.ncut; u8 narrow, u16 wide; padded to 4 bytes)
+//   deliv_off  Delivery cells in scan order (L.ndeliv; likewise)
 //   man_off    u16 [2][C] Manhattan distance from a cell to the nearest Cutboard (row 0) /
 //              Delivery (row 1) square (the two-agent static bound's B term; round 6)
 //   dmin_off   [2][nnodes] the distance from a node to the nearest Cutboard (row 0) / Delivery
 //              (row 1) approach node, 0xFF = none reachable
 //   dist_off   [nnodes][nnodes] BFS distances (last: a wide level stages the blob up to here)
-// A narrow level's first offsets are fixed: 0, 256, 768, 3328, 3584, 3840, then dmin at 4864.
+// Only the tile table's size is fixed (256 entries on a narrow level); the others follow the
+// level's cell count (round 6; before, every per-cell table had 256 entries on a narrow level).
 
 struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t W, H, perimeter, nnodes;
@@ -84,8 +85,9 @@ struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t dmin_off;  // blob offset of the nearest-Cutboard / nearest-Delivery distance rows
     int32_t tile_off, node_off, cut_off, deliv_off, dist_off;
     int32_t xy_off;    // u16 x | y << 8 per cell
-    int32_t man_off;   // u16 [2][C]: Manhattan distance from a cell to the nearest Cutboard (row 0) /
-                       // Delivery (row 1) square
+    int32_t man_off;   // u16 [2][man_stride]: Manhattan distance from a cell to the nearest Cutboard
+                       // (row 0) / Delivery (row 1) square
+    int32_t man_stride;
     int32_t wide;     // u16 cell ids (W * H > 255)
     int32_t blob_bytes;  // the blob's size (a multiple of 4)
     int32_t lds_bytes;   // what the kernels stage in LDS: all of it, or up to dist_off (dist_global)
@@ -205,14 +207,23 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
     const int cells = W * H;
     L.wide = cells > kMaxCells ? 1 : 0;
     if (cells > kMaxCellsWide) return -1;
-    const int C = L.wide ? (cells + 3) & ~3 : 256, lb = L.wide ? 2 : 1;  // table cells, list entry bytes
+    // the tile table covers every cell id a row can hold (a narrow level's 0xFF dead slot
+    // included: 256 entries); the other per-cell tables only the level's cells (round 6: a 7x7
+    // kitchen's fixed tables shrink from 4.9 to 1.1 KB, and every block stages them)
+    const int TC = L.wide ? (cells + 3) & ~3 : 256, C = (cells + 3) & ~3, lb = L.wide ? 2 : 1;
     const int max_nodes = L.wide ? kMaxNodesWide : kMaxNodesNarrow;
+    int ncut = 0, ndeliv = 0;
+    for (int c = 0; c < cells; ++c) {
+        ncut += tiles[c] == kCutboard;
+        ndeliv += tiles[c] == kDelivery;
+    }
     L.tile_off = 0;
-    L.xy_off = C;
-    L.node_off = 3 * C;
+    L.xy_off = TC;
+    L.node_off = L.xy_off + 2 * C;
     L.cut_off = L.node_off + 2 * C * 5;
-    L.deliv_off = L.cut_off + lb * C;
-    L.man_off = L.deliv_off + lb * C;
+    L.deliv_off = L.cut_off + ((lb * ncut + 3) & ~3);
+    L.man_off = L.deliv_off + ((lb * ndeliv + 3) & ~3);
+    L.man_stride = C;
     L.dmin_off = L.man_off + 2 * 2 * C;
     blob_v.assign((size_t)L.dmin_off, 0);  // grown below once the node count is known
     uint8_t* blob = blob_v.data();
@@ -222,7 +233,7 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
         if (L.wide) ((uint16_t*)(blob + off))[i] = (uint16_t)c;
         else blob[off + i] = (uint8_t)c;
     };
-    for (int c = 0; c < C; ++c) {
+    for (int c = 0; c < TC; ++c) {
         tile[c] = c < cells ? tiles[c] : (uint8_t)kCounter;
         if (c < cells && tiles[c] == kCutboard) put_list(L.cut_off, L.ncut++, c);
         if (c < cells && tiles[c] == kDelivery) put_list(L.deliv_off, L.ndeliv++, c);
@@ -878,8 +889,7 @@ struct RowOps {
         if (s.kind == 1 || s.kind == 3) {  // static B side: one table lookup per A approach
             const int nb = s.kind == 1 ? L.ncut : L.ndeliv;
             const uint8_t* dm = T + L.dmin_off + (s.kind == 1 ? 0 : L.nnodes);
-            const int C = L.wide ? (L.W * L.H + 3) & ~3 : 256;
-            const uint16_t* man_t = (const uint16_t*)(T + L.man_off) + (s.kind == 1 ? 0 : C);
+            const uint16_t* man_t = (const uint16_t*)(T + L.man_off) + (s.kind == 1 ? 0 : L.man_stride);
             visit_objs<HOIST>(br, r, s.start[0], s.kind == 3, [&](int Ac) OC_RL {
                 const float b = helper_static(s, u0, u1, Ac, nb, dm, man_t);
                 if (b < lower) lower = b;
