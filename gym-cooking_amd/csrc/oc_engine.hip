@@ -601,22 +601,28 @@ __device__ __forceinline__ ocro::RowT<K, W> load_row(const uint8_t* __restrict__
     return r;
 }
 
-// the row's agent and item planes (t and flags are the caller's)
-template <int A, int K, bool W = false>
+// the row's agent and item planes (t and flags are the caller's).  NT: non-temporal stores
+// (the rollout's outputs: 11.39-11.43 against 11.47-11.55 us per C5 launch; the bounds kernel's
+// outputs stored that way were slower, 0.095 against 0.091 ms, profiles/r05/ab/ab_nt_stores.jsonl)
+template <int A, int K, bool W = false, bool NT = false>
 __device__ __forceinline__ void store_row(uint8_t* __restrict__ sout, int64_t P, int64_t e, const ocro::RowT<K, W>& r) {
     using PL = Planes<A, K, W>;
+    auto st = [&](int64_t i, uint32_t v) {
+        if constexpr (NT) __builtin_nontemporal_store((uint8_t)v, sout + i);
+        else sout[i] = (uint8_t)v;
+    };
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-        sout[a * P + e] = (uint8_t)r.ax(a);
-        sout[(PL::Y + a) * P + e] = (uint8_t)r.ay(a);
-        sout[(PL::H + a) * P + e] = (uint8_t)r.ah(a);
+        st(a * P + e, (uint32_t)r.ax(a));
+        st((PL::Y + a) * P + e, (uint32_t)r.ay(a));
+        st((PL::H + a) * P + e, (uint32_t)r.ah(a));
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         const uint32_t c = (uint32_t)r.il(j);
-        sout[(PL::L + j) * P + e] = (uint8_t)c;
-        if (W) sout[(PL::LH + j) * P + e] = (uint8_t)(c >> 8);
-        sout[(PL::M + j) * P + e] = (uint8_t)r.im(j);
+        st((PL::L + j) * P + e, c);
+        if (W) st((PL::LH + j) * P + e, c >> 8);
+        st((PL::M + j) * P + e, (uint32_t)r.im(j));
     }
 }
 
@@ -679,11 +685,11 @@ __global__ __launch_bounds__(kRollBlock) void oc_rollout_kernel(RollArgs R, cons
             ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             f = ops.run(r, s, c0, c1, bound);
         }
-        store_row<A, K, W>(sout, P, e, r);
-        ((uint16_t*)(sout + PL::T * P))[e] = t;
-        sout[PL::F * P + e] = fl_in;
-        out_flags[e] = (uint8_t)f;
-        lb[e] = bound;
+        store_row<A, K, W, true>(sout, P, e, r);
+        __builtin_nontemporal_store(t, (uint16_t*)(sout + PL::T * P) + e);
+        __builtin_nontemporal_store(fl_in, sout + PL::F * P + e);
+        __builtin_nontemporal_store((uint8_t)f, out_flags + e);
+        __builtin_nontemporal_store(bound, lb + e);
     }
 }
 
