@@ -54,8 +54,18 @@ def main():
                 f()
                 busy.append((time.perf_counter_ns() - t0) / 1e3)
             torch.cuda.synchronize()
+            # the first call of a freshly bound launcher (the bench binds its window's launchers
+            # ahead and calls them for the first time inside the window)
+            first = []
+            for _ in range(20):
+                g = eb.step_n_launcher(s, traj[(n - 1) * S:], acts.reshape(-1), n, traj, ex, coll, stats, tot)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter_ns()
+                g()
+                first.append((time.perf_counter_ns() - t0) / 1e3)
+            torch.cuda.synchronize()
         q = lambda v: {p: round(sorted(v)[int(p / 100 * (len(v) - 1))], 1) for p in (10, 50, 90)}  # noqa: E731
-        out[sname + ("+rccl" if with_rccl else "")] = {"idle_us": q(idle), "busy_us": q(busy)}
+        out[sname + ("+rccl" if with_rccl else "")] = {"idle_us": q(idle), "busy_us": q(busy), "first_call_us": q(first)}
     print(json.dumps(out))
 
 
