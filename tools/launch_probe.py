@@ -17,6 +17,10 @@ from gym_cooking_amd.engine import OvercookedBatch  # noqa: E402
 
 def main():
     dev = "cuda:0"
+    if "--spin" in sys.argv:  # as bench.py --host-wait spin: hipDeviceScheduleSpin before torch touches the device
+        import ctypes
+        hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        assert hip.hipSetDevice(ctypes.c_int(0)) == 0 and hip.hipSetDeviceFlags(ctypes.c_uint(1)) == 0
     B, A, n = 1 << 20, 2, 20
     out = {}
     cases = [("default", False), ("created", False), ("default", True)]
