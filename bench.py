@@ -676,6 +676,34 @@ class WindowLog:
                 json.dump({"events": self.events}, f)
 
 
+def cpu_baseline_line(args, world: int, batch: int):
+    """the C restatement timed beside the GPU line, on rank 0, at every world size.
+    Its threads are the host cores this rank may use: the job's share (the CPU affinity set
+    capped by the cgroup quota; the GPU pool gives each GPU's job a share of the machine, and
+    nproc there counts every core of the host) divided among the job's ranks.  At N = 1 the same
+    sample on nproc threads is reported beside it, labelled oversubscribed when nproc exceeds
+    the share.  The sample is one rank's shard (`batch` envs), the workload one GPU runs."""
+    if args.no_cpu_baseline:
+        return None
+    hc = host_cores()
+    nproc, share = hc["limits"]["nproc"], max(1, hc["threads"] // max(1, world))
+    out = cpu_baseline(args.level, args.agents, batch, args.max_T, args.cpu_budget, share)
+    out["host_cpu_limits"] = hc["limits"]
+    out["nproc"] = nproc
+    out["ranks_sharing_the_job_cores"] = world
+    if world == 1 and share != nproc:
+        o = cpu_baseline(args.level, args.agents, batch, args.max_T, args.cpu_budget / 2, nproc)
+        out["nproc_threads_oversubscribed"] = dict(
+            {k: o[k] for k in ("value", "cores", "sample")},
+            note="%d threads (nproc) on a job granted %d CPUs" % (nproc, hc["threads"]))
+    out["reference_python_container"] = {
+        "full_step": 695, "logic_only": 9076, "unit": "env-steps/s", "cores": 1,
+        "host": "survey container (Intel Xeon, 8 cores, Python 3.10.12), not the GPU box; BASELINE.md section 2",
+        "sample": "reference OvercookedEnvironment.step() on one partial-divider_salad 2-agent env; logic_only = "
+                  "check_collisions + execute_navigation + done + reward without the copies"}
+    return out
+
+
 def launch_ranks(n: int, argv) -> int:
     """`bench.py --gpus N` outside torchrun: start the N ranks (one process per GPU) as child
     processes and exit with their status.  The rendezvous store is a TCPStore this parent hosts
@@ -733,7 +761,8 @@ def selftest_ranks(args) -> int:
                                clock=lambda: trace.append("clock") or time.perf_counter())
     if rank == 0:
         print(json.dumps({"n_gpus": world, "ranks": g.tolist(), "window_trace": trace,
-                          "window_gathered": gathered.tolist()}), flush=True)
+                          "window_gathered": gathered.tolist(),
+                          "cpu_baseline": cpu_baseline_line(args, world, sh.batch)}), flush=True)
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
     return 0
@@ -772,6 +801,10 @@ def main() -> int:
                          "the window's closing synchronize spins on the completion signal; auto: the runtime's default "
                          "wait, which let the host see a ~90 us kernel's completion 20-40 us late in some windows "
                          "(profiles/r04/window_wait/)")
+    ap.add_argument("--window-launch", choices=("graph", "call"), default="graph",
+                    help="graph (default): the window's oc_step_n launches and its all-gather replayed from one "
+                         "hipGraph captured before the window; call: one launch call per launch, then the "
+                         "all-gather call")
     ap.add_argument("--window-log", default=None,
                     help="write the timed windows' host timestamps to PATH.rankR.json (tools/window_split.py)")
     ap.add_argument("--selftest-ranks", action="store_true", help=argparse.SUPPRESS)
@@ -847,6 +880,23 @@ def main() -> int:
         return out, src
 
     timed, _ = plan(K, acts)
+    window_graph = None
+    if args.window_launch == "graph":
+        # The window's launches and its summary all-gather captured once as one hipGraph, so the
+        # timed region holds one host call (graph launch) instead of a launch call per launch
+        # plus the all-gather call.  Captured (and replayed once, untimed) here, well before the
+        # window: torch's capture collects Python's garbage first, and the warmup below rewrites
+        # everything the replay touched (s_a, the outputs, stats, the summary rows).
+        window_graph = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(device=dev)
+        cap.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.graph(window_graph, stream=cap):
+            for f in plan(K, acts)[0]:  # launchers bound to the capture stream
+                f()
+            ocdist.gather_summaries(summary_row, summary_all)
+        torch.cuda.synchronize()
+        window_graph.replay()
+        torch.cuda.synchronize()
     # The warmup steps its own action stream (another seed): the window never replays a launch
     # the warmup ran.  The window's actions are written just before it (untimed), as a policy
     # writes them before a step: at the driver's shape (K = 20, 42 MB) they are then
@@ -894,8 +944,12 @@ def main() -> int:
     # ---------------- timed region (timed_window: launches + all-gather + synchronize) ----------
     sync = torch.cuda.synchronize
     wlog = WindowLog(args.window_log)
-    elapsed, gathered = timed_window(wlog.wrap(timed), lambda: ocdist.gather_summaries(summary_row, summary_all),
-                                     sync, ocdist.barrier, clock=wlog.clock("warm"))
+    if window_graph is not None:
+        win_launches, win_gather = [window_graph.replay], (lambda: summary_all)
+    else:
+        win_launches, win_gather = timed, (lambda: ocdist.gather_summaries(summary_row, summary_all))
+    elapsed, gathered = timed_window(wlog.wrap(win_launches), win_gather, sync, ocdist.barrier,
+                                     clock=wlog.clock("warm"))
     # -------------------------------------------------------------------------------------------
     elapsed_max = ocdist.max_over_ranks(elapsed, dev)
     summary = ocdist.summarize(gathered)
@@ -938,8 +992,7 @@ def main() -> int:
     flush.fill_(1)
     stats.zero_()
     del flush
-    cold, _ = timed_window(wlog.wrap(timed), lambda: ocdist.gather_summaries(summary_row, summary_all), sync,
-                           ocdist.barrier, clock=wlog.clock("cold"))
+    cold, _ = timed_window(wlog.wrap(win_launches), win_gather, sync, ocdist.barrier, clock=wlog.clock("cold"))
     cold_max = ocdist.max_over_ranks(cold, dev)
     wlog.dump(rank)
     nS = eb.layout.num_planes  # state bytes per env (the u16 t counts 2)
@@ -975,6 +1028,8 @@ def main() -> int:
                                else "read by an untimed run of the window's launches just before it") +
                               "; the warmup steps another stream",
             "host_wait": args.host_wait,
+            "window_launch": ("one hipGraph (the launches + the RCCL all-gather), captured before the window"
+                              if window_graph is not None else "a launch call per launch, then the all-gather call"),
         },
         "open_loop": True,
         "window_cold_actions": {
@@ -1011,29 +1066,8 @@ def main() -> int:
     if not args.no_planner:
         line["planner"] = measure_planner(dev, world)
         line["bayes"] = measure_bayes(dev, world)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # the C restatement on the host cores this job actually has (the CPU
-        # affinity set capped by the cgroup quota; the GPU pool gives each GPU's job a share of
-        # the machine, and nproc there counts every core of the host).  The same sample on nproc
-        # threads is reported beside it, labelled oversubscribed when nproc exceeds the share.
-        hc = host_cores()
-        nproc = hc["limits"]["nproc"]
-        line["cpu_baseline"] = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget,
-                                            hc["threads"])
-        line["cpu_baseline"]["host_cpu_limits"] = hc["limits"]
-        line["cpu_baseline"]["nproc"] = nproc
-        if hc["threads"] != nproc:
-            o = cpu_baseline(args.level, args.agents, sh.batch, args.max_T, args.cpu_budget / 2, nproc)
-            line["cpu_baseline"]["nproc_threads_oversubscribed"] = dict(
-                {k: o[k] for k in ("value", "cores", "sample")},
-                note="%d threads (nproc) on a job granted %d CPUs" % (nproc, hc["threads"]))
-        line["cpu_baseline"]["reference_python_container"] = {
-            "full_step": 695, "logic_only": 9076, "unit": "env-steps/s", "cores": 1,
-            "host": "survey container (Intel Xeon, 8 cores, Python 3.10.12), not the GPU box; BASELINE.md section 2",
-            "sample": "reference OvercookedEnvironment.step() on one partial-divider_salad 2-agent env; logic_only = "
-                      "check_collisions + execute_navigation + done + reward without the copies"}
-    elif rank == 0:
-        line["cpu_baseline"] = None
+    if rank == 0:
+        line["cpu_baseline"] = cpu_baseline_line(args, world, sh.batch)
     if rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     ocdist.shutdown()

@@ -561,13 +561,13 @@ struct RollArgs {
 // Stage the level's table blob and the subtask configurations in LDS.
 template <int NT = kBlock>
 __device__ __forceinline__ void stage_roll_tables(const RollArgs& R, const uint8_t* blob_g, uint32_t* blob_w,
-                                                  ocro::Sub* subs) {
+                                                  ocro::Sub* subs, int nt = NT) {
     // 16-byte loads (a quarter of the load instructions; round 6), then the last < 4 words
     const int n16 = R.blob_words >> 2;
-    for (int i = threadIdx.x; i < n16; i += NT) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
-    for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += NT) blob_w[i] = ((const uint32_t*)blob_g)[i];
+    for (int i = threadIdx.x; i < n16; i += nt) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
+    for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += nt) blob_w[i] = ((const uint32_t*)blob_g)[i];
     constexpr int kSubWords = (int)(sizeof(ocro::Sub) / 4);
-    for (int i = threadIdx.x; i < R.nsub * kSubWords; i += NT)
+    for (int i = threadIdx.x; i < R.nsub * kSubWords; i += nt)
         ((uint32_t*)subs)[i] = ((const uint32_t*)R.subs)[i];
     __syncthreads();
 }
@@ -631,8 +631,14 @@ __device__ __forceinline__ void store_row(uint8_t* __restrict__ sout, int64_t P,
 #endif
 // The rollout kernel's block (one row per lane).  512- and 1,024-lane blocks (fewer blocks to
 // dispatch, each staging the tables with more lanes) measured slower at C5: 12.0-12.3 and
-// 12.2-12.4 us against 11.6 (profiles/r05/ab/ab_merge_pairs_blocks.jsonl).
+// 12.2-12.4 us against 11.6 (profiles/r05/ab/ab_merge_pairs_blocks.jsonl).  A launch of fewer
+// than kRollSmallRows rows runs one-wave blocks instead (the kernel reads its block size from
+// blockDim): the planner's 4,096-row launches then cover 64 CUs, not 16 (round 6).
 constexpr int kRollBlock = OC_ROLL_BLOCK;
+#ifndef OC_ROLL_SMALL_ROWS
+#define OC_ROLL_SMALL_ROWS 16384
+#endif
+constexpr int64_t kRollSmallRows = OC_ROLL_SMALL_ROWS;
 template <int A, int K, bool W, bool GD>
 __global__ __launch_bounds__(kRollBlock) void oc_rollout_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                             uint8_t* __restrict__ sout,
@@ -666,12 +672,13 @@ __global__ __launch_bounds__(kRollBlock) void oc_rollout_kernel(RollArgs R, cons
         for (int a = 0; a < A; ++a) v.acts |= (uint32_t)act[a * P + e] << (8 * a);
         return v;
     };
-    int64_t e = blockIdx.x * (int64_t)kRollBlock + threadIdx.x;
+    const int nt = (int)blockDim.x;  // kRollBlock, or 64 for a small launch
+    int64_t e = blockIdx.x * (int64_t)nt + threadIdx.x;
     In in;
     if (e < R.B) in = load_in(e);
-    stage_roll_tables<kRollBlock>(R, blob_g, blob_w, subs);
+    stage_roll_tables<kRollBlock>(R, blob_g, blob_w, subs, nt);
     const uint8_t* blob = (const uint8_t*)blob_w;
-    for (bool first = true; e < R.B; e += (int64_t)gridDim.x * kRollBlock, first = false) {
+    for (bool first = true; e < R.B; e += (int64_t)gridDim.x * nt, first = false) {
         if (!first) in = load_in(e);
         ocro::RowT<K, W> r = in.r;
         const uint16_t t = in.t;
@@ -1138,6 +1145,14 @@ __global__ __launch_bounds__(kBlock) void oc_step_wide_kernel(WideArgs R, const 
             for (int a = 0; a < A; ++a) EX[a] = 0u;
 #pragma unroll
             for (int k = 0; k < kEPL; ++k) {  // the lane's four envs, one after another
+                // a column past B (the batch's last word) is not stepped: its bytes go back out as
+                // they came in, with no-op executed actions and no collision (its cells may be
+                // any u16, which env_step would use as tile-table indices)
+                if (k >= rem) {
+#pragma unroll
+                    for (int a = 0; a < A; ++a) EX[a] |= 4u << (8 * k);
+                    continue;
+                }
                 const int sh = 8 * k;
                 Row r;
 #pragma unroll
@@ -2258,31 +2273,37 @@ int oc_cpu_step(const oc_handle* h, const void* state_in, void* state_out, const
 #undef OC_CPU_STEP
         return OC_OK;
     };
-    // Every range runs the same (A, K, MODE) dispatch: range 0 runs on the calling thread first,
-    // so a dispatch failure sets this thread's message; a worker's failure message is carried
-    // back to it.  Ranges whose thread cannot be started run here too.
-    int rc = run(0);
-    if (rc == OC_OK && nt > 1) {
-        std::vector<std::thread> pool;
-        std::vector<int> rcs((size_t)nt, OC_OK);
-        std::vector<std::string> msgs((size_t)nt);
-        int64_t started = 1;
-        try {
-            for (; started < nt; ++started)
-                pool.emplace_back([&, i = started] {
-                    rcs[(size_t)i] = run(i);
-                    if (rcs[(size_t)i] != OC_OK) msgs[(size_t)i] = g_last_error;
-                });
-        } catch (const std::exception&) {  // no more threads: the rest of the ranges run here
-        }
-        for (int64_t i = started; i < nt; ++i) {
-            rcs[(size_t)i] = run(i);
-            if (rcs[(size_t)i] != OC_OK) msgs[(size_t)i] = g_last_error;
-        }
-        for (auto& t : pool) t.join();
-        for (int64_t i = 1; i < nt && rc == OC_OK; ++i)
-            if (rcs[(size_t)i] != OC_OK) rc = fail(rcs[(size_t)i], "%s", msgs[(size_t)i].c_str());
+    // Every range runs the same (A, K, MODE) dispatch, so it is checked once here, on the calling
+    // thread (an unsupported shape fails before any thread starts).  Then ranges 1..nt-1 start on
+    // workers and range 0 runs on the calling thread while they work; a worker's failure message
+    // is still carried back.  Ranges whose thread cannot be started run here too.
+#define OC_CPU_NOP(...) (void)0
+    if (h->wide) {
+        OC_DISPATCH(h->A, h->K, OC_CPU_NOP)
+    } else {
+        OC_DISPATCH_STEP(h, OC_CPU_NOP)
     }
+#undef OC_CPU_NOP
+    std::vector<std::thread> pool;
+    std::vector<int> rcs((size_t)nt, OC_OK);
+    std::vector<std::string> msgs((size_t)nt);
+    int64_t started = 1;
+    try {
+        for (; started < nt; ++started)
+            pool.emplace_back([&, i = started] {
+                rcs[(size_t)i] = run(i);
+                if (rcs[(size_t)i] != OC_OK) msgs[(size_t)i] = g_last_error;
+            });
+    } catch (const std::exception&) {  // no more threads: the rest of the ranges run here
+    }
+    int rc = run(0);
+    for (int64_t i = started; i < nt; ++i) {
+        rcs[(size_t)i] = run(i);
+        if (rcs[(size_t)i] != OC_OK) msgs[(size_t)i] = g_last_error;
+    }
+    for (auto& t : pool) t.join();
+    for (int64_t i = 1; i < nt && rc == OC_OK; ++i)
+        if (rcs[(size_t)i] != OC_OK) rc = fail(rcs[(size_t)i], "%s", msgs[(size_t)i].c_str());
     if (rc == OC_OK && totals != nullptr)
         for (int64_t i = 0; i < nt; ++i)
             for (int c = 0; c < OC_NSTATS; ++c) totals[c] += part[(size_t)(i * OC_NSTATS + c)];
@@ -2423,12 +2444,13 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     RollArgs R;
     if (const int rc = roll_args(h, subtasks, num_subtasks, B, R, true)) return rc;
     if (B == 0) return OC_OK;
-    const int64_t need = (B + kRollBlock - 1) / kRollBlock, cap = (int64_t)h->cus * 8 * kBlock / kRollBlock;
+    const int nt = B < kRollSmallRows ? 64 : kRollBlock;
+    const int64_t need = (B + nt - 1) / nt, cap = (int64_t)h->cus * 8 * kBlock / nt;
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_ROLL(A, K, W, GD)                                                                             \
     if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W, GD>, h->roll.lds_bytes)) return rc;   \
-    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W, GD>), grid, dim3(kRollBlock), h->roll.lds_bytes, st, R,            \
+    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W, GD>), grid, dim3(nt), h->roll.lds_bytes, st, R,                    \
                        (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags,       \
                        lower_bound)
 #define OC_PLAN_WIDE(A, K) OC_LAUNCH_ROLL(A, K, true, true)

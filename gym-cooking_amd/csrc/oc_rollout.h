@@ -1045,7 +1045,9 @@ struct RowOps {
     // E2E_BRTDP.Q(state, action, v_l) with value_init's values (e2e_brtdp.py:736-760, :678-729);
     // false where T raises (joint co-location)
     OC_RH bool q_value(const Row& r0, const Sub& s, int c0, int c1, double& q) const {
-        return q_value(r0, s, c0, c1, target(r0, s.agent[0], c0), target(r0, s.agent[1], c1), q);
+        // agent[1]'s target only for a two-agent subtask (a one-agent q_value never reads g1)
+        const Target g0 = target(r0, s.agent[0], c0);
+        return q_value(r0, s, c0, c1, g0, s.n == 2 ? target(r0, s.agent[1], c1) : g0, q);
     }
     OC_RH bool q_value(const Row& r0, const Sub& s, int c0, int c1, const Target& g0, const Target& g1, double& q) const {
         Row r = r0;

@@ -26,6 +26,11 @@
  *  - State is structure-of-arrays: `num_planes` byte planes of `pitch` bytes each (see
  *    oc_layout).  Env e of plane p lives at byte p*pitch + e (the t plane holds u16 at
  *    2*e and spans two planes).  pitch = B rounded up to OC_PITCH_ALIGN.
+ *  - Columns [B, pitch) of an output plane belong to the engine: the step kernels move four
+ *    envs per 32-bit word, so the columns of the batch's last word past B may be rewritten
+ *    (the state planes with what the input held there or its step, exec_actions / coll_mask
+ *    with no-op / 0).  Nothing at or past the next multiple of 4 above B is written, and no
+ *    statistic counts a column past B.
  */
 #ifndef OC_ENGINE_H_
 #define OC_ENGINE_H_

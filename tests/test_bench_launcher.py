@@ -16,7 +16,7 @@ def _selftest(n):
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--batch", "4096",
-                          "--selftest-ranks"], env=env, capture_output=True, text=True, timeout=300)
+                          "--cpu-budget", "1", "--selftest-ranks"], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout  # rank 0 alone prints
@@ -30,6 +30,16 @@ def test_bench_gpus_2_starts_two_ranks():
     assert [r[0] for r in ranks] == [0, 1] and all(r[1] == 2 for r in ranks)
     assert [(r[2], r[3]) for r in ranks] == [(0, 4096), (4096, 4096)]  # contiguous global-id shards
     assert ranks[0][4] != ranks[1][4]  # two processes
+
+
+def test_bench_line_at_2_ranks_has_cpu_baseline():
+    """SURVEY 8(d) asks for the CPU path timed beside every line: at N > 1 too, rank 0 times the
+    C restatement on its share of the job's host cores over one shard's workload."""
+    d = _selftest(2)
+    cb = d["cpu_baseline"]
+    assert cb is not None and cb["value"] > 0 and cb["kind"] == "port"
+    assert cb["cores"] >= 1 and cb["ranks_sharing_the_job_cores"] == 2
+    assert "4096 envs" in cb["sample"]
 
 
 def test_timed_window_holds_launches_gather_sync_only():

@@ -246,3 +246,51 @@ def test_wide_level_planner_matches_host_search(name, A, sub, agents):
         a = p.get_next_action(env, getattr(recipes, sub[0])(sub[1]), agents, {})
         out.append((a, p.cur_obj_count, len(p.v_l), p.v_l[(p._repr(p.start), p._sub_key)]))
     assert out[0] == out[1], out
+
+
+@pytest.mark.parametrize("out", ["no_traj", "out_is_last", "separate_out"])
+def test_wide_step_n_splits_into_launches(out):
+    """oc_step_n on a wide level past the 4,096 steps one launch carries: 4,100 steps are two
+    launches of 2,050, the second starting from the first's last state (its last trajectory
+    slot, or state_out).  Every step's outputs (when kept), the final state, the in-launch totals
+    and the statistics rows against the CPU oracle, for the three output arrangements: no
+    trajectory, state_out the trajectory's last slot, state_out a buffer of its own."""
+    name, A, B, n, max_T, seed = "widegraph-24x24_salad", 2, 300, 4100, 23, 5
+    lv = levels.load_level(tw._path(name))
+    eb = _batch(lv, A, B, max_T)
+    ob = oracle.OracleBatch(lv, A, max_T, B)
+    P, S = eb.pitch, eb.layout.state_bytes
+    s_in = eb.new_state()
+    eb.reset(s_in)
+    c, c2 = ob.new_state(), ob.new_state()
+    ob.reset(c)
+    acts = torch.empty((n, A * P), dtype=torch.uint8, device="cuda:0")
+    for r in range(n):
+        eb.gen_actions(acts[r], r, seed)
+    traj = None if out == "no_traj" else torch.empty(n * S, dtype=torch.uint8, device="cuda:0")
+    ex = None if out == "no_traj" else torch.empty(n * A * P, dtype=torch.uint8, device="cuda:0")
+    coll = None if out == "no_traj" else torch.empty(n * P, dtype=torch.uint8, device="cuda:0")
+    s_out = traj[(n - 1) * S:] if out == "out_is_last" else eb.new_state()
+    stats, totals = eb.new_stats(), torch.zeros(5, dtype=torch.int64, device="cuda:0")
+    eb.step_n(s_in, s_out, acts.reshape(-1), n, traj, ex, coll, stats, totals)
+    torch.cuda.synchronize()
+    tr = None if traj is None else traj.view(n, S).cpu().numpy()
+    exh = None if ex is None else ex.view(n, A, P).cpu().numpy()
+    colh = None if coll is None else coll.view(n, P).cpu().numpy()
+    ca, cex, ccoll = ob.new_actions(), np.zeros(A * P, np.uint8), np.zeros(P, np.uint8)
+    tot = np.zeros(5, np.int64)
+    for r in range(n):
+        ob.gen_actions(ca, 0, r, seed)
+        fl_in = tl.planes_view(c, A, ob.K, P)["fl"].copy()
+        ob.step(c, c2, ca, cex, ccoll)
+        c, c2 = c2, c
+        tot += tl.window_totals(fl_in, c, ccoll, A, ob.K, P, B)
+        if tr is not None and (r % 97 == 0 or r in (2048, 2049, 2050, 2051, n - 1)):
+            assert np.array_equal(tl.env_view(tr[r], A, ob.K, P, B), tl.env_view(c, A, ob.K, P, B)), r
+            assert np.array_equal(exh[r][:, :B], cex.reshape(A, P)[:, :B]), r
+            assert np.array_equal(colh[r][:B], ccoll[:B]), r
+    host = s_out.cpu().numpy()[:S]
+    assert np.array_equal(tl.env_view(host, A, ob.K, P, B), tl.env_view(c, A, ob.K, P, B))
+    assert np.array_equal(totals.cpu().numpy(), tot)
+    assert np.array_equal(eb.reduce_stats(stats).cpu().numpy(), tot)
+    assert tot[0] >= B * (n // (max_T + 1)) // 2

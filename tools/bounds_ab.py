@@ -77,7 +77,7 @@ def child(lib):
     torch.cuda.synchronize()
     h = hashlib.sha256()
     for t in (lb[:, :rows], ok[:, :rows], out, flags[:rows], rlb[:rows], v[:rows], f[:rows], vr[:rows], fr[:rows],
-              v1[:rows], f1[:rows]):
+              v1[:rows], f1[:rows], o4, f4[:4096], l4[:4096]):
         h.update(t.contiguous().cpu().numpy().tobytes())
     print(json.dumps({"lib": os.path.basename(lib), "bounds_ms": ms_b, "rollout_ms": ms_r, "rollout_4096_ms": ms_r4,
                       "likelihood_ms": ms_l,

@@ -16,6 +16,7 @@
 #include "../gym-cooking_amd/csrc/oc_engine.hip"
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #define CK(x)                                                                                      \
@@ -186,6 +187,190 @@ __global__ __launch_bounds__(SW * 64 + (LW ? 64 : 0), LW ? LB : 1) void stepn_tl
     if (st.coll == 0xFFFFFFFFu) tl[0] = st.eps;  // keep the statistics live
 }
 
+
+// Round 6: the loader-wave form with the work handed out dynamically.  A work
+// item is (chunk of the block's 1,024 envs, segment of SEG steps); items are taken from a
+// per-launch atomic queue in segment-major order by a grid of co-resident blocks, so a block
+// that finishes early takes more work and no block starts in a second residency round.  A
+// chunk's segment k > 0 continues from the state its segment k - 1 left in the trajectory
+// slot k*SEG - 1: that step's stores are sc1 (write-through), the producing block's waves wait
+// vmcnt(0), meet at a barrier, and one lane stores the chunk's flag (sc1); the consuming
+// block's thread 0 polls the flag with sc1 loads, the block meets at a barrier and loads the
+// state with sc1 loads (MI355X_MICROARCH.md "Valid forms", row 1).  The last segment resets
+// the flag, the last block out resets the queue, so every launch starts from zeros.
+template <int A, int K, int MODE, int SEG>
+__global__ __launch_bounds__(5 * 64, 5) void stepn_seg(LevelArgs L, const uint8_t* __restrict__ sin,
+                                                        uint8_t* __restrict__ sout,
+                                                        const uint8_t* __restrict__ actions,
+                                                        uint8_t* __restrict__ traj,
+                                                        uint8_t* __restrict__ exec_out,
+                                                        uint8_t* __restrict__ coll_out, int n,
+                                                        uint32_t* __restrict__ q, uint32_t* __restrict__ flags) {
+    constexpr int CP = kCPnt, SW = 4, kBS = SW * 64;
+    __shared__ uint32_t tbl4[64];
+    __shared__ uint32_t ring[2 * kLwSteps * SW * A * 64];
+    __shared__ uint32_t item_s;
+    if (threadIdx.x < 64u) tbl4[threadIdx.x] = L.cls4[threadIdx.x];
+    __syncthreads();
+    const bool loader = threadIdx.x >= (uint32_t)kBS;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint8_t* tbl = (const uint8_t*)tbl4;
+    const uint32_t P = (uint32_t)L.pitch, nlanes = P / kEPL;
+    constexpr int NP = 3 * A + 2 * K + 3;
+    constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+    auto cls_of = [&](uint32_t cells) -> uint32_t {
+        const uint32_t b0 = tbl[cells & 0xFFu], b1 = tbl[(cells >> 8) & 0xFFu], b2 = tbl[(cells >> 16) & 0xFFu],
+                       b3 = tbl[cells >> 24];
+        return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    };
+    const __amdgpu_buffer_rsrc_t rin = make_rsrc(sin, (int64_t)NP * P), rout = make_rsrc(sout, (int64_t)NP * P);
+    const __amdgpu_buffer_rsrc_t ract = make_rsrc(actions, (int64_t)n * A * P);
+    const __amdgpu_buffer_rsrc_t tr = make_rsrc(traj, (int64_t)n * NP * P);
+    const __amdgpu_buffer_rsrc_t rex = make_rsrc(exec_out, (int64_t)n * A * P), rco = make_rsrc(coll_out, (int64_t)n * P);
+    const uint32_t nchunks = nlanes / (uint32_t)kBS, nseg = (uint32_t)((n + SEG - 1) / SEG), total = nchunks * nseg;
+    StepStats st;
+    typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+    for (;;) {
+        if (threadIdx.x == 0u) {
+            const uint32_t it = atomicAdd(q, 1u);
+            if (it < total && it >= nchunks) {  // segment k > 0: wait for the chunk's segment k - 1
+                const uint32_t c = it % nchunks, k = it / nchunks;
+                while (__hip_atomic_load(flags + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != k)
+                    __builtin_amdgcn_s_sleep(2);
+            }
+            item_s = it;
+        }
+        lds_barrier();
+        const uint32_t it = item_s;
+        if (it >= total) break;
+        const uint32_t c = it % nchunks, k = it / nchunks;
+        const int r0 = (int)k * SEG, r1 = min(n, r0 + SEG);
+        const uint32_t gb = c * (uint32_t)kBS;
+        if (loader) {
+            auto fill = [&](int rb, int h) {
+                uint32_t w[kLwSteps][SW][A];
+#pragma unroll
+                for (int qq = 0; qq < kLwSteps; ++qq)
+#pragma unroll
+                    for (int v = 0; v < SW; ++v)
+#pragma unroll
+                        for (int a = 0; a < A; ++a)
+                            w[qq][v][a] = rb + qq < r1 ? bld32<0>(ract, (gb + 64u * v + lane) * 4u,
+                                                                   (uint32_t)((rb + qq) * A + a) * P)
+                                                       : 0u;
+#pragma unroll
+                for (int qq = 0; qq < kLwSteps; ++qq)
+#pragma unroll
+                    for (int v = 0; v < SW; ++v)
+#pragma unroll
+                        for (int a = 0; a < A; ++a)
+                            ring[(((h * kLwSteps + qq) * SW + v) * A + a) * 64 + lane] = w[qq][v][a];
+            };
+            fill(r0, 0);
+            for (int rb = r0; rb < r1; rb += kLwSteps) {
+                lds_barrier();
+                if (rb + kLwSteps < r1) fill(rb + kLwSteps, (((rb - r0) / kLwSteps) & 1) ^ 1);
+            }
+            lds_barrier();  // the item's last batch has been read
+            lds_barrier();  // the stepping waves' stores drained (segment end)
+            continue;
+        }
+        const uint32_t g = gb + threadIdx.x, vo = g * 4u;
+        // the state: the batch's input (segment 0) or the slot segment k - 1 left (sc1 loads)
+        Chunk<A, K> ch;
+        {
+            const __amdgpu_buffer_rsrc_t rs = k == 0u ? rin : tr;
+            const uint32_t base = k == 0u ? 0u : (uint32_t)(r0 - 1) * NP * P;
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                ch.wx[a] = bld32<kCPsc1>(rs, vo, base + a * P);
+                ch.wy[a] = bld32<kCPsc1>(rs, vo, base + (kPY + a) * P);
+                ch.wh[a] = bld32<kCPsc1>(rs, vo, base + (kPH + a) * P);
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                ch.wl[j] = bld32<kCPsc1>(rs, vo, base + (kPL + j) * P);
+                ch.wm[j] = bld32<kCPsc1>(rs, vo, base + (kPM + j) * P);
+            }
+            const auto t = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(g * 8u), (int)(base + kPT * P), kCPsc1);
+            ch.wt = make_uint2(t[0], t[1]);
+            ch.wf = bld32<kCPsc1>(rs, vo, base + kPF * P);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        uint32_t T0 = ch.wt.x, T1 = ch.wt.y;
+        uint32_t pending = ocsw::at_done80<K, MODE>(L.sw, ch.wl);
+        const int64_t rem = L.B - (int64_t)g * kEPL;
+        const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (rem <= 0 ? 0u : (1u << (8 * (uint32_t)rem)) - 1u);
+        for (int r = r0; r < r1; ++r) {
+            uint32_t act[A], ex[A], cm;
+            const int qq = (r - r0) % kLwSteps;
+            if (qq == 0) lds_barrier();
+            const int h = ((r - r0) / kLwSteps) & 1;
+#pragma unroll
+            for (int a = 0; a < A; ++a) act[a] = ring[(((h * kLwSteps + qq) * SW + (threadIdx.x >> 6)) * A + a) * 64 + lane];
+            const uint32_t f_in = ch.wf;
+            const bool full = ocsw::step4<A, K, MODE>(L.sw, ch.wx, ch.wy, ch.wh, ch.wl, ch.wm, T0, T1, ch.wf, act, ex,
+                                                      cm, cls_of, WaveAny{}, pending);
+            st.coll += __popc(cm & vmask);
+            if (full) {
+                const uint32_t ended = (ch.wf & ~f_in & vmask) & ocsw::k01;
+                st.eps += __popc(ended);
+            }
+            const uint32_t base = (uint32_t)r * NP * P;
+            auto store_state = [&](auto pol) {
+                constexpr int PC = decltype(pol)::value;
+#pragma unroll
+                for (int a = 0; a < A; ++a) {
+                    bst32<PC>(tr, ch.wx[a], vo, base + a * P);
+                    bst32<PC>(tr, ch.wy[a], vo, base + (kPY + a) * P);
+                    bst32<PC>(tr, ch.wh[a], vo, base + (kPH + a) * P);
+                }
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    bst32<PC>(tr, ch.wl[j], vo, base + (kPL + j) * P);
+                    bst32<PC>(tr, ch.wm[j], vo, base + (kPM + j) * P);
+                }
+                const u32x2 tw = {T0, T1};
+                __builtin_amdgcn_raw_buffer_store_b64(tw, tr, (int)(g * 8u), (int)(base + kPT * P), PC);
+                bst32<PC>(tr, ch.wf, vo, base + kPF * P);
+            };
+            if (r + 1 == r1 && r1 < n) store_state(std::integral_constant<int, kCPsc1>{});  // the hand-off slot
+            else store_state(std::integral_constant<int, CP>{});
+#pragma unroll
+            for (int a = 0; a < A; ++a) bst32<CP>(rex, ex[a], vo, (uint32_t)(r * A + a) * P);
+            bst32<CP>(rco, cm, vo, (uint32_t)r * P);
+        }
+        lds_barrier();  // pairs with the loader's end-of-item barrier
+        if (r1 == n) {
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                bst32<CP>(rout, ch.wx[a], vo, a * P);
+                bst32<CP>(rout, ch.wy[a], vo, (kPY + a) * P);
+                bst32<CP>(rout, ch.wh[a], vo, (kPH + a) * P);
+            }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                bst32<CP>(rout, ch.wl[j], vo, (kPL + j) * P);
+                bst32<CP>(rout, ch.wm[j], vo, (kPM + j) * P);
+            }
+            const u32x2 tw = {T0, T1};
+            __builtin_amdgcn_raw_buffer_store_b64(tw, rout, (int)(g * 8u), (int)(kPT * P), CP);
+            bst32<CP>(rout, ch.wf, vo, kPF * P);
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's hand-off stores are done
+        }
+        lds_barrier();  // every stepping wave's stores drained
+        if (threadIdx.x == 0u)
+            __hip_atomic_store(flags + c, r1 == n ? 0u : k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the last block out resets the queue for the next launch
+    if (threadIdx.x == 0u && atomicAdd(q + 1, 1u) == gridDim.x - 1u) {
+        __hip_atomic_store(q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(q + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (st.coll == 0xFFFFFFFFu) flags[0] = st.eps;  // keep the statistics live
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -291,6 +476,44 @@ int main(int argc, char** argv) {
     time("noload (no loads, no barrier)", stepn_tl<3, 4, 0, false, true, false>, false);
     time("noload + stamps", stepn_tl<3, 4, 0, false, true, true>, false);
     report("noload");
+    // round 6: the dynamic (chunk, segment) queue; outputs compared with the product form's
+    uint32_t* qf;
+    CK(hipMalloc(&qf, (2 + nlanes / 256) * 4));
+    CK(hipMemset(qf, 0, (2 + nlanes / 256) * 4));
+    std::vector<uint8_t> ref_traj((size_t)n * S), got((size_t)n * S), ref_ex((size_t)n * 3 * P), got_ex((size_t)n * 3 * P);
+    launch(stepn_tl<3, 4, 0, true, false, false>, true);
+    CK(hipMemcpy(ref_traj.data(), traj, ref_traj.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(ref_ex.data(), ex, ref_ex.size(), hipMemcpyDeviceToHost));
+    auto seg = [&](const char* name, auto kern, int per_cu) {
+        auto go = [&]() {
+            hipLaunchKernelGGL(kern, dim3((unsigned)(h->cus * per_cu)), dim3(320), 0, nullptr, L, s0, sout, acts, traj, ex,
+                               coll, n, qf, qf + 2);
+        };
+        CK(hipMemset(traj, 0, (size_t)n * S));
+        go();
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(got.data(), traj, got.size(), hipMemcpyDeviceToHost));
+        CK(hipMemcpy(got_ex.data(), ex, got_ex.size(), hipMemcpyDeviceToHost));
+        const bool same = got == ref_traj && got_ex == ref_ex;
+        for (int i = 0; i < 3; ++i) go();
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < 10; ++i) go();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        CK(hipMemcpy(got.data(), traj, got.size(), hipMemcpyDeviceToHost));
+        const bool same2 = got == ref_traj;
+        printf("%-44s %8.3f us/step  outputs %s\n", name, ms * 1e3 / 10 / n,
+               same && same2 ? "identical to lw" : "DIFFER from lw");
+    };
+    seg("seg 20 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 20>, 3);
+    seg("seg 20 steps, 4 blocks/CU", stepn_seg<3, 4, 0, 20>, 4);
+    seg("seg 10 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 10>, 3);
+    seg("seg 25 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 25>, 3);
+    seg("seg 50 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 50>, 3);
+    seg("seg 100 steps (queue only), 3 blocks/CU", stepn_seg<3, 4, 0, 100>, 3);
+    time("lw (product form) again", stepn_tl<3, 4, 0, true, false, false>, true);
     // the product launch, for reference (C-ABI, with the statistics)
     uint64_t* stats;
     int64_t nb;
