@@ -801,10 +801,11 @@ def main() -> int:
                          "the window's closing synchronize spins on the completion signal; auto: the runtime's default "
                          "wait, which let the host see a ~90 us kernel's completion 20-40 us late in some windows "
                          "(profiles/r04/window_wait/)")
-    ap.add_argument("--window-launch", choices=("graph", "call"), default="graph",
-                    help="graph (default): the window's oc_step_n launches and its all-gather replayed from one "
-                         "hipGraph captured before the window; call: one launch call per launch, then the "
-                         "all-gather call")
+    ap.add_argument("--window-launch", choices=("call", "graph"), default="call",
+                    help="call (default): one launch call per launch, then the all-gather call; graph: the "
+                         "window's oc_step_n launches and its all-gather replayed from one hipGraph captured before "
+                         "the window (round 6, measured no faster: 117.9-128.5 us windows either way over three "
+                         "alternating runs each, profiles/r06/pass_b/)")
     ap.add_argument("--window-log", default=None,
                     help="write the timed windows' host timestamps to PATH.rankR.json (tools/window_split.py)")
     ap.add_argument("--selftest-ranks", action="store_true", help=argparse.SUPPRESS)

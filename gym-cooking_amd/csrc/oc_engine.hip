@@ -561,13 +561,13 @@ struct RollArgs {
 // Stage the level's table blob and the subtask configurations in LDS.
 template <int NT = kBlock>
 __device__ __forceinline__ void stage_roll_tables(const RollArgs& R, const uint8_t* blob_g, uint32_t* blob_w,
-                                                  ocro::Sub* subs, int nt = NT) {
+                                                  ocro::Sub* subs) {
     // 16-byte loads (a quarter of the load instructions; round 6), then the last < 4 words
     const int n16 = R.blob_words >> 2;
-    for (int i = threadIdx.x; i < n16; i += nt) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
-    for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += nt) blob_w[i] = ((const uint32_t*)blob_g)[i];
+    for (int i = threadIdx.x; i < n16; i += NT) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
+    for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += NT) blob_w[i] = ((const uint32_t*)blob_g)[i];
     constexpr int kSubWords = (int)(sizeof(ocro::Sub) / 4);
-    for (int i = threadIdx.x; i < R.nsub * kSubWords; i += nt)
+    for (int i = threadIdx.x; i < R.nsub * kSubWords; i += NT)
         ((uint32_t*)subs)[i] = ((const uint32_t*)R.subs)[i];
     __syncthreads();
 }
@@ -631,14 +631,12 @@ __device__ __forceinline__ void store_row(uint8_t* __restrict__ sout, int64_t P,
 #endif
 // The rollout kernel's block (one row per lane).  512- and 1,024-lane blocks (fewer blocks to
 // dispatch, each staging the tables with more lanes) measured slower at C5: 12.0-12.3 and
-// 12.2-12.4 us against 11.6 (profiles/r05/ab/ab_merge_pairs_blocks.jsonl).  A launch of fewer
-// than kRollSmallRows rows runs one-wave blocks instead (the kernel reads its block size from
-// blockDim): the planner's 4,096-row launches then cover 64 CUs, not 16 (round 6).
+// 12.2-12.4 us against 11.6 (profiles/r05/ab/ab_merge_pairs_blocks.jsonl).  One-wave blocks for
+// launches under 16 Ki rows (the planner's 4,096-row launches on 64 CUs instead of 16) were
+// slower too: 6.79-6.81 against 5.98-5.99 us for 4,096 rows, 11.28-11.37 against 11.32-11.37 at
+// 2^18 (profiles/r06/pass_b/ab_roll_small.jsonl, round 6): a block's table staging by one wave
+// takes four times as many load rounds, and that staging is on every row's critical path.
 constexpr int kRollBlock = OC_ROLL_BLOCK;
-#ifndef OC_ROLL_SMALL_ROWS
-#define OC_ROLL_SMALL_ROWS 16384
-#endif
-constexpr int64_t kRollSmallRows = OC_ROLL_SMALL_ROWS;
 template <int A, int K, bool W, bool GD>
 __global__ __launch_bounds__(kRollBlock) void oc_rollout_kernel(RollArgs R, const uint8_t* __restrict__ sin,
                                                             uint8_t* __restrict__ sout,
@@ -672,13 +670,12 @@ __global__ __launch_bounds__(kRollBlock) void oc_rollout_kernel(RollArgs R, cons
         for (int a = 0; a < A; ++a) v.acts |= (uint32_t)act[a * P + e] << (8 * a);
         return v;
     };
-    const int nt = (int)blockDim.x;  // kRollBlock, or 64 for a small launch
-    int64_t e = blockIdx.x * (int64_t)nt + threadIdx.x;
+    int64_t e = blockIdx.x * (int64_t)kRollBlock + threadIdx.x;
     In in;
     if (e < R.B) in = load_in(e);
-    stage_roll_tables<kRollBlock>(R, blob_g, blob_w, subs, nt);
+    stage_roll_tables<kRollBlock>(R, blob_g, blob_w, subs);
     const uint8_t* blob = (const uint8_t*)blob_w;
-    for (bool first = true; e < R.B; e += (int64_t)gridDim.x * nt, first = false) {
+    for (bool first = true; e < R.B; e += (int64_t)gridDim.x * kRollBlock, first = false) {
         if (!first) in = load_in(e);
         ocro::RowT<K, W> r = in.r;
         const uint16_t t = in.t;
@@ -689,7 +686,7 @@ __global__ __launch_bounds__(kRollBlock) void oc_rollout_kernel(RollArgs R, cons
         if (ai < R.nsub) {
             const ocro::Sub& s = subs[ai];
             const int c0 = (in.acts >> (8 * s.agent[0])) & 0xFFu, c1 = s.n == 2 ? (in.acts >> (8 * s.agent[1])) & 0xFFu : ocro::kNoop;
-            ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+            ocro::RowOps<A, K, W, false, GD> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             f = ops.run(r, s, c0, c1, bound);
         }
         store_row<A, K, W, true>(sout, P, e, r);
@@ -742,7 +739,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
             uint32_t taken = 0;
 #pragma unroll
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
-            ocro::RowOps<A, K, W, true> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+            ocro::RowOps<A, K, W, true, GD> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
             if (s.kind == 0) {
                 f = 0;
                 if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
@@ -923,7 +920,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
                     uint32_t taken = 0;
 #pragma unroll
                     for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
-                    ocro::RowOps<A, K, W, true> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
+                    ocro::RowOps<A, K, W, true, GD> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
                     if (s.kind == 0) {
                         f = 0;
                         if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
@@ -981,7 +978,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
                 const int ai = alloc != nullptr ? alloc[e] : 0;
                 const ocro::Sub& s = subs[ai];
                 ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
-                ocro::RowOps<A, K, W, true> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
+                ocro::RowOps<A, K, W, true, GD> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
                 ops.level0(r, s);
                 const bool joint = s.n == 2;
                 const int a0 = joint ? k / 5 : k, c1 = joint ? k % 5 : ocro::kNoop;
@@ -1062,7 +1059,7 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
     const int i0 = (int)(blockIdx.y * R.nsub / gridDim.y), i1 = (int)((blockIdx.y + 1) * R.nsub / gridDim.y);
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
         const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
-        ocro::RowOps<A, K, W> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+        ocro::RowOps<A, K, W, false, GD> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
         const auto br = ops.template bound_row<true>(r);  // the row's agent nodes, slot sets: once for its configurations
         for (int i = i0; i < i1; ++i) {
             float v;
@@ -2003,12 +2000,14 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     return OC_OK;
 }
 
-int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, int64_t node_of_len, uint8_t* dist,
-                    int64_t dist_len) {
+// the node table and the distances, as u8 (oc_reachability) or u16 (oc_reachability16)
+static int reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, int64_t node_of_len, void* dist,
+                        int64_t dist_len, int out_bytes) {
     if (h == nullptr || num_nodes == nullptr) return fail(OC_EINVAL, "bad argument");
     ErrScope es_(h);
     if (h->roll.nnodes < 0)
-        return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (a level of more than 255 cells) or a BFS distance of 255", ocro::kMaxNodesWide);
+        return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (a level of more than %d cells)", ocro::kMaxNodesWide,
+                    ocro::kMaxCellsWide);
     const int n = h->roll.nnodes, cells = h->level.width * h->level.height;
     *num_nodes = n;
     if (node_of != nullptr) {
@@ -2016,10 +2015,30 @@ int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, i
         memcpy(node_of, h->roll_blob_host.data() + h->roll.node_off, (size_t)cells * 5 * sizeof(uint16_t));
     }
     if (dist != nullptr) {
-        if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %d bytes", n * n);
-        memcpy(dist, h->roll_blob_host.data() + h->roll.dist_off, (size_t)n * n);
+        if (dist_len < (int64_t)n * n) return fail(OC_EINVAL, "dist needs %d entries", n * n);
+        const uint8_t* src = h->roll_blob_host.data() + h->roll.dist_off;
+        const size_t nn = (size_t)n * n;
+        if (out_bytes == 1) {
+            if (h->roll.dist16)
+                return fail(OC_ELEVEL, "a BFS distance of 255 or more: the u8 table cannot hold it (oc_reachability16)");
+            memcpy(dist, src, nn);
+        } else if (h->roll.dist16) {
+            memcpy(dist, src, nn * 2);
+        } else {
+            for (size_t i = 0; i < nn; ++i) ((uint16_t*)dist)[i] = src[i] == ocro::kNone ? (uint16_t)0xFFFF : src[i];
+        }
     }
     return OC_OK;
+}
+
+int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, int64_t node_of_len, uint8_t* dist,
+                    int64_t dist_len) {
+    return reachability(h, num_nodes, node_of, node_of_len, dist, dist_len, 1);
+}
+
+int oc_reachability16(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, int64_t node_of_len, uint16_t* dist,
+                      int64_t dist_len) {
+    return reachability(h, num_nodes, node_of, node_of_len, dist, dist_len, 2);
 }
 
 int oc_destroy(oc_handle* h) {
@@ -2384,7 +2403,9 @@ static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num
         if (subtasks[i].level != OC_LEVEL0 && !level1_ok)
             return fail(OC_EINVAL, "subtask %d: only oc_rollout takes OC_LEVEL1", i);
     if (num_subtasks < 1 || num_subtasks > OC_MAX_SUBTASKS) return fail(OC_EINVAL, "num_subtasks %d", num_subtasks);
-    if (h->roll.nnodes < 0) return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (a level of more than 255 cells) or a BFS distance of 255", ocro::kMaxNodesWide);
+    if (h->roll.nnodes < 0)
+        return fail(OC_ELEVEL, "reachability graph exceeds %d nodes (a level of more than %d cells)", ocro::kMaxNodesWide,
+                    ocro::kMaxCellsWide);
     if (h->roll_blob == nullptr) return fail(OC_EHIP, "rollout tables not on the device");
     R.L = h->roll;
     R.nsub = num_subtasks;
@@ -2444,13 +2465,12 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     RollArgs R;
     if (const int rc = roll_args(h, subtasks, num_subtasks, B, R, true)) return rc;
     if (B == 0) return OC_OK;
-    const int nt = B < kRollSmallRows ? 64 : kRollBlock;
-    const int64_t need = (B + nt - 1) / nt, cap = (int64_t)h->cus * 8 * kBlock / nt;
+    const int64_t need = (B + kRollBlock - 1) / kRollBlock, cap = (int64_t)h->cus * 8 * kBlock / kRollBlock;
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_ROLL(A, K, W, GD)                                                                             \
     if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W, GD>, h->roll.lds_bytes)) return rc;   \
-    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W, GD>), grid, dim3(nt), h->roll.lds_bytes, st, R,                    \
+    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W, GD>), grid, dim3(kRollBlock), h->roll.lds_bytes, st, R,            \
                        (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags,       \
                        lower_bound)
 #define OC_PLAN_WIDE(A, K) OC_LAUNCH_ROLL(A, K, true, true)

@@ -9,7 +9,8 @@
 //   lower_bound()   get_lower_bound_for_subtask_given_objs  overcooked_environment.py:480-664,
 //                   World.get_lower_bound_between(_helper), check_bound  world.py:115-283
 // The reachability graph of the static level (world.py:67-108) is precomputed by
-// build_roll_level() as a compact all-pairs distance table (u8, 0xFF = no path).  The static
+// build_roll_level() as a compact all-pairs distance table (u8, 0xFF = no path; u16, 0xFFFF = no
+// path, when some BFS distance reaches 255: a maze kitchen's long corridors, round 6).  The static
 // tables of a level (tile classes, graph node ids, Cutboard / Delivery lists, distances) form
 // one byte blob, sized per level (the tables + nnodes^2 distance bytes).  A narrow level's
 // kernels stage all of it in LDS when its graph has at most kMaxNodes nodes: a 7x7 kitchen's blob
@@ -51,8 +52,9 @@ constexpr int kMaxCells = 255;      // narrow levels: cell ids are bytes, 0xFF =
 constexpr int kMaxCellsWide = 1024;  // wide levels (more than 255 cells): u16 cell ids, 0xFFFF dead
 // compact reachability-graph node ids are u16 (kNoNode = none); at most kMaxNodes nodes keep a
 // block's LDS (blob + 64 configurations + the kernels' own) within the 160 KB of a gfx950 CU,
-// a larger graph's distances stay in device memory; distances are bytes (0xFF = no path), so a
-// graph whose BFS distances reach 255 is refused
+// a larger graph's distances stay in device memory; distances are bytes (0xFF = no path), or
+// u16 (0xFFFF = no path) in device memory when some BFS distance reaches 255 (RollLevel.dist16;
+// round 5 refused such a graph)
 constexpr int kMaxNodes = 360;  // 360^2 + the other tables + the compacted likelihood's 18 KB < 160 KB
 constexpr int kMaxNodesNarrow = 5 * kMaxCells;    // narrow levels: every node 255 cells can make
 constexpr int kMaxNodesWide = 5 * kMaxCellsWide;  // wide levels: the distances stay in device memory
@@ -73,8 +75,9 @@ constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NA
 //   man_off    u16 [2][C] Manhattan distance from a cell to the nearest Cutboard (row 0) /
 //              Delivery (row 1) square (the two-agent static bound's B term; round 6)
 //   dmin_off   [2][nnodes] the distance from a node to the nearest Cutboard (row 0) / Delivery
-//              (row 1) approach node, 0xFF = none reachable
-//   dist_off   [nnodes][nnodes] BFS distances (last: a wide level stages the blob up to here)
+//              (row 1) approach node, 0xFF = none reachable (u16 and 0xFFFF with dist16)
+//   dist_off   [nnodes][nnodes] BFS distances (last: a wide level stages the blob up to here;
+//              u16 entries with dist16)
 // Only the tile table's size is fixed (256 entries on a narrow level); the others follow the
 // level's cell count (round 6; before, every per-cell table had 256 entries on a narrow level).
 
@@ -93,6 +96,8 @@ struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t lds_bytes;   // what the kernels stage in LDS: all of it, or up to dist_off (dist_global)
     int32_t dist_global; // the distance table is read from device memory: a wide level, or a narrow
                          // one of more than kMaxNodes nodes (the planner kernels' GD instantiation)
+    int32_t dist16;      // the distance and nearest-side tables are u16 (some BFS distance >= 255);
+                         // implies dist_global (round 6)
 };
 
 // The environment step's level constants (the scalar step of wide levels, RowOps::env_step).
@@ -195,8 +200,8 @@ OC_RH bool has_u16(uint64_t w, uint32_t v) {
 // ---- host: level tables ----------------------------------------------------------------------
 // Builds the reachability graph of make_reachability_graph (world.py:67-108) and its BFS
 // distances into `blob_v` (resized to the blob).  Returns the node count, or -1 when the level
-// has more cells than its layout takes (255 narrow, kMaxCellsWide wide), or a BFS distance past
-// 254 (the byte table cannot hold it).
+// has more cells than its layout takes (255 narrow, kMaxCellsWide wide).  The distance table is
+// u8 while every BFS distance is below 255, u16 otherwise (dist16).
 inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, int H, const uint8_t* tiles, int enc) {
     L.W = W;
     L.enc = enc;
@@ -204,6 +209,7 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
     L.perimeter = 2 * (W + H);
     L.ncut = L.ndeliv = 0;
     L.nnodes = -1;
+    L.dist16 = 0;
     const int cells = W * H;
     L.wide = cells > kMaxCells ? 1 : 0;
     if (cells > kMaxCellsWide) return -1;
@@ -299,15 +305,11 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
             else if (!coll && !ncoll) link(node[c * 5 + 4], node[nc * 5 + 4]);
         }
     }
-    L.dist_off = (L.dmin_off + 2 * n + 3) & ~3;
-    blob_v.resize((size_t)L.dist_off + (size_t)n * n + 4, 0);
-    blob = blob_v.data();
-    tile = blob + L.tile_off;
-    node = (uint16_t*)(blob + L.node_off);
-    uint8_t* dist = blob + L.dist_off;
+    // all-pairs BFS into u16 rows first: a distance of 255 or more makes the tables u16
+    std::vector<uint16_t> d16((size_t)n * n, (uint16_t)0xFFFF);
+    int dmax = 0;
     for (int s = 0; s < n; ++s) {
-        uint8_t* row = dist + (size_t)s * n;
-        for (int t = 0; t < n; ++t) row[t] = kNone;
+        uint16_t* row = d16.data() + (size_t)s * n;
         int qh = 0, qt = 0;
         row[s] = 0;
         q[qt++] = s;
@@ -315,38 +317,50 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
             const int u = q[qh++];
             for (int k = 0; k < deg[u]; ++k) {
                 const int v = adj(u, k);
-                if (row[v] == kNone) {
-                    if (row[u] + 1 >= kNone) return -1;  // a distance the byte table cannot hold
-                    row[v] = (uint8_t)(row[u] + 1);
+                if (row[v] == 0xFFFF) {
+                    row[v] = (uint16_t)(row[u] + 1);
+                    dmax = row[v] > dmax ? row[v] : dmax;
                     q[qt++] = v;
                 }
             }
         }
     }
+    L.dist16 = dmax >= (int)kNone ? 1 : 0;
+    const int db = L.dist16 ? 2 : 1;  // bytes per distance entry
+    const uint32_t none = L.dist16 ? 0xFFFFu : kNone;
+    L.dist_off = (L.dmin_off + 2 * n * db + 3) & ~3;
+    blob_v.resize((size_t)L.dist_off + (size_t)n * n * db + 4, 0);
+    blob = blob_v.data();
+    tile = blob + L.tile_off;
+    node = (uint16_t*)(blob + L.node_off);
+    auto put = [&](size_t off, size_t i, uint32_t v) {
+        if (L.dist16) ((uint16_t*)(blob + off))[i] = (uint16_t)v;
+        else blob[off + i] = (uint8_t)v;
+    };
+    for (size_t i = 0; i < (size_t)n * n; ++i) put((size_t)L.dist_off, i, d16[i] == 0xFFFF ? none : d16[i]);
     // Chop and Deliver have a static B side (every Cutboard / every Delivery square, from any
     // side it is approached from): the single-agent bound's min over B of dist(A node, B node)
     // is this per-node table (world.py:175-189 evaluated once per level)
     for (int side = 0; side < 2; ++side) {
         const int off = side == 0 ? L.cut_off : L.deliv_off;
         const int nc = side == 0 ? L.ncut : L.ndeliv;
-        uint8_t* dm = blob + L.dmin_off + side * n;
         for (int v = 0; v < n; ++v) {
-            int best = kNone;
+            uint32_t best = none;
             for (int i = 0; i < nc; ++i) {
                 const int cell = L.wide ? ((const uint16_t*)(blob + off))[i] : blob[off + i];
                 for (int d = 0; d < 4; ++d) {
                     const int b = node[cell * 5 + d];
                     if (b == kNoNode) continue;
-                    const int dd = dist[(size_t)v * n + b];
-                    if (dd != kNone && dd < best) best = dd;
+                    const uint32_t dd = d16[(size_t)v * n + b];
+                    if (dd != 0xFFFF && dd < best) best = dd;
                 }
             }
-            dm[v] = (uint8_t)best;
+            put((size_t)L.dmin_off, (size_t)side * n + v, best);
         }
     }
     L.nnodes = n;
-    L.blob_bytes = (int32_t)((L.dist_off + (size_t)n * n + 3) & ~(size_t)3);
-    L.dist_global = L.wide || n > kMaxNodes ? 1 : 0;
+    L.blob_bytes = (int32_t)((L.dist_off + (size_t)n * n * db + 3) & ~(size_t)3);
+    L.dist_global = L.wide || n > kMaxNodes || L.dist16 ? 1 : 0;
     L.lds_bytes = L.dist_global ? L.dist_off : L.blob_bytes;
     blob_v.resize((size_t)L.blob_bytes, 0);
     return n;
@@ -356,7 +370,10 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
 // LEAN (the likelihood kernels, whose compacted form sits at 122 of the 128 VGPRs that keep 4
 // waves per SIMD): the bound walk reads a square's tile before its approach nodes, as before
 // round 6, instead of all five node reads at once (which keeps more values live).
-template <int A, int K, bool WIDE = false, bool LEAN = false>
+// DG (the planner kernels' device-memory-distance instantiation, and the host builds): the level
+// may have u16 distance tables (RollLevel.dist16, a wave-uniform branch at each read); without DG
+// the tables are u8 (a dist16 level always takes the device-memory path).
+template <int A, int K, bool WIDE = false, bool LEAN = false, bool DG = false>
 struct RowOps {
     using Row = RowT<K, WIDE>;
     using AcT = typename ConditionalT<WIDE, uint64_t, uint32_t>::type;
@@ -596,8 +613,26 @@ struct RowOps {
         const bool none = u == kNoNode || v == kNoNode;
         // narrow: u * nnodes < 1275^2 < 2^24, the full-rate 24-bit multiply; wide: up to 5,120^2
         const uint32_t i = WIDE ? (uint32_t)u * (uint32_t)L.nnodes + (uint32_t)v : mul24((uint32_t)u, (uint32_t)L.nnodes) + (uint32_t)v;
+        if constexpr (DG) {
+            if (L.dist16) {
+                const int d = ((const uint16_t*)D)[none ? 0u : i];
+                return none || d == 0xFFFF ? -1 : d;
+            }
+        }
         const int d = D[none ? 0u : i];
         return none || d == kNone ? -1 : d;
+    }
+    // the nearest-Cutboard / nearest-Delivery distance of node v (dmin row `side`), or -1
+    OC_RH int dmin(int side, int v) const {
+        const uint32_t i = (uint32_t)(side * L.nnodes + (v == kNoNode ? 0 : v));
+        if constexpr (DG) {
+            if (L.dist16) {
+                const int m = ((const uint16_t*)(T + L.dmin_off))[i];
+                return m == 0xFFFF ? -1 : m;
+            }
+        }
+        const int m = T[L.dmin_off + i];
+        return m == kNone ? -1 : m;
     }
 
     // A square's graph nodes as the bound walks them: its four approach nodes when it is
@@ -721,7 +756,7 @@ struct RowOps {
     //    approach node.
     // helper() clamps each pair's result to >= 1 and starts from perimeter + 1; both are
     // monotone, so the min over B of helper() is this with the same clamp.  Exact in fp32.
-    OC_RH float helper_static(const Sub& s, int u0, int u1, int Ac, int nb, const uint8_t* dm,
+    OC_RH float helper_static(const Sub& s, int u0, int u1, int Ac, int nb, int side,
                               const uint16_t* man_t) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
@@ -734,9 +769,9 @@ struct RowOps {
             for (int ia = 0; ia < 4; ++ia) {
                 if (ia >= nA) continue;
                 const int vA = vAs[ia];
-                const int a1 = dn(u0, vA), m = dm[vA == kNoNode ? 0 : vA];
+                const int a1 = dn(u0, vA), m = dmin(side, vA);
                 const float bound = (float)(a1 + m - 1);
-                lower = vA != kNoNode && a1 >= 0 && m != kNone && bound < lower ? bound : lower;
+                lower = vA != kNoNode && a1 >= 0 && m >= 0 && bound < lower ? bound : lower;
             }
         } else {
             const int man = man_t[Ac];  // min over the side's squares (the level's table)
@@ -888,10 +923,10 @@ struct RowOps {
         float lower = (float)L.perimeter + 1.0f;
         if (s.kind == 1 || s.kind == 3) {  // static B side: one table lookup per A approach
             const int nb = s.kind == 1 ? L.ncut : L.ndeliv;
-            const uint8_t* dm = T + L.dmin_off + (s.kind == 1 ? 0 : L.nnodes);
+            const int side = s.kind == 1 ? 0 : 1;
             const uint16_t* man_t = (const uint16_t*)(T + L.man_off) + (s.kind == 1 ? 0 : L.man_stride);
             visit_objs<HOIST>(br, r, s.start[0], s.kind == 3, [&](int Ac) OC_RL {
-                const float b = helper_static(s, u0, u1, Ac, nb, dm, man_t);
+                const float b = helper_static(s, u0, u1, Ac, nb, side, man_t);
                 if (b < lower) lower = b;
             });
         } else if (s.kind == 2) {

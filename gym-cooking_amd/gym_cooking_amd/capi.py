@@ -21,7 +21,7 @@ OC_MAX_NARROW_CELLS = 255   # up to this many cells: byte cell ids; more ("wide"
 OC_MAX_GOALS = 4
 OC_PITCH_ALIGN = 4096
 OC_NSTATS = 5
-OC_ABI_VERSION = 9  # include/oc_engine.h
+OC_ABI_VERSION = 10  # include/oc_engine.h
 OC_DEVICE_HOST = -1  # oc_create: a host-only handle (no HIP call)
 OC_LIK_FORM_AUTO, OC_LIK_FORM_GROUPED = 0, 1
 OC_EINVAL, OC_EHIP, OC_ELEVEL = -1, -2, -3
@@ -35,7 +35,7 @@ OC_STAT_NAMES = ("episodes", "successes", "steps", "collisions", "errors")
 # Every symbol include/oc_engine.h declares (tests check the library exports them all).
 EXPORTED_SYMBOLS = (
     "oc_abi_version", "oc_last_error", "oc_create", "oc_destroy", "oc_get_layout", "oc_reset",
-    "oc_step", "oc_step_n", "oc_cpu_step", "oc_rollout", "oc_nav_likelihood", "oc_subtask_bounds", "oc_reachability", "oc_render", "oc_render_ordered",
+    "oc_step", "oc_step_n", "oc_cpu_step", "oc_rollout", "oc_nav_likelihood", "oc_subtask_bounds", "oc_reachability", "oc_reachability16", "oc_render", "oc_render_ordered",
     "oc_gen_actions", "oc_state_checksum", "oc_stats_size", "oc_stats_reduce", "oc_get_last_error",
     "oc_set_likelihood_form",
 )
@@ -197,6 +197,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.oc_subtask_bounds.argtypes = [vp, vp, ctypes.POINTER(OcSubtask), i32, vp, vp, i64, vp]
     lib.oc_reachability.restype = ctypes.c_int
     lib.oc_reachability.argtypes = [vp, ctypes.POINTER(i32), vp, i64, vp, i64]
+    lib.oc_reachability16.restype = ctypes.c_int
+    lib.oc_reachability16.argtypes = [vp, ctypes.POINTER(i32), vp, i64, vp, i64]
     lib.oc_render.argtypes = [vp, vp, vp, vp, ctypes.POINTER(OcRenderDesc), vp, i64, vp]
     lib.oc_render_ordered.restype = ctypes.c_int
     lib.oc_render_ordered.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(OcRenderDesc), vp, i64, vp]
@@ -224,8 +226,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 
 class LevelError(RuntimeError):
     """OC_ELEVEL: the level is outside an entry point's envelope (oc_create's validation: more
-    than 1,024 cells, a 17th object or a 4th of one food; the planner entry points: a
-    reachability graph with a BFS distance of 255 or more)."""
+    than 1,024 cells, a 17th object or a 4th of one food; oc_reachability's u8 table: a
+    reachability graph with a BFS distance of 255 or more, which oc_reachability16 exports)."""
 
 
 def check(rc: int) -> None:

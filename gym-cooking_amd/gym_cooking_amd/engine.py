@@ -259,16 +259,17 @@ class OvercookedBatch:
         return buf.value.decode()
 
     def reachability(self):
-        """The level's static reachability graph (oc_reachability): (node_of u16 [W*H*5] with
-        0xFFFF = not a node, dist u8 [n][n] with 0xFF = no path)."""
+        """The level's static reachability graph (oc_reachability16): (node_of u16 [W*H*5] with
+        0xFFFF = not a node, dist u16 [n][n] with 0xFFFF = no path; any level, a maze's BFS
+        distances of 255 and more included)."""
         import ctypes
         n = ctypes.c_int32()
-        capi.check(self.lib.oc_reachability(self._h, ctypes.byref(n), None, 0, None, 0))
+        capi.check(self.lib.oc_reachability16(self._h, ctypes.byref(n), None, 0, None, 0))
         cells = self.level.width * self.level.height
         node_of = np.zeros(cells * 5, np.uint16)
-        dist = np.zeros((n.value, n.value), np.uint8)
-        capi.check(self.lib.oc_reachability(self._h, ctypes.byref(n), node_of.ctypes.data, node_of.size,
-                                            dist.ctypes.data, dist.size))
+        dist = np.zeros((n.value, n.value), np.uint16)
+        capi.check(self.lib.oc_reachability16(self._h, ctypes.byref(n), node_of.ctypes.data, node_of.size,
+                                              dist.ctypes.data, dist.size))
         return node_of, dist
 
     def gen_actions(self, actions: torch.Tensor, step: int, seed: int = 0, env_offset: int = 0) -> torch.Tensor:

@@ -180,6 +180,7 @@ class ReachabilityGraph:
                 c, d = divmod(key, 5)
                 self._id[((c % width, c // width), self._APPROACH[d])] = n
         self._dist = dist
+        self._nopath = 0xFFFF if dist.dtype == np.uint16 else 0xFF  # oc_reachability16 / oc_reachability
 
     def nodes(self) -> list:
         return sorted(self._id, key=self._id.get)
@@ -202,7 +203,7 @@ class ReachabilityGraph:
     def shortest_path_length(self, source, target) -> int:
         """nx.shortest_path_length(reachability_graph, source, target); raises NoPath."""
         u, v = self._id.get(self._key(source)), self._id.get(self._key(target))
-        if u is None or v is None or self._dist[u, v] == 0xFF:
+        if u is None or v is None or self._dist[u, v] == self._nopath:
             raise NoPath("no path between %r and %r" % (source, target))
         return int(self._dist[u, v])
 

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define OC_ABI_VERSION 9
+#define OC_ABI_VERSION 10
 
 #define OC_MAX_AGENTS 4
 #define OC_MAX_ITEMS 16  /* item slots: K = 4, 8 or 16 per level */
@@ -362,10 +362,14 @@ int oc_set_likelihood_form(oc_handle* h, int32_t form);
  * World.get_lower_bound_between(_helper) (world.py:115-283) evaluates over exactly this table.
  * The planner kernels keep the distance table in LDS for a graph of at most 360 nodes, in device
  * memory past that (a narrow level: every node its 255 cells can make; a wide one: up to 5,120).
- * OC_ELEVEL (here and from the planner entry points) for a BFS distance of 255 or more, which the
- * u8 table cannot hold. */
+ * A graph with a BFS distance of 255 or more (a maze kitchen's corridors) has u16 tables, in
+ * device memory (ABI 10; ABI 9 refused it): oc_reachability then fails with OC_ELEVEL when
+ * `dist` is given (the u8 table cannot hold it), and oc_reachability16 gives it. */
 int oc_reachability(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, int64_t node_of_len, uint8_t* dist,
                     int64_t dist_len);
+/* The same with u16 distances (0xFFFF = no path), for every level (ABI 10). */
+int oc_reachability16(const oc_handle* h, int32_t* num_nodes, uint16_t* node_of, int64_t node_of_len, uint16_t* dist,
+                      int64_t dist_len);
 
 /* ---------------------------------------------------------------------------------------
  * Subtask bounds on full environment states (no planner Level-0 view): for every env e and

@@ -14,7 +14,7 @@ HEADER = os.path.join(tl.ROOT, "include", "oc_engine.h")
 
 def _declared():
     src = open(HEADER).read()
-    decl = r"^(?:int|void|const char\s*\*)\s*\*?\s*(oc_[a-z_]+)\s*\("  # function declarations
+    decl = r"^(?:int|void|const char\s*\*)\s*\*?\s*(oc_[a-z_0-9]+)\s*\("  # function declarations
     return sorted(set(re.findall(decl, src, re.M)))
 
 

@@ -2,10 +2,16 @@
 narrow level's planner kernels hold in LDS:
   * widegraph-24x24_salad: 576 cells (wide: u16 cell ids), a 605-node graph;
   * dense-15x17_salad: 255 cells (narrow: byte cell ids), a 417-node graph (round 5; round 4
-    refused it with OC_ELEVEL).
+    refused it with OC_ELEVEL);
+  * maze-31x31_salad: 961 cells (wide), a serpentine whose BFS distances pass 255 (about 450
+    edges end to end): u16 distance tables (round 6; round 5 refused it with OC_ELEVEL);
+  * corridor-255x4_salad: 1,020 cells, a 255-column corridor with distances of 250 and more
+    below its perimeter (518), so its subtask bounds past 255 are exact values, not the
+    perimeter + 1 the maze's saturate to (round 6).
 Their planner kernels stage the level's other tables in LDS and read the distance table from
 device memory (oc_rollout.h, RollLevel.dist_global).  Pinned on the CPU to the reference's own
-runs of the level files (tests/golden/gen_widegraph.py, gen_densegraph.py):
+runs of the level files (tests/golden/gen_widegraph.py, gen_densegraph.py, gen_mazegraph.py,
+gen_corridorgraph.py):
 
 * the parser and the engine's graph (node count, and the BFS distance of 400 random node pairs
   against the reference's nx.shortest_path_length);
@@ -29,7 +35,9 @@ from oracle import oracle
 
 NAME = "widegraph-24x24_salad"
 # kitchen -> (fixture prefix, wide layout)
-KITCHENS = {"widegraph-24x24_salad": ("widegraph", True), "dense-15x17_salad": ("densegraph", False)}
+KITCHENS = {"widegraph-24x24_salad": ("widegraph", True), "dense-15x17_salad": ("densegraph", False),
+            "maze-31x31_salad": ("mazegraph", True), "corridor-255x4_salad": ("corridorgraph", True)}
+LONG = ("maze-31x31_salad", "corridor-255x4_salad")  # BFS distances of 255 and more: u16 tables
 
 
 def _info(name=NAME):
@@ -38,19 +46,20 @@ def _info(name=NAME):
 
 
 def _graph(lv):
-    """The engine's graph (oc_reachability, a host-only handle): node count, node_of
-    [cells * 5], dist [n * n]."""
+    """The engine's graph (oc_reachability16, a host-only handle): node count, node_of
+    [cells * 5], dist [n * n] (u16, 0xFFFF = no path)."""
     lib = capi.load_library()
     d = capi.level_desc(lv, 2)
     h = ctypes.c_void_p()
     capi.check(lib.oc_create(ctypes.byref(d), 2, 100, capi.OC_DEVICE_HOST, ctypes.byref(h)))
     try:
         n = ctypes.c_int32()
-        capi.check(lib.oc_reachability(h, ctypes.byref(n), None, 0, None, 0))
+        capi.check(lib.oc_reachability16(h, ctypes.byref(n), None, 0, None, 0))
         node_of = np.zeros(lv.ncells * 5, np.uint16)
-        dist = np.zeros(n.value * n.value, np.uint8)
-        capi.check(lib.oc_reachability(h, ctypes.byref(n), node_of.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
-                                       len(node_of), dist.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), len(dist)))
+        dist = np.zeros(n.value * n.value, np.uint16)
+        capi.check(lib.oc_reachability16(h, ctypes.byref(n), node_of.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
+                                         len(node_of), dist.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
+                                         len(dist)))
     finally:
         lib.oc_destroy(h)
     return n.value, node_of, dist.reshape(n.value, n.value)
@@ -81,9 +90,36 @@ def test_widegraph_level_matches_reference_graph(name):
         v = int(node_of[(vy * lv.width + vx) * 5 + _NAV[tuple(vd)]])
         assert u != 0xFFFF and v != 0xFFFF
         got = int(dist[u, v])
-        assert (got if got != 0xFF else -1) == d, ((ux, uy), ud, (vx, vy), vd, got, d)
+        assert (got if got != 0xFFFF else -1) == d, ((ux, uy), ud, (vx, vy), vd, got, d)
         checked += 1
     assert checked == 400
+    if name in LONG:  # the reason for these kitchens: distances a byte cannot hold
+        assert max(p[4] for p in ref["dist_pairs"]) >= 255 and int(dist.max(initial=0, where=dist != 0xFFFF)) >= 255
+
+
+def test_u8_reachability_refuses_only_the_long_graph():
+    """oc_reachability's u8 table holds every graph whose BFS distances stay below 255 (the
+    same bytes as oc_reachability16's low bytes there); on the maze it refuses the table with
+    OC_ELEVEL (the node count and node ids still come back), and oc_reachability16 gives it."""
+    lib = capi.load_library()
+    for name in sorted(KITCHENS):
+        lv = levels.load_level(tw._path(name))
+        d = capi.level_desc(lv, 2)
+        h = ctypes.c_void_p()
+        capi.check(lib.oc_create(ctypes.byref(d), 2, 100, capi.OC_DEVICE_HOST, ctypes.byref(h)))
+        try:
+            n = ctypes.c_int32()
+            capi.check(lib.oc_reachability(h, ctypes.byref(n), None, 0, None, 0))
+            d8 = np.zeros(n.value * n.value, np.uint8)
+            rc = lib.oc_reachability(h, ctypes.byref(n), None, 0, d8.ctypes.data, len(d8))
+            _, _, d16 = _graph(lv)
+            if name in LONG:
+                assert rc == capi.OC_ELEVEL and b"oc_reachability16" in lib.oc_last_error()
+            else:
+                assert rc == 0 and int(d16[d16 != 0xFFFF].max()) < 255
+                assert np.array_equal(d8.reshape(d16.shape), np.where(d16 == 0xFFFF, 0xFF, d16).astype(np.uint8))
+        finally:
+            lib.oc_destroy(h)
 
 
 @KIT

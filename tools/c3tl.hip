@@ -507,13 +507,25 @@ int main(int argc, char** argv) {
         printf("%-44s %8.3f us/step  outputs %s\n", name, ms * 1e3 / 10 / n,
                same && same2 ? "identical to lw" : "DIFFER from lw");
     };
-    seg("seg 20 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 20>, 3);
-    seg("seg 20 steps, 4 blocks/CU", stepn_seg<3, 4, 0, 20>, 4);
-    seg("seg 10 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 10>, 3);
-    seg("seg 25 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 25>, 3);
-    seg("seg 50 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 50>, 3);
-    seg("seg 100 steps (queue only), 3 blocks/CU", stepn_seg<3, 4, 0, 100>, 3);
-    time("lw (product form) again", stepn_tl<3, 4, 0, true, false, false>, true);
+    if (getenv("C3TL_SEG")) {  // pass A of round 6 (profiles/r06/pass_a/c3tl.log)
+        seg("seg 20 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 20>, 3);
+        seg("seg 20 steps, 4 blocks/CU", stepn_seg<3, 4, 0, 20>, 4);
+        seg("seg 10 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 10>, 3);
+        seg("seg 25 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 25>, 3);
+        seg("seg 50 steps, 3 blocks/CU", stepn_seg<3, 4, 0, 50>, 3);
+        seg("seg 100 steps (queue only), 3 blocks/CU", stepn_seg<3, 4, 0, 100>, 3);
+    }
+    // round 6, pass C: blocks of more stepping waves per loader (fewer loader waves, and at 8
+    // stepping waves every block of a 2^20-env launch is resident at once: 512 blocks of 9 waves,
+    // two per CU), against the product form, alternating
+    for (int rep = 0; rep < 3; ++rep) {
+        time("lw (product form)", stepn_tl<3, 4, 0, true, false, false>, true);
+        time("lw, 8 stepping waves + loader, 2 blocks/CU", stepn_tl<3, 4, 0, true, false, false, 8, 2>, true, 8, 2);
+        time("lw, 6 stepping waves + loader, 3 blocks/CU", stepn_tl<3, 4, 0, true, false, false, 6, 3>, true, 6, 3);
+        time("lw, launch bounds 6 waves per SIMD", stepn_tl<3, 4, 0, true, false, false, 4, 6>, true);
+    }
+    time("lw8 + stamps", stepn_tl<3, 4, 0, true, false, true, 8, 2>, true, 8, 2);
+    report("lw8");
     // the product launch, for reference (C-ABI, with the statistics)
     uint64_t* stats;
     int64_t nb;

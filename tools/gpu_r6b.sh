@@ -18,3 +18,6 @@ print('$m', $r, '%.4g' % d['value'], 'win %.1f us' % (d['ms_per_step']*20e3), 'k
 done
 timeout -k 10 600 python tools/bounds_ab.py --libs gym-cooking_amd/gym_cooking_amd/liboc_engine.so tools/ab_libs/lib_roll256.so --rounds 3 > $O/ab_roll_small.jsonl 2> $O/ab_roll_small.err || { echo AB_FAILED; tail -20 $O/ab_roll_small.err; exit 1; }
 cat $O/ab_roll_small.jsonl
+timeout -k 10 600 python -u -m pytest tests/test_widegraph_gpu.py tests/test_widelevels_gpu.py tests/test_biglevels_gpu.py tests/test_rollout_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread -k "not maze" > $O/gputest_graphs.log 2>&1 \
+  || { echo PYTEST_FAILED; grep -E "FAILED|Error|error" $O/gputest_graphs.log | head -20; tail -30 $O/gputest_graphs.log; exit 1; }
+tail -1 $O/gputest_graphs.log
