@@ -47,10 +47,55 @@ def main():
     generate(LEVELS, BOUND_CONFIGS, ROLL_CONFIGS, "widegraph", pair_seed=605, gid0=12700)
 
 
+_DIST_MEMO = {}
+
+
+def _cache_distances_bfs(self):
+    """OvercookedEnvironment.cache_distances (overcooked_environment.py:775-821) with one BFS per
+    source node (nx.single_source_shortest_path_length) instead of one nx.shortest_path_length
+    per (source, destination, approach pair): the same dict, entry for entry and in the same
+    insertion order (on an unweighted graph shortest_path_length is the BFS distance; a missing
+    node or no path leaves the pair out of the min, np.inf when none is left; a source's own
+    entry is overwritten by the loop, as in the reference), computed once per level.  Every
+    reset() calls it; the original makes ~W^2 H^2 BFS calls, hours on a 961-cell kitchen.  The
+    reference only caches and copies env.distances (:105, world.py:39): no recorded value reads it."""
+    import networkx as nx
+    from utils.world import World
+    key = self.arglist.level
+    if key not in _DIST_MEMO:
+        g = self.world.reachability_graph
+        names = [n for n in self.world.objects if "Supply" in n or "Counter" in n or "Delivery" in n or "Cut" in n]
+        src = copy.copy(self.world.objects["Floor"])
+        for n in names:
+            src += copy.copy(self.world.objects[n])
+        edges = lambda o: [(0, 0)] if not o.collidable else World.NAV_ACTIONS  # noqa: E731
+        bfs = {}
+        for o in src:
+            for e in edges(o):
+                node = (o.location, e)
+                bfs[node] = nx.single_source_shortest_path_length(g, node) if node in g else {}
+        dist = {}
+        for s_ in src:
+            dist[s_.location] = {s_.location: 0}
+            for d_ in src:
+                best = np.inf
+                for se in edges(s_):
+                    row = bfs[(s_.location, se)]
+                    for de in edges(d_):
+                        v = row.get((d_.location, de))
+                        if v is not None and v < best:
+                            best = v
+                dist[s_.location][d_.location] = best
+        _DIST_MEMO[key] = dist
+    self.distances = _DIST_MEMO[key]
+    self.world.distances = self.distances
+
+
 def generate(LEVELS, BOUND_CONFIGS, ROLL_CONFIGS, prefix, pair_seed, gid0):
     """Record <prefix>.json (tables, graph size, 400 reference BFS distances), <prefix>.npz
     (episodes), bounds_<prefix>.npz and rollout_<prefix>.npz for the kitchens LEVELS."""
     ref = gg.load_reference()
+    ref[0].cache_distances = _cache_distances_bfs
     gg.MAXK = 8
     gr.canon = gd.canon_k
     scratch = tempfile.mkdtemp(prefix="oc_%s_" % prefix)

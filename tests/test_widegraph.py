@@ -5,8 +5,8 @@ narrow level's planner kernels hold in LDS:
     refused it with OC_ELEVEL);
   * maze-31x31_salad: 961 cells (wide), a serpentine whose BFS distances pass 255 (about 450
     edges end to end): u16 distance tables (round 6; round 5 refused it with OC_ELEVEL);
-  * corridor-255x4_salad: 1,020 cells, a 255-column corridor with distances of 250 and more
-    below its perimeter (518), so its subtask bounds past 255 are exact values, not the
+  * corridor-204x5_salad: 1,020 cells, two lanes joined at one end (a U), distances to about 410
+    below its perimeter (418), so its subtask bounds past 255 are exact values, not the
     perimeter + 1 the maze's saturate to (round 6).
 Their planner kernels stage the level's other tables in LDS and read the distance table from
 device memory (oc_rollout.h, RollLevel.dist_global).  Pinned on the CPU to the reference's own
@@ -36,8 +36,8 @@ from oracle import oracle
 NAME = "widegraph-24x24_salad"
 # kitchen -> (fixture prefix, wide layout)
 KITCHENS = {"widegraph-24x24_salad": ("widegraph", True), "dense-15x17_salad": ("densegraph", False),
-            "maze-31x31_salad": ("mazegraph", True), "corridor-255x4_salad": ("corridorgraph", True)}
-LONG = ("maze-31x31_salad", "corridor-255x4_salad")  # BFS distances of 255 and more: u16 tables
+            "maze-31x31_salad": ("mazegraph", True), "corridor-204x5_salad": ("corridorgraph", True)}
+LONG = ("maze-31x31_salad", "corridor-204x5_salad")  # BFS distances of 255 and more: u16 tables
 
 
 def _info(name=NAME):
