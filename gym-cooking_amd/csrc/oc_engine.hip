@@ -1071,25 +1071,26 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
 }
 
 // ---- wide levels (more than 255 cells: u16 cell ids) ----------------------------------------
-// The byte-cell SWAR step does not reach past 255 cells; a wide level steps one env per lane
-// with the scalar restatement of the same rules (ocro::RowOps::env_step), over
-// byte-plane loads and stores (64 consecutive bytes per wave instruction).  Such levels are
-// user kitchens; the shipped ones are all narrow.
+// A wide level (more than 255 cells, u16 cell ids) is stepped by ocsw::step4w: the SWAR step
+// with every cell-valued quantity as two byte words (its low and high bytes, the wide layout's
+// two item-cell planes), four envs per lane like oc_step_n_kernel (round 6; rounds 4-5 ran the
+// scalar RowOps::env_step, one env after another).  Such levels are user kitchens; the shipped
+// ones are all narrow.
 struct WideArgs {
     ocro::RollLevel L;   // W, H, enc; tile_off 0: the table below
     ocro::StepLevel S;
-    int32_t tile_words;  // the tile-class table's words (W * H bytes rounded up to 4)
+    ocsw::SwarLevel sw;  // the SWAR step's constants (step4w reads the wide fields)
+    int32_t tile_words;  // the tile table's words (W * H bytes rounded up to 4)
     int64_t pitch, B;
 };
 
 // n steps of every env (oc_step: n = 1, no trajectory): the state stays in registers between
 // the steps; step r's state goes to traj[r] (when given), its executed actions and collision
-// mask to exec_out / coll_out at r * A * pitch / r * pitch; the final state to sout.
-// Round 5: four envs per lane, every plane read and written one dword per lane (256 B per wave
-// instruction, as the narrow kernels; round 4 moved one byte per lane, 64 B per instruction),
+// mask to exec_out / coll_out at r * A * pitch / r * pitch; the final state to sout.  Four envs
+// per lane, every plane read and written one dword per lane (256 B per wave instruction)
 // through buffer resources (an absent output's stores are dropped by its num_records = 0, so
-// every store is unconditional), nt stores, and the next step's action words loaded before the
-// current step runs.  The four envs step one after another through the scalar env_step.
+// every store is unconditional), nt stores, the next step's action words loaded before the
+// current step runs.
 template <int A, int K>
 __global__ __launch_bounds__(kBlock) void oc_step_wide_kernel(WideArgs R, const uint8_t* __restrict__ tiles_g,
                                                               const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
@@ -1097,11 +1098,23 @@ __global__ __launch_bounds__(kBlock) void oc_step_wide_kernel(WideArgs R, const 
                                                               uint8_t* __restrict__ traj, uint8_t* __restrict__ exec_out,
                                                               uint8_t* __restrict__ coll_out, uint64_t* __restrict__ stats,
                                                               uint32_t stat_rows, int n) {
-    __shared__ uint32_t tiles_w[ocro::kMaxCellsWide / 4];
-    for (int i = threadIdx.x; i < R.tile_words; i += kBlock) tiles_w[i] = ((const uint32_t*)tiles_g)[i];
+    // tile class bytes (ocsw::tile_class: Floor 0x80, Counter 0, Cutboard 0x20, Delivery 0x40)
+    // of the OC_TILE_* codes, one v_perm per word
+    __shared__ uint32_t cls_w[ocro::kMaxCellsWide / 4];
+    for (int i = threadIdx.x; i < R.tile_words; i += kBlock)
+        cls_w[i] = __builtin_amdgcn_perm(0u, 0x40200080u, ((const uint32_t*)tiles_g)[i]);
     __syncthreads();
+    const uint8_t* cls_b = (const uint8_t*)cls_w;
+    auto cls_of = [&](const ocsw::Cell2& c) -> uint32_t {  // per env: the class of cell (hi << 8 | lo)
+        uint32_t r = 0u;
+#pragma unroll
+        for (int q = 0; q < kEPL; ++q) {
+            const uint32_t idx = __builtin_amdgcn_perm(c.hi >> (8 * q), c.lo >> (8 * q), 0x0C0C0400u) & 0x3FFu;
+            r |= (uint32_t)cls_b[idx] << (8 * q);
+        }
+        return r;
+    };
     using PL = Planes<A, K, true>;
-    using Row = ocro::RowT<K, true>;
     const uint32_t P = (uint32_t)R.pitch;
     const uint32_t nlanes = (uint32_t)((R.B + kEPL - 1) / kEPL);
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(sin, (int64_t)PL::NP * P);
@@ -1112,7 +1125,6 @@ __global__ __launch_bounds__(kBlock) void oc_step_wide_kernel(WideArgs R, const 
                                                 exec_out ? (int64_t)n * A * P : 0);
     const __amdgpu_buffer_rsrc_t rc = make_rsrc(coll_out ? (const void*)coll_out : (const void*)sin,
                                                 coll_out ? (int64_t)n * P : 0);
-    ocro::RowOps<A, K, true> ops(R.L, (const uint8_t*)tiles_w);
     StepStats st;
     typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
     for (uint32_t g = blockIdx.x * (uint32_t)kBlock + threadIdx.x; g < nlanes; g += gridDim.x * (uint32_t)kBlock) {
@@ -1132,71 +1144,27 @@ __global__ __launch_bounds__(kBlock) void oc_step_wide_kernel(WideArgs R, const 
             M[j] = bld32(rs, vo, (PL::M + j) * P);
         }
         const auto tw0 = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(g * 8u), (int)(PL::T * P), 0);
-        uint32_t T[2] = {tw0[0], tw0[1]}, F = bld32(rs, vo, PL::F * P);
+        uint32_t T0 = tw0[0], T1 = tw0[1], F = bld32(rs, vo, PL::F * P);
+        uint32_t pending = ocsw::at_done80w<K>(R.sw, LO, HI);  // the loaded state: the full path once
         const int64_t rem = R.B - (int64_t)g * kEPL;
+        const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (rem <= 0 ? 0u : (1u << (8 * (uint32_t)rem)) - 1u);
         for (int q = 0; q < n; ++q) {
 #pragma unroll
             for (int a = 0; a < A; ++a) nx[a] = q + 1 < n ? bld32(ra, vo, (uint32_t)((q + 1) * A + a) * P) : 0u;
-            uint32_t EX[A], CM = 0u;
-#pragma unroll
-            for (int a = 0; a < A; ++a) EX[a] = 0u;
-#pragma unroll
-            for (int k = 0; k < kEPL; ++k) {  // the lane's four envs, one after another
-                // a column past B (the batch's last word) is not stepped: its bytes go back out as
-                // they came in, with no-op executed actions and no collision (its cells may be
-                // any u16, which env_step would use as tile-table indices)
-                if (k >= rem) {
-#pragma unroll
-                    for (int a = 0; a < A; ++a) EX[a] |= 4u << (8 * k);
-                    continue;
-                }
-                const int sh = 8 * k;
-                Row r;
-#pragma unroll
-                for (int a = 0; a < A; ++a) {
-                    r.x |= ((X[a] >> sh) & 0xFFu) << (8 * a);
-                    r.y |= ((Y[a] >> sh) & 0xFFu) << (8 * a);
-                    r.h |= ((H[a] >> sh) & 0xFFu) << (8 * a);
-                }
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    const uint64_t c = ((LO[j] >> sh) & 0xFFu) | (((HI[j] >> sh) & 0xFFu) << 8);
-                    r.loc[j / Row::LPW] |= c << (Row::kLocBits * (j % Row::LPW));
-                    r.mask[j >> 3] |= (uint64_t)((M[j] >> sh) & 0xFFu) << (8 * (j & 7));
-                }
-                uint32_t t = (T[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                const uint32_t fl = (F >> sh) & 0xFFu;
-                uint32_t av = 0u, ex, cm;
-#pragma unroll
-                for (int a = 0; a < A; ++a) av |= ((wa[a] >> sh) & 0xFFu) << (8 * a);
-                const uint32_t f = ops.env_step(r, t, fl, av, R.S, ex, cm);
-                if (k < rem) {  // statistics over the batch's envs only
-                    if ((f & 1u) && !(fl & 1u)) {  // an episode ended (DONE newly set)
-                        st.eps += 1u;
-                        st.succ += (f >> 1) & 1u;
-                        st.err += (f >> 2) & 1u;
-                        st.steps += t;
-                    }
-                    st.coll += __popc(cm);
-                }
-                const uint32_t keep = ~(0xFFu << sh);
-#pragma unroll
-                for (int a = 0; a < A; ++a) {
-                    X[a] = (X[a] & keep) | ((uint32_t)r.ax(a) << sh);
-                    Y[a] = (Y[a] & keep) | ((uint32_t)r.ay(a) << sh);
-                    H[a] = (H[a] & keep) | ((uint32_t)r.ah(a) << sh);
-                    EX[a] |= ((ex >> (8 * a)) & 0xFFu) << sh;
-                }
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    const uint32_t c = (uint32_t)r.il(j);
-                    LO[j] = (LO[j] & keep) | ((c & 0xFFu) << sh);
-                    HI[j] = (HI[j] & keep) | ((c >> 8) << sh);
-                    M[j] = (M[j] & keep) | ((uint32_t)r.im(j) << sh);
-                }
-                T[k >> 1] = (T[k >> 1] & ~(0xFFFFu << (16 * (k & 1)))) | (t << (16 * (k & 1)));
-                F = (F & keep) | (f << sh);
-                CM |= cm << sh;
+            uint32_t EX[A], CM;
+            const uint32_t f_in = F;
+            const bool full = ocsw::step4w<A, K>(R.sw, X, Y, H, LO, HI, M, T0, T1, F, wa, EX, CM, cls_of, WaveAny{},
+                                                 pending);
+            st.coll += __popc(CM & vmask);
+            if (full) {  // episode ends only on the full path
+                const uint32_t ended = (F & ~f_in & vmask) & ocsw::k01;
+                st.eps += __popc(ended);
+                st.succ += __popc(F & (ended << 1));
+                st.err += __popc(F & (ended << 2));
+                const uint32_t efull = (0x80808080u - ended) ^ 0x80808080u;
+                const uint32_t sa = T0 & __builtin_amdgcn_perm(0u, efull, 0x01010000u);
+                const uint32_t sb2 = T1 & __builtin_amdgcn_perm(0u, efull, 0x03030202u);
+                st.steps += (sa & 0xFFFFu) + (sa >> 16) + (sb2 & 0xFFFFu) + (sb2 >> 16);
             }
             const uint32_t base = (uint32_t)q * PL::NP * P;
 #pragma unroll
@@ -1212,7 +1180,7 @@ __global__ __launch_bounds__(kBlock) void oc_step_wide_kernel(WideArgs R, const 
                 bst32<kCPnt>(rt, HI[j], vo, base + (PL::LH + j) * P);
                 bst32<kCPnt>(rt, M[j], vo, base + (PL::M + j) * P);
             }
-            const u32x2 tv = {T[0], T[1]};
+            const u32x2 tv = {T0, T1};
             __builtin_amdgcn_raw_buffer_store_b64(tv, rt, (int)(g * 8u), (int)(base + PL::T * P), kCPnt);
             bst32<kCPnt>(rt, F, vo, base + PL::F * P);
             bst32<kCPnt>(rc, CM, vo, (uint32_t)q * P);
@@ -1231,7 +1199,7 @@ __global__ __launch_bounds__(kBlock) void oc_step_wide_kernel(WideArgs R, const 
             bst32<kCPnt>(ro, HI[j], vo, (PL::LH + j) * P);
             bst32<kCPnt>(ro, M[j], vo, (PL::M + j) * P);
         }
-        const u32x2 tv = {T[0], T[1]};
+        const u32x2 tv = {T0, T1};
         __builtin_amdgcn_raw_buffer_store_b64(tv, ro, (int)(g * 8u), (int)(PL::T * P), kCPnt);
         bst32<kCPnt>(ro, F, vo, PL::F * P);
     }
@@ -1780,52 +1748,87 @@ static void cpu_step_words(const oc_handle* h, const uint8_t* sin, uint8_t* sout
     st[OC_STAT_ERRORS] = err;
 }
 
-// oc_cpu_step on a wide level: envs [e0, e1) through the host pass of the scalar step
+// oc_cpu_step on a wide level: words [g0, g1) (4 envs each) through the host pass of the
+// wide SWAR step (ocsw::step4w), per-word rare-event split, as oc_step_wide_kernel
 template <int A, int K>
 static void cpu_step_wide(const oc_handle* h, const uint8_t* sin, uint8_t* sout, const uint8_t* act, uint8_t* exo,
-                          uint8_t* coll, int64_t P, int64_t e0, int64_t e1, uint64_t* st) {
+                          uint8_t* coll, int64_t B, int64_t P, int64_t g0, int64_t g1, uint64_t* st) {
     using PL = Planes<A, K, true>;
-    using Row = ocro::RowT<K, true>;
+    const ocsw::SwarLevel& SL = h->args.sw;
+    uint8_t cls[ocro::kMaxCellsWide];
+    for (int c = 0; c < ocro::kMaxCellsWide; ++c) cls[c] = ocsw::tile_class(h->wide_tiles_host[c]);
+    auto cls_of = [&cls](const ocsw::Cell2& c) -> uint32_t {
+        uint32_t r = 0u;
+        for (int q = 0; q < kEPL; ++q) {
+            const uint32_t idx = ((((c.hi >> (8 * q)) & 0xFFu) << 8) | ((c.lo >> (8 * q)) & 0xFFu)) & 0x3FFu;
+            r |= (uint32_t)cls[idx] << (8 * q);
+        }
+        return r;
+    };
+    auto rd = [P](const uint8_t* base, int plane, int64_t g) {
+        uint32_t v;
+        memcpy(&v, base + plane * P + 4 * g, 4);
+        return v;
+    };
+    auto wr = [P](uint8_t* base, int plane, int64_t g, uint32_t v) { memcpy(base + plane * P + 4 * g, &v, 4); };
     uint64_t eps = 0, succ = 0, steps = 0, ncoll = 0, err = 0;
-    ocro::RowOps<A, K, true> ops(h->step_lv, h->wide_tiles_host);
-    for (int64_t e = e0; e < e1; ++e) {
-        Row r;
+    for (int64_t g = g0; g < g1; ++g) {
+        uint32_t X[A], Y[A], Hh[A], LL[K], LH[K], M[K], AC[A], EX[A], T0, T1, F, CM;
         for (int a = 0; a < A; ++a) {
-            r.x |= (uint32_t)sin[a * P + e] << (8 * a);
-            r.y |= (uint32_t)sin[(PL::Y + a) * P + e] << (8 * a);
-            r.h |= (uint32_t)sin[(PL::H + a) * P + e] << (8 * a);
+            X[a] = rd(sin, PL::X + a, g);
+            Y[a] = rd(sin, PL::Y + a, g);
+            Hh[a] = rd(sin, PL::H + a, g);
+            AC[a] = rd(act, a, g);
         }
         for (int j = 0; j < K; ++j) {
-            r.set_loc(j, (uint32_t)sin[(PL::L + j) * P + e] | ((uint32_t)sin[(PL::LH + j) * P + e] << 8));
-            r.set_mask(j, sin[(PL::M + j) * P + e]);
+            LL[j] = rd(sin, PL::L + j, g);
+            LH[j] = rd(sin, PL::LH + j, g);
+            M[j] = rd(sin, PL::M + j, g);
         }
-        uint32_t t = (uint32_t)sin[PL::T * P + 2 * e] | ((uint32_t)sin[PL::T * P + 2 * e + 1] << 8);
-        const uint32_t fl = sin[PL::F * P + e];
-        uint32_t a4 = 0, ex, cm;
-        for (int a = 0; a < A; ++a) a4 |= (uint32_t)act[a * P + e] << (8 * a);
-        const uint32_t f = ops.env_step(r, t, fl, a4, h->step, ex, cm);
-        if ((f & 1u) && !(fl & 1u)) {
-            ++eps;
-            succ += (f >> 1) & 1u;
-            err += (f >> 2) & 1u;
-            steps += t;
+        memcpy(&T0, sin + PL::T * P + 8 * g, 4);
+        memcpy(&T1, sin + PL::T * P + 8 * g + 4, 4);
+        F = rd(sin, PL::F, g);
+        const uint32_t f_in = F;
+        uint32_t pending = ocsw::at_done80w<K>(SL, LL, LH);
+        const bool full = ocsw::step4w<A, K>(SL, X, Y, Hh, LL, LH, M, T0, T1, F, AC, EX, CM, cls_of,
+                                             [](uint32_t v) { return v != 0u; }, pending);
+        const int64_t rem = B - g * kEPL;
+        const uint32_t vmask = rem >= kEPL ? 0xFFFFFFFFu : (1u << (8 * (uint32_t)rem)) - 1u;
+        ncoll += (uint64_t)__builtin_popcount(CM & vmask);
+        if (full) {
+            const uint32_t ended = (F & ~f_in & vmask) & ocsw::k01;
+            for (int q = 0; q < kEPL; ++q) {
+                if (!((ended >> (8 * q)) & 1u)) continue;
+                ++eps;
+                succ += (F >> (8 * q + 1)) & 1u;
+                err += (F >> (8 * q + 2)) & 1u;
+                steps += ((q < 2 ? T0 : T1) >> (16 * (q & 1))) & 0xFFFFu;
+            }
         }
-        ncoll += (uint64_t)__builtin_popcount(cm);
+        // the batch's last word: only its columns below B are written (a host caller's buffer
+        // may be exactly B bytes per plane past the pitch's start)
+        const int ncol = rem >= kEPL ? kEPL : (int)rem;
+        auto put = [&](uint8_t* base, int plane, uint32_t v) {
+            if (ncol == kEPL) wr(base, plane, g, v);
+            else memcpy(base + plane * P + 4 * g, &v, (size_t)ncol);
+        };
         for (int a = 0; a < A; ++a) {
-            sout[a * P + e] = (uint8_t)r.ax(a);
-            sout[(PL::Y + a) * P + e] = (uint8_t)r.ay(a);
-            sout[(PL::H + a) * P + e] = (uint8_t)r.ah(a);
-            if (exo != nullptr) exo[a * P + e] = (uint8_t)(ex >> (8 * a));
+            put(sout, PL::X + a, X[a]);
+            put(sout, PL::Y + a, Y[a]);
+            put(sout, PL::H + a, Hh[a]);
+            if (exo != nullptr) put(exo, a, EX[a]);
         }
         for (int j = 0; j < K; ++j) {
-            sout[(PL::L + j) * P + e] = (uint8_t)r.il(j);
-            sout[(PL::LH + j) * P + e] = (uint8_t)(r.il(j) >> 8);
-            sout[(PL::M + j) * P + e] = (uint8_t)r.im(j);
+            put(sout, PL::L + j, LL[j]);
+            put(sout, PL::LH + j, LH[j]);
+            put(sout, PL::M + j, M[j]);
         }
-        sout[PL::T * P + 2 * e] = (uint8_t)t;
-        sout[PL::T * P + 2 * e + 1] = (uint8_t)(t >> 8);
-        sout[PL::F * P + e] = (uint8_t)f;
-        if (coll != nullptr) coll[e] = (uint8_t)cm;
+        uint8_t tb[8];
+        memcpy(tb, &T0, 4);
+        memcpy(tb + 4, &T1, 4);
+        memcpy(sout + PL::T * P + 8 * g, tb, (size_t)(2 * ncol));
+        put(sout, PL::F, F);
+        if (coll != nullptr) put(coll, 0, CM);
     }
     st[OC_STAT_EPISODES] = eps;
     st[OC_STAT_SUCCESSES] = succ;
@@ -1930,9 +1933,16 @@ int oc_create(const oc_level_desc* lv, int32_t num_agents, int32_t max_T, int32_
     L.max_T = max_T;
     const int dcell[5] = {W, -W, -1, 1, 0};
     for (int c = 0; c < 5; ++c) L.dcell_lut |= (uint64_t)((dcell[c] + 128) & 0xFF) << (8 * c);
-    if (!wide)
-        ocsw::build_swar_level(L.sw, W, H, L.done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x,
-                               lv->spawn_y, num_agents, cell8, mask, lv->encoding, lv->tiles);
+    ocsw::build_swar_level(L.sw, W, H, L.done_cell, lv->goal_mask, lv->num_goals, max_T, lv->spawn_x, lv->spawn_y,
+                           num_agents, cell8, mask, lv->encoding, lv->tiles);
+    if (wide) {  // step4w: u16 cells as low / high byte words (the LUTs, x / y and W - 1 stay bytes)
+        L.sw.done_rep = (uint32_t)(L.done_cell & 0xFF) * 0x01010101u;
+        L.sw.done_hi_rep = (uint32_t)(L.done_cell >> 8) * 0x01010101u;
+        for (int j = 0; j < 16; ++j) {
+            L.sw.tmpl_l[j] = (uint32_t)(cell[j] & 0xFF) * 0x01010101u;
+            L.sw.tmpl_lh[j] = (uint32_t)(cell[j] >> 8) * 0x01010101u;
+        }
+    }
     oc_handle* h = new oc_handle;
     h->wide = wide;
     h->step = ocro::StepLevel{};
@@ -2173,6 +2183,7 @@ static int step_wide(const oc_handle* h, const void* sin, void* sout, const uint
     WideArgs R;
     R.L = h->step_lv;
     R.S = h->step;
+    R.sw = h->args.sw;
     R.tile_words = (h->level.width * h->level.height + 3) / 4;
     R.pitch = pitch_for(B);
     R.B = B;
@@ -2218,6 +2229,7 @@ int oc_reset(const oc_handle* h, void* state, int64_t B, void* stream) {
         WideArgs R;
         R.L = h->step_lv;
         R.S = h->step;
+        R.sw = h->args.sw;
         R.tile_words = 0;
         R.pitch = pitch_for(B);
         R.B = B;
@@ -2280,9 +2292,8 @@ int oc_cpu_step(const oc_handle* h, const void* state_in, void* state_out, const
         const uint8_t* si = (const uint8_t*)state_in;
         uint8_t* so = (uint8_t*)state_out;
         uint64_t* st = part.data() + i * OC_NSTATS;
-        if (h->wide) {  // one env at a time; the ranges are in words of 4 envs
-            const int64_t e0 = 4 * g0, e1 = 4 * g1 < B ? 4 * g1 : B;
-#define OC_CPU_WSTEP(A, K) cpu_step_wide<A, K>(h, si, so, actions, exec_actions, coll_mask, P, e0, e1, st)
+        if (h->wide) {  // the wide SWAR step (step4w), four envs per word as the kernel
+#define OC_CPU_WSTEP(A, K) cpu_step_wide<A, K>(h, si, so, actions, exec_actions, coll_mask, B, P, g0, g1, st)
             OC_DISPATCH(h->A, h->K, OC_CPU_WSTEP)
 #undef OC_CPU_WSTEP
             return OC_OK;

@@ -100,7 +100,7 @@ struct RollLevel {  // scalars (kernel argument); the tables are in the blob
                          // implies dist_global (round 6)
 };
 
-// The environment step's level constants (the scalar step of wide levels, RowOps::env_step).
+// A wide level's reset template (oc_reset_wide_kernel).
 struct StepLevel {
     int32_t done_cell;  // first Delivery in scan order (done() reads only it, overcooked_environment.py:349)
     int32_t max_T;      // 0 = no limit
@@ -982,99 +982,6 @@ struct RowOps {
         else if (is_goal(r, s)) fl |= 2;
         lb = lower_bound(r, s);
         return fl;
-    }
-
-    // ---- the environment step (OvercookedEnvironment.step, overcooked_environment.py:255-306),
-    // one env: the scalar step of the wide levels, the same rules as ocsw::step4.
-
-    // is_collision (overcooked_environment.py:671-722) of agents i, j with the original action
-    // codes ci, cj: the next squares (unclamped: in the grid, the caller checked), a collidable
-    // one replaced by the agent's own; bit 0 blocks i, bit 1 blocks j
-    OC_RH int collide(const Row& r, int i, int j, int ci, int cj) const {
-        const int lix = r.ax(i), liy = r.ay(i), ljx = r.ax(j), ljy = r.ay(j);
-        int nix = lix + kDX[ci], niy = liy + kDY[ci], njx = ljx + kDX[cj], njy = ljy + kDY[cj];
-        if (static_tile(cell(nix, niy)) != kFloor) { nix = lix; niy = liy; }
-        if (static_tile(cell(njx, njy)) != kFloor) { njx = ljx; njy = ljy; }
-        if (nix == njx && niy == njy) {
-            if (nix == lix && niy == liy && ci != kNoop) return 2;
-            if (njx == ljx && njy == ljy && cj != kNoop) return 1;
-            return 3;
-        }
-        return lix == njx && liy == njy && ljx == nix && ljy == niy ? 3 : 0;
-    }
-
-    // One step of one env.  act: agent a's action code in byte a (codes past 4 are no-ops);
-    // t: the u16 step counter; returns the output flags (OC_FLAG_*) and sets ex (executed codes,
-    // byte a) and cm (collision pairs in itertools.combinations order).
-    OC_RH uint32_t env_step(Row& r, uint32_t& t, uint32_t fl, uint32_t act, const StepLevel& S, uint32_t& ex,
-                            uint32_t& cm) {
-        ac = kNoAc;
-        constexpr uint32_t kNoops = 0x04040404u & (A == 4 ? 0xFFFFFFFFu : (1u << (8 * (A & 3))) - 1u);
-        cm = 0u;
-        ex = kNoops;
-        if (fl & 1u) {  // next-step auto-reset (build-defined): the level template
-            r = Row{};
-#pragma unroll
-            for (int a = 0; a < A; ++a) {
-                Row::s32(r.x, a, S.spawn_x[a]);
-                Row::s32(r.y, a, S.spawn_y[a]);
-                Row::s32(r.h, a, kNone);
-            }
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                r.set_loc(j, S.item_cell[j]);
-                r.set_mask(j, S.item_mask[j]);
-            }
-            t = 0u;
-            return 0u;
-        }
-        t = (t + 1u) & 0xFFFFu;  // :257
-        int c[A];
-#pragma unroll
-        for (int a = 0; a < A; ++a) {
-            const int k = (int)((act >> (8 * a)) & 0xFFu);
-            c[a] = k > kNoop ? kNoop : k;
-        }
-        if (A >= 2) {  // check_collisions looks the unclamped next square up: off the grid it asserts
-            bool off = false;
-#pragma unroll
-            for (int a = 0; a < A; ++a) {
-                const int nx = r.ax(a) + kDX[c[a]], ny = r.ay(a) + kDY[c[a]];
-                off |= nx < 0 || ny < 0 || nx >= L.W || ny >= L.H;
-            }
-            if (off) return 1u | 4u;  // world.py:429 raises before anything moves: t advanced only
-        }
-        uint32_t blocked = 0u;
-        int pair = 0;
-#pragma unroll
-        for (int i = 0; i < A; ++i)
-#pragma unroll
-            for (int j = i + 1; j < A; ++j, ++pair) {
-                const int b = collide(r, i, j, c[i], c[j]);
-                blocked |= (b & 1 ? 1u << i : 0u) | (b & 2 ? 1u << j : 0u);
-                cm |= b ? 1u << pair : 0u;
-            }
-        ex = 0u;
-#pragma unroll
-        for (int a = 0; a < A; ++a) {  // execute_navigation (:767-770), agents in order
-            const int e = (blocked >> a) & 1u ? kNoop : c[a];
-            interact(r, a, e);
-            ex |= (uint32_t)e << (8 * a);
-        }
-        // new_obs = copy.copy(self) (:289) raises when two co-located agents both hold
-#pragma unroll
-        for (int i = 0; i < A; ++i)
-#pragma unroll
-            for (int j = i + 1; j < A; ++j)
-                if (r.ah(i) != kNone && r.ah(j) != kNone && r.ax(i) == r.ax(j) && r.ay(i) == r.ay(j)) return 1u | 4u;
-        if (S.max_T != 0 && (int)t >= S.max_T) return 1u;  // done(): the timeout first (:328-332)
-        for (int g = 0; g < S.ngoals; ++g) {  // every goal mask at the first Delivery (:344-359)
-            bool ok = false;
-#pragma unroll
-            for (int j = 0; j < K; ++j) ok |= r.il(j) == S.done_cell && r.im(j) == S.goal[g];
-            if (!ok) return 0u;
-        }
-        return 1u | 2u;
     }
 
     // E2E_BRTDP.Q(state, action, v_l) with value_init's values (e2e_brtdp.py:736-760, :678-729);

@@ -131,6 +131,10 @@ struct SwarLevel {
                              // content predicates below read 2-bit counts, a plate bit and a Fresh bit
     int32_t edge;            // a Floor square on the grid's border: an action can point off the grid
     uint32_t wm1_rep, hm1_rep;  // W - 1, H - 1 replicated (the off-grid test)
+    // wide levels (more than 255 cells, u16 cell ids; step4w): done_rep and tmpl_l hold the low
+    // bytes of the first Delivery cell and of the template's item cells, these the high bytes
+    uint32_t done_hi_rep;
+    uint32_t tmpl_lh[16];
 };
 
 // Host-side construction of the SwarLevel constants (called by oc_create after validation).
@@ -533,6 +537,283 @@ OC_SW bool step4(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         OC_TIED_SEL(Lc[j], rst, L.tmpl_l[j]);
+        OC_TIED_SEL(M[j], rst, L.tmpl_m[j]);
+    }
+    OC_TIED_ANDN(T0, perm(rst, rst, 0x01010000u));
+    OC_TIED_ANDN(T1, perm(rst, rst, 0x03030202u));
+    OC_TIED_OR(F, andn(fl, rst));
+    OC_TIED_ANDN(CM, rst);
+    return true;
+}
+
+// ---- wide levels (more than 255 cells): cells are u16, held as two byte words ----
+// A cell-valued quantity of four envs is a pair of dwords, its low bytes and its high bytes (the
+// wide state layout's two item-cell planes), so the step stays four envs
+// per dword and every byte-valued field (agent x / y / held slot, item masks, actions, flags)
+// keeps step4's byte arithmetic.  Cell arithmetic (y * W + x, the move) runs in packed u16
+// lanes (v_pk_mad_u16 / v_pk_add_u16 / v_pk_sub_u16: no carry or borrow crosses a lane), two
+// envs per dword, and is repacked into the two byte words.
+struct Cell2 {
+    uint32_t lo, hi;
+};
+OC_SW Cell2 csel(uint32_t m, const Cell2& a, const Cell2& b) { return Cell2{sel(m, a.lo, b.lo), sel(m, a.hi, b.hi)}; }
+// h80 of (a == b) per env, all 16 bits
+OC_SW uint32_t ceq80(const Cell2& a, const Cell2& b) {
+    return zf80(bop3<OC_LUT((a ^ b) | c)>(a.hi, b.hi, a.lo ^ b.lo));
+}
+// h80 per env: some item of the env lies on the first Delivery square (wide levels)
+template <int K>
+OC_SW uint32_t at_done80w(const SwarLevel& L, const uint32_t (&LL)[K], const uint32_t (&LH)[K]) {
+    uint32_t hit = 0u;
+#pragma unroll
+    for (int j = 0; j < K; ++j) hit |= zf80(bop3<OC_LUT((a ^ b) | c)>(LH[j], L.done_hi_rep, LL[j] ^ L.done_rep));
+    return hit;
+}
+
+// step4 for a wide level: the same rules, in the same order (see step4 for the reference
+// citations and the rare-event split); cells as Cell2 (LL / LH: the item slots' low / high
+// bytes).  `cls_of(Cell2)` returns the tile class byte per env.
+template <int A, int K, class ClassOf, class AnyOf>
+OC_SW bool step4w(const SwarLevel& L, uint32_t (&X)[A], uint32_t (&Y)[A], uint32_t (&H)[A], uint32_t (&LL)[K],
+                  uint32_t (&LH)[K], uint32_t (&M)[K], uint32_t& T0, uint32_t& T1, uint32_t& F,
+                  const uint32_t (&ACT)[A], uint32_t (&EX)[A], uint32_t& CM, ClassOf cls_of, AnyOf any_of,
+                  uint32_t& pending) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const bool counts = (bool)L.counts, edge = (bool)L.edge;
+    const uint32_t rst = full80((F << 7) & k80);  // input DONE => next-step auto-reset
+    const u16x2 wv = {(unsigned short)L.W, (unsigned short)L.W};
+
+    uint32_t act[A], cls[A], nn80[A], bump80[A], blk80[A], out80[A];
+    Cell2 loc[A], nraw[A], nxt[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        uint32_t c = ACT[a];
+        const uint32_t ge5 = bop3<OC_LUT((a | b) & c)>((c & k7F) + 0x7B7B7B7Bu, c, k80);
+        act[a] = sel(full80(ge5), k04, c);  // codes > 4 act as (0, 0)
+        out80[a] = 0u;
+    }
+    uint32_t raise80 = 0u;
+    if (edge) {  // an action off the grid (a Floor on the border): step4's off-grid raise
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            const uint32_t c = act[a];
+            out80[a] = or3(and3(z80(c), z80(Y[a] ^ L.hm1_rep), k80), and3(z80(c ^ k01), z80(Y[a]), k80),
+                           and3(z80(c ^ 0x02020202u), z80(X[a]), k80) | and3(z80(c ^ 0x03030303u), z80(X[a] ^ L.wm1_rep), k80));
+            if (A >= 2) raise80 |= out80[a];
+        }
+        if (A >= 2) {
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                act[a] = sel(full80(raise80), k04, act[a]);
+                out80[a] = 0u;
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        const uint32_t c = act[a];
+        nn80[a] = nz80(c ^ k04);
+        // envs 0 and 2 (selector bytes 0 and 2), envs 1 and 3 (1 and 3) as u16 lanes
+        const u16x2 y02 = __builtin_bit_cast(u16x2, perm(0u, Y[a], 0x0C020C00u));
+        const u16x2 y13 = __builtin_bit_cast(u16x2, perm(0u, Y[a], 0x0C030C01u));
+        const u16x2 x02 = __builtin_bit_cast(u16x2, perm(0u, X[a], 0x0C020C00u));
+        const u16x2 x13 = __builtin_bit_cast(u16x2, perm(0u, X[a], 0x0C030C01u));
+        const u16x2 l02 = y02 * wv + x02, l13 = y13 * wv + x13;
+        // the move: + max(delta, 0) - max(-delta, 0) (LUTs on the action code; a selector byte
+        // 0x0C reads zero, so each u16 lane gets the byte value)
+        const uint32_t s02 = perm(0x0C0C0C0Cu, c, 0x04020400u), s13 = perm(0x0C0C0C0Cu, c, 0x04030401u);
+        const u16x2 n02 = l02 + __builtin_bit_cast(u16x2, perm(L.dp_hi, L.dp_lo, s02)) -
+                          __builtin_bit_cast(u16x2, perm(L.dn_hi, L.dn_lo, s02));
+        const u16x2 n13 = l13 + __builtin_bit_cast(u16x2, perm(L.dp_hi, L.dp_lo, s13)) -
+                          __builtin_bit_cast(u16x2, perm(L.dn_hi, L.dn_lo, s13));
+        const uint32_t L02 = __builtin_bit_cast(uint32_t, l02), L13 = __builtin_bit_cast(uint32_t, l13);
+        const uint32_t N02 = __builtin_bit_cast(uint32_t, n02), N13 = __builtin_bit_cast(uint32_t, n13);
+        loc[a] = Cell2{perm(L13, L02, 0x06020400u), perm(L13, L02, 0x07030501u)};
+        nraw[a] = Cell2{perm(N13, N02, 0x06020400u), perm(N13, N02, 0x07030501u)};
+        if (edge) nraw[a] = csel(full80(out80[a]), loc[a], nraw[a]);  // World.inbounds (one agent)
+        cls[a] = cls_of(nraw[a]);
+        const uint32_t onF80 = cls[a] & k80;
+        nxt[a] = csel(full80(onF80), nraw[a], loc[a]);
+        bump80[a] = andn(nn80[a], onF80);
+        blk80[a] = 0u;
+    }
+
+    // ---- check_collisions: pairs in itertools.combinations order ----
+    uint32_t cm = 0u;
+    int p = 0;
+#pragma unroll
+    for (int i = 0; i < A; ++i) {
+#pragma unroll
+        for (int j = i + 1; j < A; ++j, ++p) {
+            const uint32_t eq = ceq80(nxt[i], nxt[j]);
+            const uint32_t sw = ceq80(loc[i], nxt[j]) & ceq80(loc[j], nxt[i]);
+            const uint32_t bi = bop3<OC_LUT(a ? !b : c)>(eq, bump80[i], sw);
+            const uint32_t u = bop3<OC_LUT((a | !b) & c)>(bump80[i], bump80[j], k80);
+            const uint32_t bj = sel(eq, u, sw);
+            blk80[i] |= bi;
+            blk80[j] |= bj;
+            cm |= (bi | bj) >> (7 - p);
+        }
+    }
+    if (edge && A >= 2) cm = andn(cm, full80(raise80));
+
+    // ---- execute_navigation: interact per agent, in order ----
+    uint32_t dlv = 0u;
+#pragma unroll
+    for (int k = 0; k < A; ++k) {
+        const uint32_t go80 = andn(nn80[k], blk80[k]);
+        EX[k] = sel(full80(go80), act[k], k04);
+        const Cell2 tc = nraw[k];
+        const uint32_t isF80 = cls[k] & k80;
+        const uint32_t isD80 = (cls[k] << 1) & k80;
+        const uint32_t isC80 = (cls[k] << 2) & k80;
+        const uint32_t h = H[k];
+        const uint32_t hold80 = andn(k80, h);
+        uint32_t ne[K];  // bit 7: slot j is NOT at tc
+#pragma unroll
+        for (int j = 0; j < K; ++j) ne[j] = ~zf80(bop3<OC_LUT((a ^ b) | c)>(LH[j], tc.hi, LL[j] ^ tc.lo));
+        auto any_at = [&](auto pick) -> uint32_t {
+            uint32_t all = 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                if (pick(j)) all &= ne[j];
+            return andn(k80, all);
+        };
+        const uint32_t seen = any_at([](int) { return true; });
+        const uint32_t ob0 = any_at([](int j) { return (j & 1) != 0; });
+        const uint32_t ob1 = any_at([](int j) { return (j & 2) != 0; });
+        const uint32_t ob2 = K > 4 ? any_at([](int j) { return (j & 4) != 0; }) : 0u;
+        const uint32_t ob3 = K > 8 ? any_at([](int j) { return (j & 8) != 0; }) : 0u;
+        const uint32_t so1 = (ob0 >> 5) | kLanes;
+        const uint32_t sh = bop3<OC_LUT((a & b) | c)>(h << 2, k04, kLanes);
+        uint32_t om, hm;
+        if constexpr (K == 4) {
+            const uint32_t so2 = (ob1 >> 5) | kLanes, sh2 = bop3<OC_LUT(a | (b & c))>(kLanes, h << 1, k04);
+            om = perm(perm(M[3], M[2], so1), perm(M[1], M[0], so1), so2);
+            hm = perm(perm(M[3], M[2], sh), perm(M[1], M[0], sh), sh2);
+        } else {
+            const uint32_t fo1 = full80(ob1), fo2 = full80(ob2), fo3 = K == 16 ? full80(ob3) : 0u;
+            const uint32_t fh1 = full80((h << 6) & k80), fh2 = full80((h << 5) & k80);
+            const uint32_t fh3 = K == 16 ? full80((h << 4) & k80) : 0u;
+            om = gather<K>(M, so1, fo1, fo2, fo3);
+            hm = gather<K>(M, sh, fh1, fh2, fh3);
+        }
+        const uint32_t nf = andn(go80, isF80), mv = andn(go80 & isF80, out80[k]);
+        uint32_t two_r, nallch_r, nplate_r, nfood_r, nch_r, cu, chopped;
+        if (counts) {
+            const uint32_t x = hm & k7F;
+            two_r = bop3<OC_LUT((a & b) | c)>((x | k80) - k01, x, x & 0x2A2A2A2Au) + k7F;
+            nallch_r = 0u;
+            nplate_r = and3(hm, om, 0x40404040u) + k7F;
+            nfood_r = hm | om;
+            nch_r = hm;
+            cu = x + (om & k7F);
+            chopped = x;
+        } else {
+            const uint32_t c4 = hm & k0F;
+            two_r = (((c4 | k80) - k01) & c4) + k7F;
+            nallch_r = bop3<OC_LUT((!a) & b & c)>(hm >> 4, hm, k07) + k7F;
+            cu = hm | om;
+            nplate_r = and3(hm, om, k08) + k7F;
+            nfood_r = bop3<OC_LUT((!a) & b & c)>(cu >> 4, cu, k07) + k7F;
+            nch_r = bop3<OC_LUT(a & !b & !c)>(c4 + k7F, two_r, (hm & k78) + k7F);
+            chopped = bop3<OC_LUT((a & b) | c)>(hm << 4, 0x70707070u, hm);
+        }
+        const uint32_t nfh = nf & hold80;
+        const uint32_t deliver = bop3<OC_LUT(a & b & !c)>(nfh & isD80, two_r, nallch_r);
+        const uint32_t cnt = andn(nfh, isD80);
+        const uint32_t merge = bop3<OC_LUT(a & b & !c)>(cnt, seen, nplate_r | nfood_r);
+        const uint32_t empty = andn(cnt, seen);
+        const uint32_t chop = and3(empty, isC80, nch_r);
+        const uint32_t put = andn(empty, chop);
+        const uint32_t pick = andn(bop3<OC_LUT(a & !b & c)>(nf, hold80, seen), isD80);
+        const uint32_t reloc = or3(mv, deliver, put);
+        dlv |= deliver;
+
+        const uint32_t amv = bop3<OC_LUT(a | ((!b) & c))>(act[k], mv >> 5, k04);
+        X[k] = X[k] + perm(kDXhi, kDXlo, amv) - k01;
+        Y[k] = Y[k] + perm(kDYhi, kDYlo, amv) - k01;
+        const uint32_t fmg = full80(merge), fpk = full80(pick);
+        const Cell2 newOl = {fmg | sel(fpk, loc[k].lo, tc.lo), fmg | sel(fpk, loc[k].hi, tc.hi)};  // merged away: 0xFFFF
+        const uint32_t newOm = andn(om, fmg);
+        const Cell2 newHl = csel(full80(reloc), tc, loc[k]);
+        const uint32_t newHm = sel(fmg, cu, sel(full80(chop), chopped, hm));
+        const uint32_t oidx = (ob0 >> 7) | (ob1 >> 6) | (ob2 >> 5) | (ob3 >> 4);
+        const uint32_t fwo = full80(merge | pick);
+        const uint32_t fwh = full80(and3(hold80, or3(reloc, merge, chop), k80));
+        const uint32_t so = sel(fwo, oidx, 0x0C0C0C0Cu), shw = sel(fwh, h, 0x0C0C0C0Cu);
+        uint32_t so_lo = so, shw_lo = shw, so_hi = 0x0C0C0C0Cu, shw_hi = 0x0C0C0C0Cu;
+        if constexpr (K == 16) {
+            const uint32_t o8 = full80(and3(oidx << 4, k80, fwo)), h8 = full80(and3(h << 4, k80, fwh));
+            so_lo = sel(o8, 0x0C0C0C0Cu, so);
+            shw_lo = sel(h8, 0x0C0C0C0Cu, shw);
+            so_hi = sel(o8, oidx ^ 0x08080808u, 0x0C0C0C0Cu);
+            shw_hi = sel(h8, h ^ 0x08080808u, 0x0C0C0C0Cu);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const int jj = j & 7;
+            const uint32_t lut_lo = jj < 4 ? 0xFFu << (8 * jj) : 0u, lut_hi = jj < 4 ? 0u : 0xFFu << (8 * (jj - 4));
+            const uint32_t eo = perm(lut_hi, lut_lo, j < 8 ? so_lo : so_hi);
+            const uint32_t eh = perm(lut_hi, lut_lo, j < 8 ? shw_lo : shw_hi);
+            LL[j] = sel(eh, newHl.lo, sel(eo, newOl.lo, LL[j]));
+            LH[j] = sel(eh, newHl.hi, sel(eo, newOl.hi, LH[j]));
+            M[j] = sel(eh, newHm, sel(eo, newOm, M[j]));
+        }
+        H[k] = sel(full80(deliver | put), kFF, sel(fpk, oidx, h));
+    }
+
+    // ---- the copy crash: two co-located agents both holding (ERR) ----
+    uint32_t err = 0u;
+#pragma unroll
+    for (int i = 0; i < A; ++i)
+#pragma unroll
+        for (int j = i + 1; j < A; ++j) {
+            const uint32_t same = z80(bop3<OC_LUT((a ^ b) | c)>(X[i], X[j], Y[i] ^ Y[j]));
+            err |= and3(same, andn(k80, H[i]), andn(k80, H[j]));
+        }
+    err |= raise80;
+
+    // ---- done() and reward() ----
+    const u16x2 one = {1, 1};
+    u16x2 t0 = __builtin_bit_cast(u16x2, T0) + one, t1 = __builtin_bit_cast(u16x2, T1) + one;
+    uint32_t tout = 0u;
+    if (L.maxT_rep != 0u) {
+        const u16x2 mt = __builtin_bit_cast(u16x2, L.maxT_rep);
+        const uint32_t d0 = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(mt, t0));
+        const uint32_t d1 = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(mt, t1));
+        const uint32_t z0 = andn(0x80008000u, ((d0 & 0x7FFF7FFFu) + 0x7FFF7FFFu) | d0);
+        const uint32_t z1 = andn(0x80008000u, ((d1 & 0x7FFF7FFFu) + 0x7FFF7FFFu) | d1);
+        tout = perm(z1, z0, 0x07050301u);
+    }
+    T0 = __builtin_bit_cast(uint32_t, t0);
+    T1 = __builtin_bit_cast(uint32_t, t1);
+    F = 0u;
+    CM = cm;
+    if (!any_of(or3(rst, tout | err, dlv | pending))) return false;  // wave-uniform: no rare event
+    pending = 0u;
+    uint32_t ok = k80;
+    for (int g = 0; g < L.ngoals; ++g) {
+        uint32_t hit = 0u;
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            hit |= zf80(or3(LL[j] ^ L.done_rep, LH[j] ^ L.done_hi_rep, M[j] ^ L.goals_rep[g]));
+        ok &= hit;
+    }
+    const uint32_t done80 = or3(err, tout, ok);
+    const uint32_t succ80 = bop3<OC_LUT(a & !b & !c)>(ok, err, tout);
+    uint32_t fl = or3(done80 >> 7, succ80 >> 6, err >> 5);
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        OC_TIED_SEL(X[a], rst, L.tmpl_x[a]);
+        OC_TIED_SEL(Y[a], rst, L.tmpl_y[a]);
+        OC_TIED_OR(H[a], rst);
+        OC_TIED_SEL(EX[a], rst, k04);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        OC_TIED_SEL(LL[j], rst, L.tmpl_l[j]);
+        OC_TIED_SEL(LH[j], rst, L.tmpl_lh[j]);
         OC_TIED_SEL(M[j], rst, L.tmpl_m[j]);
     }
     OC_TIED_ANDN(T0, perm(rst, rst, 0x01010000u));
