@@ -215,3 +215,55 @@ def test_wide_host_rows_match_oracle_random(name, A):
     ok = o_f == capi.LIK_OK
     assert ok.sum() > 20
     np.testing.assert_allclose(h_v[ok], o_v[ok], rtol=1e-12)
+
+
+def _variant(kind):
+    """wide-17x17_salad edited into the level kinds the wide SWAR step (ocsw::step4w) has
+    branches for: `edge` opens two border squares to Floor (an action can point off the grid);
+    `counts` repeats the foods (OC_ENC_COUNTS masks, 8 item slots); `many` has 10 objects (16)."""
+    rows, rest = open(_path("wide-17x17_salad")).read().split("\n\n", 1)
+    grid = [list(r) for r in rows.split("\n")]
+    if kind == "edge":
+        grid[0][3] = " "
+        grid[10][16] = " "
+    if kind in ("counts", "many"):
+        grid[16][3], grid[0][12] = "t", "l"
+    if kind == "many":
+        grid[3][16], grid[16][12], grid[0][14], grid[8][0] = "p", "p", "o", "t"
+    return levels.parse_level_text("\n".join("".join(r) for r in grid) + "\n\n" + rest, "wide-17x17-" + kind)
+
+
+@pytest.mark.parametrize("kind,A", [("edge", 1), ("edge", 3), ("counts", 2), ("counts", 4), ("many", 3)])
+def test_wide_swar_step_variants_match_oracle(kind, A):
+    """The wide SWAR step's wave-uniform branches (Floor on the border with one agent, where
+    interact clamps the square, and with several, where check_collisions raises; repeated foods
+    in the counts encoding; 16 item slots) on oc_cpu_step, the host pass of the kernel's code,
+    against the oracle over random play with timeouts and resets."""
+    lv = _variant(kind)
+    assert capi.is_wide(lv)
+    B, steps, max_T = 1003, 150, 37
+    ob = oracle.OracleBatch(lv, A, max_T, B)
+    cs = CpuStepper(lv, A, B, max_T, nthreads=3)
+    assert cs.K == {"edge": 4, "counts": 8, "many": 16}[kind] and lv.encoding == (0 if kind == "edge" else 1)
+    P = ob.pitch
+    s1, n1 = ob.new_state(), ob.new_state()
+    ob.reset(s1)
+    s2, n2 = s1.copy(), s1.copy()
+    act = ob.new_actions()
+    e1, e2 = np.zeros(A * P, np.uint8), np.zeros(A * P, np.uint8)
+    c1, c2 = np.zeros(P, np.uint8), np.zeros(P, np.uint8)
+    tot, want = np.zeros(5, np.uint64), np.zeros(5, np.int64)
+    for t in range(steps):
+        ob.gen_actions(act, 0, t, 53 * A + 11)
+        fl_in = tl.planes_view(s1, A, ob.K, P)["fl"].copy()
+        ob.step(s1, n1, act, e1, c1)
+        cs.step(s2, n2, act, e2, c2, tot)
+        s1, n1, s2, n2 = n1, s1, n2, s2
+        want += tl.window_totals(fl_in, s1, c1, A, ob.K, P, B)
+        v1, v2 = tl.env_view(s1, A, ob.K, P, B), tl.env_view(s2, A, ob.K, P, B)
+        assert np.array_equal(v1, v2), (t, np.argwhere(v1 != v2)[:5].tolist())
+        assert np.array_equal(e1.reshape(A, -1)[:, :B], e2.reshape(A, -1)[:, :B]), t
+        assert np.array_equal(c1[:B], c2[:B]), t
+    assert np.array_equal(tot.astype(np.int64), want), (tot, want)
+    if kind == "edge" and A > 1:
+        assert want[4] > 0  # off-grid raises (ERR ends)

@@ -294,3 +294,44 @@ def test_wide_step_n_splits_into_launches(out):
     assert np.array_equal(totals.cpu().numpy(), tot)
     assert np.array_equal(eb.reduce_stats(stats).cpu().numpy(), tot)
     assert tot[0] >= B * (n // (max_T + 1)) // 2
+
+
+@pytest.mark.parametrize("kind,A", [("edge", 1), ("edge", 3), ("counts", 2), ("counts", 4), ("many", 3)])
+def test_wide_swar_step_variants_on_device(kind, A):
+    """The wide SWAR step's branches (border Floor, repeated foods, 16 item slots:
+    test_widelevels._variant) in oc_step_n on the device: two 30-step launches over 20,003 envs
+    against the oracle, every step's state, executed actions and collision mask, and totals."""
+    lv = tw._variant(kind)
+    B, n, max_T, seed = 20003, 30, 29, 17 + A
+    eb = _batch(lv, A, B, max_T)
+    ob = oracle.OracleBatch(lv, A, max_T, B)
+    P, S = eb.pitch, eb.layout.state_bytes
+    s_in, s_out = eb.new_state(), eb.new_state()
+    eb.reset(s_in)
+    c, c2 = ob.new_state(), ob.new_state()
+    ob.reset(c)
+    ca, cex, ccoll = ob.new_actions(), np.zeros(A * P, np.uint8), np.zeros(P, np.uint8)
+    acts = torch.empty((n, A * P), dtype=torch.uint8, device="cuda:0")
+    traj = torch.empty(n * S, dtype=torch.uint8, device="cuda:0")
+    ex = torch.empty(n * A * P, dtype=torch.uint8, device="cuda:0")
+    coll = torch.empty(n * P, dtype=torch.uint8, device="cuda:0")
+    stats, totals = eb.new_stats(), torch.zeros(5, dtype=torch.int64, device="cuda:0")
+    for launch in range(2):
+        tot = np.zeros(5, np.int64)
+        for r in range(n):
+            eb.gen_actions(acts[r], launch * n + r, seed)
+        eb.step_n(s_in, s_out, acts.reshape(-1), n, traj, ex, coll, stats, totals)
+        tr, exh, colh = traj.view(n, S).cpu().numpy(), ex.view(n, A, P).cpu().numpy(), coll.view(n, P).cpu().numpy()
+        for r in range(n):
+            ob.gen_actions(ca, 0, launch * n + r, seed)
+            fl_in = tl.planes_view(c, A, ob.K, P)["fl"].copy()
+            ob.step(c, c2, ca, cex, ccoll, nthreads=16)
+            c, c2 = c2, c
+            tot += tl.window_totals(fl_in, c, ccoll, A, ob.K, P, B)
+            g, o = tl.env_view(tr[r], A, ob.K, P, B), tl.env_view(c, A, ob.K, P, B)
+            assert np.array_equal(g, o), (launch, r, np.argwhere(g != o)[:5].tolist())
+            assert np.array_equal(exh[r][:, :B], cex.reshape(A, P)[:, :B]), (launch, r)
+            assert np.array_equal(colh[r][:B], ccoll[:B]), (launch, r)
+        assert np.array_equal(eb.reduce_stats(stats).cpu().numpy() - (0 if launch == 0 else prev), tot), launch
+        prev = eb.reduce_stats(stats).cpu().numpy()
+        s_in, s_out = s_out, s_in
