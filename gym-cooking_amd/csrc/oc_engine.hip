@@ -2421,6 +2421,15 @@ static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num
     R.L = h->roll;
     R.nsub = num_subtasks;
     R.blob_words = h->roll.lds_bytes / 4;  // staged in LDS: the whole blob, or the tables before the distances
+    if (R.L.sq_off != 0 && B > (int64_t)h->cus * kRollBlock) {
+        // The node-to-square table (the blob's tail) shortens the one-agent Merge bound from ~3.8
+        // to 1.1-2.0 us of a wave; that pays where a launch is one round of blocks (the planner's
+        // latency shape: 9.03 -> 8.87 us at 4096 rows) and not past it, where every block stages
+        // 40% more table for it (11.16-11.34 -> 11.35-11.51 us at 2^18): tools/rollx.hip,
+        // profiles/r06/pass_i.  Larger launches search B's approach nodes as before.
+        R.blob_words = R.L.sq_off / 4;
+        R.L.sq_off = 0;
+    }
     R.pitch = pitch_for(B);
     R.B = B;
     for (int i = 0; i < num_subtasks; ++i) {
@@ -2480,8 +2489,8 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_ROLL(A, K, W, GD)                                                                             \
-    if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W, GD>, h->roll.lds_bytes)) return rc;   \
-    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W, GD>), grid, dim3(kRollBlock), h->roll.lds_bytes, st, R,            \
+    if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W, GD>, R.blob_words * 4)) return rc;   \
+    hipLaunchKernelGGL((oc_rollout_kernel<A, K, W, GD>), grid, dim3(kRollBlock), R.blob_words * 4, st, R,            \
                        (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags,       \
                        lower_bound)
 #define OC_PLAN_WIDE(A, K) OC_LAUNCH_ROLL(A, K, true, true)
@@ -2523,8 +2532,8 @@ int oc_nav_likelihood(const oc_handle* h, const void* state, const uint8_t* take
     hipStream_t st = (hipStream_t)stream;
 #define OC_LIK_GO(KERN, A, K, GG, W, GD)                                                                             \
     do {                                                                                                             \
-        if (const int rc = allow_dyn_lds((const void*)KERN<A, K, GG, W, GD>, h->roll.lds_bytes)) return rc;          \
-        hipLaunchKernelGGL((KERN<A, K, GG, W, GD>), grid, dim3(kBlock), h->roll.lds_bytes, st, R, (const uint8_t*)state, \
+        if (const int rc = allow_dyn_lds((const void*)KERN<A, K, GG, W, GD>, R.blob_words * 4)) return rc;          \
+        hipLaunchKernelGGL((KERN<A, K, GG, W, GD>), grid, dim3(kBlock), R.blob_words * 4, st, R, (const uint8_t*)state, \
                            taken, alloc, h->roll_blob, self_agent, beta, none_action_prob, likelihood, out_flags);   \
     } while (0)
 #define OC_LAUNCH_LIK(A, K, W, GD)                                                                                   \
@@ -2575,8 +2584,8 @@ int oc_subtask_bounds(const oc_handle* h, const void* state, const oc_subtask* s
     const dim3 grid((unsigned)bx, (unsigned)chunks);
     hipStream_t st = (hipStream_t)stream;
 #define OC_LAUNCH_BOUNDS(A, K, W, GD)                                                                         \
-    if (const int rc = allow_dyn_lds((const void*)oc_bounds_kernel<A, K, W, GD>, h->roll.lds_bytes)) return rc;  \
-    hipLaunchKernelGGL((oc_bounds_kernel<A, K, W, GD>), grid, dim3(kBlock), h->roll.lds_bytes, st, R,           \
+    if (const int rc = allow_dyn_lds((const void*)oc_bounds_kernel<A, K, W, GD>, R.blob_words * 4)) return rc;  \
+    hipLaunchKernelGGL((oc_bounds_kernel<A, K, W, GD>), grid, dim3(kBlock), R.blob_words * 4, st, R,           \
                        (const uint8_t*)state, h->roll_blob, lower_bound, doable)
 #define OC_PLAN_WIDE(A, K) OC_LAUNCH_BOUNDS(A, K, true, true)
 #define OC_PLAN_NARROW_GD(A, K) OC_LAUNCH_BOUNDS(A, K, false, true)

@@ -56,6 +56,7 @@ constexpr int kMaxCellsWide = 1024;  // wide levels (more than 255 cells): u16 c
 // u16 (0xFFFF = no path) in device memory when some BFS distance reaches 255 (RollLevel.dist16;
 // round 5 refused such a graph)
 constexpr int kMaxNodes = 360;  // 360^2 + the other tables + the compacted likelihood's 18 KB < 160 KB
+constexpr int kMaxSqBytes = 8192;  // the node-to-square table is built when nnodes x cells fits this
 constexpr int kMaxNodesNarrow = 5 * kMaxCells;    // narrow levels: every node 255 cells can make
 constexpr int kMaxNodesWide = 5 * kMaxCellsWide;  // wide levels: the distances stay in device memory
 constexpr uint8_t kNone = 0xFF;
@@ -76,8 +77,12 @@ constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NA
 //              Delivery (row 1) square (the two-agent static bound's B term; round 6)
 //   dmin_off   [2][nnodes] the distance from a node to the nearest Cutboard (row 0) / Delivery
 //              (row 1) approach node, 0xFF = none reachable (u16 and 0xFFFF with dist16)
-//   dist_off   [nnodes][nnodes] BFS distances (last: a wide level stages the blob up to here;
-//              u16 entries with dist16)
+//   dist_off   [nnodes][nnodes] BFS distances (a wide level stages the blob up to here; u16
+//              entries with dist16)
+//   sq_off     [nnodes][cells] node-to-square distances: min over the square's approach nodes
+//              (its own node for a Floor square), 0xFF = none reachable; only on a small narrow
+//              level whose blob stays in LDS (kMaxSqBytes), where the single-agent Merge bound
+//              reads it once per (A approach, B square) instead of walking B's approaches
 // Only the tile table's size is fixed (256 entries on a narrow level); the others follow the
 // level's cell count (round 6; before, every per-cell table had 256 entries on a narrow level).
 
@@ -98,6 +103,9 @@ struct RollLevel {  // scalars (kernel argument); the tables are in the blob
                          // one of more than kMaxNodes nodes (the planner kernels' GD instantiation)
     int32_t dist16;      // the distance and nearest-side tables are u16 (some BFS distance >= 255);
                          // implies dist_global (round 6)
+    int32_t sq_off;      // blob offset of the node-to-square table ([nnodes][cells] u8, the distance
+                         // from a node to the nearest approach node of a square), 0 = none (round 6)
+    int32_t sq_cells;    // its row length (the level's cell count)
 };
 
 // A wide level's reset template (oc_reset_wide_kernel).
@@ -210,6 +218,8 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
     L.ncut = L.ndeliv = 0;
     L.nnodes = -1;
     L.dist16 = 0;
+    L.sq_off = 0;
+    L.sq_cells = 0;
     const int cells = W * H;
     L.wide = cells > kMaxCells ? 1 : 0;
     if (cells > kMaxCellsWide) return -1;
@@ -361,6 +371,30 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
     L.nnodes = n;
     L.blob_bytes = (int32_t)((L.dist_off + (size_t)n * n * db + 3) & ~(size_t)3);
     L.dist_global = L.wide || n > kMaxNodes || L.dist16 ? 1 : 0;
+    if (!L.dist_global && (size_t)n * cells <= (size_t)kMaxSqBytes) {
+        // node-to-square distances (World.get_lower_bound_between_helper's min over B's approach
+        // nodes, world.py:175-189, for every (node, square)); a collidable square's approaches are
+        // its approach-0..3 nodes, a Floor square's its own node (the static graph; a square that
+        // is an AgentCounter in a Level-0 view is caught at the lookup)
+        L.sq_off = L.blob_bytes;
+        L.sq_cells = cells;
+        blob_v.resize((size_t)L.sq_off + (size_t)n * cells + 4, 0);
+        blob = blob_v.data();
+        node = (uint16_t*)(blob + L.node_off);
+        uint8_t* sq = blob + L.sq_off;
+        for (int v = 0; v < n; ++v)
+            for (int c = 0; c < cells; ++c) {
+                uint32_t best = kNone;
+                for (int d = 0; d < 5; ++d) {
+                    const int b = node[c * 5 + d];
+                    if (b == kNoNode || (d == 4) != (tiles[c] == kFloor)) continue;
+                    const uint32_t dd = d16[(size_t)v * n + b];
+                    if (dd != 0xFFFF && dd < best) best = dd;
+                }
+                sq[(size_t)v * cells + c] = (uint8_t)best;
+            }
+        L.blob_bytes = (int32_t)((L.sq_off + (size_t)n * cells + 3) & ~(size_t)3);
+    }
     L.lds_bytes = L.dist_global ? L.dist_off : L.blob_bytes;
     blob_v.resize((size_t)L.blob_bytes, 0);
     return n;
@@ -622,6 +656,13 @@ struct RowOps {
         const int d = D[none ? 0u : i];
         return none || d == kNone ? -1 : d;
     }
+    // the distance from node v to the nearest approach node of square c (the node-to-square table,
+    // when the level has one), or -1: none reachable, v missing, or c an AgentCounter of the
+    // Level-0 view (collidable there, and its approach nodes are not in the static graph)
+    OC_RH int dsq(int v, int c) const {
+        const int m = T[L.sq_off + (int)mul24((uint32_t)(v == kNoNode ? 0 : v), (uint32_t)L.sq_cells) + c];
+        return v == kNoNode || m == kNone || is_ac(c) ? -1 : m;
+    }
     // the nearest-Cutboard / nearest-Delivery distance of node v (dmin row `side`), or -1
     OC_RH int dmin(int side, int v) const {
         const uint32_t i = (uint32_t)(side * L.nnodes + (v == kNoNode ? 0 : v));
@@ -682,6 +723,21 @@ struct RowOps {
         float lower = per + 1.0f;
         int vA[4], vB[NB][4];
         const bool Acoll = approaches(Ac, vA);
+        if (L.sq_off != 0 && s.n == 1) {  // wave-uniform: min over B's approaches from the table
+            const int nA = wave_any(Acoll) ? 4 : 1;
+#pragma unroll
+            for (int ia = 0; ia < 4; ++ia) {
+                if (ia >= nA) continue;  // wave-uniform
+                const int a1 = dn(u0, vA[ia]);
+#pragma unroll
+                for (int j = 0; j < NB; ++j) {
+                    const int b2 = dsq(vA[ia], Bc[j]);
+                    const float bound = (float)(a1 + b2 - 1);
+                    lower = a1 >= 0 && b2 >= 0 && bound < lower ? bound : lower;
+                }
+            }
+            return lower > 1.0f ? lower : 1.0f;
+        }
         bool Bcoll = false;
 #pragma unroll
         for (int j = 0; j < NB; ++j) Bcoll |= approaches(Bc[j], vB[j]);

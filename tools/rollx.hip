@@ -1,0 +1,441 @@
+// tools/rollx.hip -- round 6: where does a planner-shape rollout launch (4,096 rows, 64
+// configurations, one wave per configuration) spend its time, per configuration and per row
+// phase?    Standalone: it includes only the row code
+// (oc_rollout.h) and the SWAR step (oc_swar.h, to make mid-episode states), so it builds in
+// seconds.
+// Build: hipcc -O3 -std=c++20 --offload-arch=gfx950 -o tools/rollx tools/rollx.hip
+// Run:   tools/rollx LEVEL.bin   (full-divider_salad's oc_level_desc for 4 agents)
+// Workload: bench.py's C5 rows: 4 agents, mid-episode random-play states, the 64 Salad
+// (subtask, agents) configurations, random joint actions, rows configuration-major; 2^18 rows and
+// the planner's 4,096.
+//   product   oc_rollout_kernel's body (RowOps::run)
+//   stamped   the same row, restated with s_memrealtime stamps between its phases (outputs must
+//             equal the product's); per configuration: each phase's mean over the configuration's
+//             waves, and the launch's slowest waves
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../include/oc_engine.h"
+#include "../gym-cooking_amd/csrc/oc_rollout.h"
+#include "../gym-cooking_amd/csrc/oc_swar.h"
+
+#define CK(x)                                                                                      \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } \
+    } while (0)
+
+namespace {
+
+constexpr int A = 4, K = 4, NP = 3 * A + 2 * K + 3, kBlk = 256, kPhases = 9;
+constexpr int kPY = A, kPH = 2 * A, kPL = 3 * A, kPM = 3 * A + K, kPT = 3 * A + 2 * K, kPF = kPT + 2;
+
+struct RollArgs {
+    ocro::RollLevel L;
+    ocro::Sub subs[64];
+    int32_t nsub, blob_words;
+    int64_t pitch, B;
+};
+
+__device__ __forceinline__ ocro::RowT<K> load_row(const uint8_t* __restrict__ sin, int64_t P, int64_t e) {
+    ocro::RowT<K> r;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        r.x |= (uint32_t)sin[a * P + e] << (8 * a);
+        r.y |= (uint32_t)sin[(kPY + a) * P + e] << (8 * a);
+        r.h |= (uint32_t)sin[(kPH + a) * P + e] << (8 * a);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        r.loc[0] |= (uint64_t)sin[(kPL + j) * P + e] << (8 * j);
+        r.mask[0] |= (uint64_t)sin[(kPM + j) * P + e] << (8 * j);
+    }
+    return r;
+}
+__device__ __forceinline__ void store_row(uint8_t* __restrict__ sout, int64_t P, int64_t e, const ocro::RowT<K>& r) {
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        __builtin_nontemporal_store((uint8_t)r.ax(a), sout + a * P + e);
+        __builtin_nontemporal_store((uint8_t)r.ay(a), sout + (kPY + a) * P + e);
+        __builtin_nontemporal_store((uint8_t)r.ah(a), sout + (kPH + a) * P + e);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        __builtin_nontemporal_store((uint8_t)r.il(j), sout + (kPL + j) * P + e);
+        __builtin_nontemporal_store((uint8_t)r.im(j), sout + (kPM + j) * P + e);
+    }
+}
+
+template <bool STAMP>
+__global__ __launch_bounds__(kBlk) void k_roll(RollArgs R, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
+                                              const uint8_t* __restrict__ act, const uint8_t* __restrict__ alloc,
+                                              const uint8_t* __restrict__ blob_g, uint8_t* __restrict__ out_flags,
+                                              float* __restrict__ lb, uint64_t* __restrict__ tl) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t blob_w[];
+    __shared__ ocro::Sub subs[64];
+    const int64_t P = R.pitch;
+    const uint32_t wave = (blockIdx.x * (uint32_t)kBlk + threadIdx.x) >> 6;
+    const bool rec = STAMP && (threadIdx.x & 63u) == 0u;
+    uint64_t st[kPhases + 1];
+    auto stamp = [&](int i) {
+        if (STAMP) {
+            __builtin_amdgcn_s_waitcnt(0);
+            st[i] = __builtin_amdgcn_s_memrealtime();
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+        }
+    };
+    stamp(0);
+    int64_t e = blockIdx.x * (int64_t)kBlk + threadIdx.x;
+    ocro::RowT<K> r;
+    uint16_t t = 0;
+    uint8_t fl = 0;
+    int ai = 0;
+    uint32_t acts = 0;
+    if (e < R.B) {
+        r = load_row(sin, P, e);
+        t = ((const uint16_t*)(sin + kPT * P))[e];
+        fl = sin[kPF * P + e];
+        ai = alloc[e];
+#pragma unroll
+        for (int a = 0; a < A; ++a) acts |= (uint32_t)act[a * P + e] << (8 * a);
+    }
+    {
+        const int n16 = R.blob_words >> 2;
+        for (int i = threadIdx.x; i < n16; i += kBlk) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
+        for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += kBlk) blob_w[i] = ((const uint32_t*)blob_g)[i];
+        for (int i = threadIdx.x; i < R.nsub * 4; i += kBlk) ((uint32_t*)subs)[i] = ((const uint32_t*)R.subs)[i];
+        __syncthreads();
+    }
+    stamp(1);
+    const uint8_t* blob = (const uint8_t*)blob_w;
+    if (e >= R.B) return;
+    float bound = 0.0f;
+    int f = OC_ROLL_BADALLOC;
+    if (ai < R.nsub) {
+        const ocro::Sub& s = subs[ai];
+        int c0 = (acts >> (8 * s.agent[0])) & 0xFFu, c1 = s.n == 2 ? (acts >> (8 * s.agent[1])) & 0xFFu : ocro::kNoop;
+        ocro::RowOps<A, K> ops(R.L, blob);
+        if (!STAMP) {
+            f = ops.run(r, s, c0, c1, bound);
+        } else {  // RowOps::run, phase by phase
+            const ocro::RowT<K> r_in = r;
+            stamp(2);  // the row's loads waited for by the stamp
+            const bool raised = ops.level0(r, s);
+            stamp(3);
+            if (raised) {
+                r = r_in;
+                f = 8;
+                for (int i = 4; i <= kPhases; ++i) st[i] = st[3];
+            } else {
+                if (s.kind == 0) c0 = c1 = ocro::kNoop;
+                c0 = c0 > ocro::kNoop ? ocro::kNoop : c0;
+                c1 = c1 > ocro::kNoop ? ocro::kNoop : c1;
+                const auto g0 = ops.target(r, s.agent[0], c0);
+                const auto g1 = s.n == 2 ? ops.target(r, s.agent[1], c1) : g0;
+                f = ops.action_legal(r, s, c0, c1, g0, g1) ? 1 : 0;
+                stamp(4);
+                ops.interact(r, s.agent[0], c0, g0);
+                if (s.n == 2) ops.interact(r, s.agent[1], c1, g1);
+                stamp(5);
+                const bool asserted = s.n == 2 && ops.agent_cell(r, s.agent[0]) == ops.agent_cell(r, s.agent[1]);
+                if (asserted) f |= 4;
+                else if (ops.is_goal(r, s)) f |= 2;
+                stamp(6);
+                bound = ops.lower_bound(r, s);
+                stamp(7);
+            }
+        }
+    }
+    store_row(sout, P, e, r);
+    __builtin_nontemporal_store(t, (uint16_t*)(sout + kPT * P) + e);
+    __builtin_nontemporal_store(fl, sout + kPF * P + e);
+    __builtin_nontemporal_store((uint8_t)f, out_flags + e);
+    __builtin_nontemporal_store(bound, lb + e);
+    if (STAMP) {
+        __builtin_amdgcn_s_waitcnt(0);  // the stores acknowledged
+        stamp(8);
+        stamp(9);
+        if (rec) {
+            uint64_t* o = tl + (uint64_t)wave * (kPhases + 2);
+            o[0] = (uint64_t)ai;
+            for (int i = 0; i <= kPhases; ++i) o[1 + i] = st[i];
+        }
+    }
+}
+
+
+// Round 6 variant: the row's Level-0 view is built while the level tables are still on their
+// way: the row loads, then the table blob's 16-byte loads into registers (up to kQ per lane, all
+// in flight at once), the configurations into LDS, an LDS-only barrier, level0, then the blob
+// into LDS and a second barrier.  (The product stages with a loop whose rounds each wait for
+// their load before the LDS write, and builds the view after the barrier.)
+constexpr int kQ = 4;  // blob <= kQ x 256 x 16 B = 16 KB staged this way
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+__global__ __launch_bounds__(kBlk) void k_roll_early(RollArgs R, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
+                                                    const uint8_t* __restrict__ act, const uint8_t* __restrict__ alloc,
+                                                    const uint8_t* __restrict__ blob_g, uint8_t* __restrict__ out_flags,
+                                                    float* __restrict__ lb, uint64_t* __restrict__ tl) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t blob_w[];
+    __shared__ ocro::Sub subs[64];
+    const int64_t P = R.pitch;
+    int64_t e = blockIdx.x * (int64_t)kBlk + threadIdx.x;
+    const bool live = e < R.B;
+    const int64_t ee = live ? e : 0;
+    ocro::RowT<K> r = load_row(sin, P, ee);
+    const uint16_t t = ((const uint16_t*)(sin + kPT * P))[ee];
+    const uint8_t fl = sin[kPF * P + ee];
+    const int ai = alloc[ee];
+    uint32_t acts = 0;
+#pragma unroll
+    for (int a = 0; a < A; ++a) acts |= (uint32_t)act[a * P + ee] << (8 * a);
+    const int n16 = R.blob_words >> 2;
+    uint4 q[kQ];
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) {
+        const int i = threadIdx.x + k * kBlk;
+        if (i < n16) q[k] = ((const uint4*)blob_g)[i];
+    }
+    for (int i = threadIdx.x; i < R.nsub * 4; i += kBlk) ((uint32_t*)subs)[i] = ((const uint32_t*)R.subs)[i];
+    lds_barrier();  // the configurations; the blob's loads stay in flight
+    const uint8_t* blob = (const uint8_t*)blob_w;
+    ocro::RowOps<A, K> ops(R.L, blob);
+    const bool ok = ai < R.nsub;
+    const ocro::Sub& s = subs[ok ? ai : 0];
+    const ocro::RowT<K> r_in = r;
+    const bool raised = ops.level0(r, s);  // reads no table
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) {
+        const int i = threadIdx.x + k * kBlk;
+        if (i < n16) ((uint4*)blob_w)[i] = q[k];
+    }
+    for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += kBlk) blob_w[i] = ((const uint32_t*)blob_g)[i];
+    lds_barrier();
+    if (!live) return;
+    float bound = 0.0f;
+    int f = OC_ROLL_BADALLOC;
+    if (!ok) {
+        r = r_in;
+    } else if (raised) {
+        r = r_in;
+        f = 8;
+    } else {
+        int c0 = (acts >> (8 * s.agent[0])) & 0xFFu, c1 = s.n == 2 ? (acts >> (8 * s.agent[1])) & 0xFFu : ocro::kNoop;
+        if (s.kind == 0) c0 = c1 = ocro::kNoop;
+        c0 = c0 > ocro::kNoop ? ocro::kNoop : c0;
+        c1 = c1 > ocro::kNoop ? ocro::kNoop : c1;
+        const auto g0 = ops.target(r, s.agent[0], c0);
+        const auto g1 = s.n == 2 ? ops.target(r, s.agent[1], c1) : g0;
+        f = ops.action_legal(r, s, c0, c1, g0, g1) ? 1 : 0;
+        ops.interact(r, s.agent[0], c0, g0);
+        if (s.n == 2) ops.interact(r, s.agent[1], c1, g1);
+        const bool asserted = s.n == 2 && ops.agent_cell(r, s.agent[0]) == ops.agent_cell(r, s.agent[1]);
+        if (asserted) f |= 4;
+        else if (ops.is_goal(r, s)) f |= 2;
+        bound = ops.lower_bound(r, s);
+    }
+    store_row(sout, P, e, r);
+    __builtin_nontemporal_store(t, (uint16_t*)(sout + kPT * P) + e);
+    __builtin_nontemporal_store(fl, sout + kPF * P + e);
+    __builtin_nontemporal_store((uint8_t)f, out_flags + e);
+    __builtin_nontemporal_store(bound, lb + e);
+    (void)tl;
+}
+
+__global__ void k_gen(ocsw::SwarLevel sw, const uint32_t* cls4g, uint8_t* s, int64_t P, int steps, uint32_t seed) {
+    __shared__ uint32_t cls4[64];
+    if (threadIdx.x < 64u) cls4[threadIdx.x] = cls4g[threadIdx.x];
+    __syncthreads();
+    const uint8_t* tbl = (const uint8_t*)cls4;
+    auto cls_of = [&](uint32_t c) -> uint32_t {
+        return (uint32_t)tbl[c & 0xFFu] | ((uint32_t)tbl[(c >> 8) & 0xFFu] << 8) | ((uint32_t)tbl[(c >> 16) & 0xFFu] << 16) |
+               ((uint32_t)tbl[c >> 24] << 24);
+    };
+    const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (g * 4 >= P) return;
+    uint32_t X[A], Y[A], H[A], L[K], M[K], T0, T1, F, EX[A], CM, act[A];
+    auto w = [&](int plane) -> uint32_t* { return (uint32_t*)(s + plane * P) + g; };
+    for (int a = 0; a < A; ++a) { X[a] = *w(a); Y[a] = *w(kPY + a); H[a] = *w(kPH + a); }
+    for (int j = 0; j < K; ++j) { L[j] = *w(kPL + j); M[j] = *w(kPM + j); }
+    T0 = ((uint32_t*)(s + kPT * P))[2 * g];
+    T1 = ((uint32_t*)(s + kPT * P))[2 * g + 1];
+    F = *w(kPF);
+    for (int r = 0; r < steps; ++r) {
+        for (int a = 0; a < A; ++a) {
+            uint32_t h = (uint32_t)g * 0x9E3779B1u ^ (uint32_t)r * 0x85EBCA6Bu ^ (uint32_t)(a + 1) * 0xC2B2AE35u ^ seed;
+            h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+            act[a] = ((h & 0xFFu) % 5u) | (((h >> 8) & 0xFFu) % 5u) << 8 | (((h >> 16) & 0xFFu) % 5u) << 16 | ((h >> 24) % 5u) << 24;
+        }
+        uint32_t pending = 0xFFFFFFFFu;
+        ocsw::step4<A, K, 1>(sw, X, Y, H, L, M, T0, T1, F, act, EX, CM, cls_of, [](uint32_t) { return true; }, pending);
+    }
+    for (int a = 0; a < A; ++a) { *w(a) = X[a]; *w(kPY + a) = Y[a]; *w(kPH + a) = H[a]; }
+    for (int j = 0; j < K; ++j) { *w(kPL + j) = L[j]; *w(kPM + j) = M[j]; }
+    ((uint32_t*)(s + kPT * P))[2 * g] = T0;
+    ((uint32_t*)(s + kPT * P))[2 * g + 1] = T1;
+    *w(kPF) = F;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    oc_level_desc lv{};
+    FILE* fp = fopen(argc > 1 ? argv[1] : "gpurun_out/c5_level.bin", "rb");
+    if (fp == nullptr || fread(&lv, sizeof lv, 1, fp) != 1) { printf("level file\n"); return 1; }
+    fclose(fp);
+    const int W = lv.width, H = lv.height;
+    RollArgs R{};
+    std::vector<uint8_t> blob;
+    if (ocro::build_roll_level(R.L, blob, W, H, lv.tiles, lv.encoding) < 0) { printf("level tables\n"); return 1; }
+    R.blob_words = R.L.lds_bytes / 4;
+    printf("level tables: %d nodes, blob %d B, node-to-square table at %d\n", R.L.nnodes, R.L.blob_bytes, R.L.sq_off);
+    // the 64 Salad configurations (bench.py SALAD_SUBTASKS x agent sets), as roll_args packs them
+    const int sal[9][4] = {{1, 0x01, 0, 0x11}, {1, 0x02, 0, 0x22}, {2, 0x11, 0x22, 0x33}, {2, 0x11, 0x08, 0x19},
+                           {2, 0x22, 0x08, 0x2A}, {2, 0x33, 0x08, 0x3B}, {2, 0x19, 0x22, 0x3B}, {2, 0x2A, 0x11, 0x3B},
+                           {3, 0x3B, 0, 0x3B}};
+    std::vector<std::vector<int>> sets;
+    for (int i = 0; i < A; ++i) sets.push_back({i});
+    for (int i = 0; i < A; ++i)
+        for (int j = i + 1; j < A; ++j) sets.push_back({i, j});
+    int ns = 0;
+    for (int k = 0; k < 9 && ns < 64; ++k)
+        for (auto& ag : sets) {
+            if (ns == 64) break;
+            ocro::Sub& d = R.subs[ns++];
+            d.kind = sal[k][0];
+            d.n = (int)ag.size();
+            d.agent[0] = (uint8_t)ag[0];
+            d.agent[1] = (uint8_t)(ag.size() == 2 ? ag[1] : ag[0]);
+            d.start[0] = (uint8_t)sal[k][1];
+            d.start[1] = (uint8_t)sal[k][2];
+            d.goal = (uint8_t)sal[k][3];
+            d.count = 0;
+            d.level = 0;
+        }
+    R.nsub = ns;
+    // states: the template, then 37 random steps (bench.py's C5 rows are 37 steps in)
+    const int64_t B = 1 << 18, P = B;
+    ocsw::SwarLevel sw;
+    uint8_t cell[16], mask[16];
+    uint32_t cls4[64] = {};
+    int done_cell = -1;
+    for (int j = 0; j < 16; ++j) {
+        cell[j] = j < lv.num_items ? (uint8_t)lv.item_cell[j] : 0xFF;
+        mask[j] = j < lv.num_items ? lv.item_mask[j] : 0;
+    }
+    for (int c = 0; c < W * H; ++c) {
+        cls4[c >> 2] |= (uint32_t)ocsw::tile_class(lv.tiles[c]) << (8 * (c & 3));
+        if (lv.tiles[c] == OC_TILE_DELIVERY && done_cell < 0) done_cell = c;
+    }
+    ocsw::build_swar_level(sw, W, H, done_cell, lv.goal_mask, lv.num_goals, 100, lv.spawn_x, lv.spawn_y, A, cell, mask,
+                           lv.encoding, lv.tiles);
+    std::vector<uint8_t> s0((size_t)NP * P, 0);
+    for (int a = 0; a < A; ++a) {
+        memset(&s0[(size_t)a * P], lv.spawn_x[a], P);
+        memset(&s0[(size_t)(kPY + a) * P], lv.spawn_y[a], P);
+        memset(&s0[(size_t)(kPH + a) * P], 0xFF, P);
+    }
+    for (int j = 0; j < K; ++j) {
+        memset(&s0[(size_t)(kPL + j) * P], cell[j], P);
+        memset(&s0[(size_t)(kPM + j) * P], mask[j], P);
+    }
+    uint8_t *sin, *sout, *act, *alloc, *blob_g, *fl;
+    float* lb;
+    uint32_t* cls4g;
+    uint64_t* tl;
+    CK(hipMalloc(&sin, s0.size())); CK(hipMalloc(&sout, s0.size())); CK(hipMalloc(&act, (size_t)A * P));
+    CK(hipMalloc(&alloc, P)); CK(hipMalloc(&blob_g, blob.size())); CK(hipMalloc(&fl, P)); CK(hipMalloc(&lb, 4 * P));
+    CK(hipMalloc(&cls4g, 256)); CK(hipMalloc(&tl, (P / 64) * (kPhases + 2) * 8));
+    CK(hipMemcpy(sin, s0.data(), s0.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(blob_g, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(cls4g, cls4, 256, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_gen, dim3((unsigned)(P / 4 / 256)), dim3(256), 0, nullptr, sw, cls4g, sin, P, 37, 11u);
+    std::vector<uint8_t> ah((size_t)A * P), al(P);
+    uint64_t x = 88172645463325252ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    for (auto& v : ah) v = (uint8_t)(rnd() % 5);
+    for (auto& v : al) v = (uint8_t)(rnd() % ns);
+    std::vector<uint8_t> al_small(al.begin(), al.begin() + 4096);
+    std::sort(al.begin(), al.end());
+    std::sort(al_small.begin(), al_small.end());
+    CK(hipMemcpy(act, ah.data(), ah.size(), hipMemcpyHostToDevice));
+    const int dyn = R.L.lds_bytes;
+    CK(hipFuncSetAttribute((const void*)k_roll<false>, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(dyn, 1)));
+    CK(hipFuncSetAttribute((const void*)k_roll<true>, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(dyn, 1)));
+    CK(hipFuncSetAttribute((const void*)k_roll_early, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(dyn, 1)));
+    if (R.blob_words / 4 > kQ * kBlk) { printf("blob too large for the early variant\n"); return 1; }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    std::vector<uint8_t> ref_s, ref_f, got_s, got_f;
+    for (int shape = 0; shape < 2; ++shape) {
+        const int64_t rows = shape == 0 ? B : 4096;
+        R.pitch = P;
+        R.B = rows;
+        CK(hipMemcpy(alloc, shape == 0 ? al.data() : al_small.data(), rows, hipMemcpyHostToDevice));
+        const unsigned grid = (unsigned)((rows + kBlk - 1) / kBlk);
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlk), dyn, nullptr, R, sin, sout, act, alloc, blob_g, fl, lb, tl);
+        };
+        auto tm = [&](const char* name, auto kern, int reps) {
+            for (int i = 0; i < 3; ++i) go(kern);
+            CK(hipEventRecord(e0));
+            for (int i = 0; i < reps; ++i) go(kern);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            got_s.resize((size_t)NP * P);
+            got_f.resize((size_t)5 * rows);
+            CK(hipMemcpy(got_s.data(), sout, got_s.size(), hipMemcpyDeviceToHost));
+            CK(hipMemcpy(got_f.data(), fl, rows, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(got_f.data() + rows, lb, 4 * rows, hipMemcpyDeviceToHost));
+            const bool first = ref_s.empty();
+            if (first) { ref_s = got_s; ref_f = got_f; }
+            printf("%6lld rows  %-30s %8.3f us  outputs %s\n", (long long)rows, name, ms * 1e3 / reps,
+                   first ? "(reference)" : (got_s == ref_s && got_f == ref_f) ? "identical" : "DIFFER");
+            fflush(stdout);
+        };
+        ref_s.clear();
+        const int32_t sq_off = R.L.sq_off;
+        for (int rep = 0; rep < 2; ++rep) {
+            R.L.sq_off = 0;
+            tm("product, no node-to-square table", k_roll<false>, shape == 0 ? 200 : 400);
+            R.L.sq_off = sq_off;
+            tm("product (node-to-square table)", k_roll<false>, shape == 0 ? 200 : 400);
+            tm("early view, batched staging", k_roll_early, shape == 0 ? 200 : 400);
+            tm("stamped", k_roll<true>, shape == 0 ? 200 : 400);
+        }
+        if (shape == 1) {  // the planner shape's phases per configuration (100 MHz stamps)
+            const int nw = (int)((rows + 63) / 64);
+            std::vector<uint64_t> v((size_t)nw * (kPhases + 2));
+            CK(hipMemcpy(v.data(), tl, v.size() * 8, hipMemcpyDeviceToHost));
+            uint64_t t0 = ~0ull;
+            for (int w = 0; w < nw; ++w) t0 = std::min(t0, v[(size_t)w * (kPhases + 2) + 1]);
+            const char* names[kPhases] = {"stage", "rowload", "level0", "legal", "interact", "goal", "bound", "store", "-"};
+            printf("planner shape: per wave (config of lane 0): start, then phase durations in us\n");
+            std::vector<std::pair<double, int>> order;
+            for (int w = 0; w < nw; ++w) {
+                const uint64_t* o = &v[(size_t)w * (kPhases + 2)];
+                order.push_back({(o[1 + 8] - t0) * 0.01, w});
+            }
+            std::sort(order.begin(), order.end());
+            for (auto& [end, w] : order) {
+                const uint64_t* o = &v[(size_t)w * (kPhases + 2)];
+                const ocro::Sub& s = R.subs[o[0] < 64 ? o[0] : 0];
+                printf("  wave %2d cfg %2llu kind %d n %d start %5.2f |", w, (unsigned long long)o[0], s.kind, s.n,
+                       (o[1] - t0) * 0.01);
+                for (int i = 0; i < 8; ++i) printf(" %s %5.2f", names[i], (o[2 + i] - o[1 + i]) * 0.01);
+                printf(" | end %6.2f\n", end);
+            }
+        }
+    }
+    return 0;
+}
