@@ -629,6 +629,9 @@ __device__ __forceinline__ void store_row(uint8_t* __restrict__ sout, int64_t P,
 #ifndef OC_ROLL_BLOCK
 #define OC_ROLL_BLOCK 256
 #endif
+#ifndef OC_ROLL_GROUP
+#define OC_ROLL_GROUP 4
+#endif
 // The rollout kernel's block (one row per lane).  512- and 1,024-lane blocks (fewer blocks to
 // dispatch, each staging the tables with more lanes) measured slower at C5: 12.0-12.3 and
 // 12.2-12.4 us against 11.6 (profiles/r05/ab/ab_merge_pairs_blocks.jsonl).  One-wave blocks for
@@ -690,6 +693,192 @@ __global__ __launch_bounds__(kRollBlock) void oc_rollout_kernel(RollArgs R, cons
             f = ops.run(r, s, c0, c1, bound);
         }
         store_row<A, K, W, true>(sout, P, e, r);
+        __builtin_nontemporal_store(t, (uint16_t*)(sout + PL::T * P) + e);
+        __builtin_nontemporal_store(fl_in, sout + PL::F * P + e);
+        __builtin_nontemporal_store((uint8_t)f, out_flags + e);
+        __builtin_nontemporal_store(bound, lb + e);
+    }
+}
+
+// Lane-group rollout rows (round 6), for launches that fit one round of blocks with G lanes per
+// row: the planner's own launches (<= 4,096 rows), where the launch lasts as long as its slowest
+// wave's row chain.  The G lanes of a group run one row together: every lane builds the Level-0
+// view and runs legality, interact and the goal test (one chain), and the lower bound -- the
+// longest phase (2.4 of the 8.8 us of a 4,096-row launch, tools/rollx.hip ablations) -- splits
+// its approach walks: lane q takes A approach q * 4 / G .. (one-agent rows and the static Chop /
+// Deliver side) or B square q & 1 of each Merge pair (two agents, whose per-type minima need both
+// sides whole).  The group's minima meet by DPP swaps inside a quad; lane 0 stores.  4,096 rows:
+// 8.91 us one row per lane, 7.96 lane pairs, 7.76 lane quads; splitting a two-agent row's
+// legality by agent as well, 8.02 / 7.82 (profiles/r06/pass_n/rollx.log).  Narrow levels with LDS
+// distances only (every kitchen the reference ships); the others keep one row per lane.
+constexpr int kRollGroup = OC_ROLL_GROUP;
+template <int G>
+__device__ __forceinline__ float group_min(float v) {
+    static_assert(G == 2 || G == 4, "lane groups of 2 or 4");
+    int o = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    v = __int_as_float(o) < v ? __int_as_float(o) : v;
+    if (G == 4) {
+        o = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+        v = __int_as_float(o) < v ? __int_as_float(o) : v;
+    }
+    return v;
+}
+template <int G, int A, int K>
+struct GroupRowOps : ocro::RowOps<A, K> {
+    using Base = ocro::RowOps<A, K>;
+    using typename Base::Row;
+    using typename Base::Target;
+    using Base::L;
+    using Base::T;
+    static constexpr int NA = 4 / G;  // A approaches per lane when the walk takes four
+    int q;                            // this lane's index in its group
+    __device__ GroupRowOps(const ocro::RollLevel& l, const uint8_t* blob, int lane) : Base(l, blob), q(lane) {}
+    __device__ int approach(bool four, int k) const { return four ? NA * q + k : 0; }
+
+    // Base::helper_static over this lane's A approaches
+    __device__ float helper_static(const ocro::Sub& s, int u0, int u1, int Ac, int nb, int side, const uint16_t* man_t) const {
+        const float per = (float)L.perimeter;
+        float lower = per + 1.0f;
+        if (nb == 0) return lower;
+        int vAs[4];
+        const bool four = ocro::wave_any(this->approaches(Ac, vAs));
+        if (s.n == 1) {
+#pragma unroll
+            for (int k = 0; k < NA; ++k) {
+                const int vA = vAs[approach(four, k)];
+                const int a1 = this->dn(u0, vA), m = this->dmin(side, vA);
+                const float bound = (float)(a1 + m - 1);
+                lower = vA != ocro::kNoNode && a1 >= 0 && m >= 0 && bound < lower ? bound : lower;
+                if (!four) break;  // wave-uniform: a Floor square's one node
+            }
+        } else {
+            const int man = man_t[Ac];
+            float mA = per;
+#pragma unroll
+            for (int k = 0; k < NA; ++k) {
+                const int vA = vAs[approach(four, k)];
+                int t;
+                const float b1A = (t = this->dn(u0, vA)) < 0 ? per : (float)t;
+                const float b2A = (t = this->dn(u1, vA)) < 0 ? per : (float)t;
+                const float m2 = b1A < b2A ? b1A : b2A;
+                mA = m2 < mA ? m2 : mA;
+                if (!four) break;
+            }
+            const float bound = mA + (float)man - 1.0f;
+            if (bound < lower) lower = bound;
+        }
+        return lower > 1.0f ? lower : 1.0f;
+    }
+    // Base::helper_n<2>(Ac, {B1, B2}): one agent, this lane's A approaches (the node-to-square
+    // table when the level has one); two agents, B square q & 1
+    __device__ float helper_pair(const ocro::Sub& s, int u0, int u1, int Ac, int B1, int B2) const {
+        if (s.n == 1 && L.sq_off != 0) {
+            float lower = (float)L.perimeter + 1.0f;
+            int vA[4];
+            const bool four = ocro::wave_any(this->approaches(Ac, vA));
+#pragma unroll
+            for (int k = 0; k < NA; ++k) {
+                const int v = vA[approach(four, k)];
+                const int a1 = this->dn(u0, v), b1 = this->dsq(v, B1), b2 = this->dsq(v, B2);
+                const float x1 = (float)(a1 + b1 - 1), x2 = (float)(a1 + b2 - 1);
+                lower = a1 >= 0 && b1 >= 0 && x1 < lower ? x1 : lower;
+                lower = a1 >= 0 && b2 >= 0 && x2 < lower ? x2 : lower;
+                if (!four) break;
+            }
+            return lower > 1.0f ? lower : 1.0f;
+        }
+        const int Bc[1] = {(q & 1) ? B2 : B1};
+        return this->template helper_n<1>(s, u0, u1, Ac, Bc);
+    }
+    // Base::lower_bound with the walks split; the group's min (the clamps are monotone)
+    __device__ float lower_bound(const Row& r, const ocro::Sub& s) const {
+        const auto br = this->template bound_row<false>(r);
+        int u0, u1;
+        float pen;
+        this->template bound_agents<false>(br, s, u0, u1, pen);
+        float lower = (float)L.perimeter + 1.0f;
+        if (s.kind == 1 || s.kind == 3) {
+            const int nb = s.kind == 1 ? L.ncut : L.ndeliv;
+            const int side = s.kind == 1 ? 0 : 1;
+            const uint16_t* man_t = (const uint16_t*)(T + L.man_off) + (s.kind == 1 ? 0 : L.man_stride);
+            this->template visit_objs<false>(br, r, s.start[0], s.kind == 3, [&](int Ac) {
+                const float b = helper_static(s, u0, u1, Ac, nb, side, man_t);
+                if (b < lower) lower = b;
+            });
+        } else if (s.kind == 2) {
+            this->template visit_objs<false>(br, r, s.start[0], false, [&](int Ac) {
+                this->template visit_obj_pairs<false>(br, r, s.start[1], false, [&](int B1, int B2) {
+                    const float b = helper_pair(s, u0, u1, Ac, B1, B2);
+                    if (b < lower) lower = b;
+                });
+            });
+        }
+        return group_min<G>(lower) + pen;
+    }
+    // Base::run
+    __device__ int run(Row& r, const ocro::Sub& s, int c0, int c1, float& lb) {
+        const Row r_in = r;
+        if (this->level0(r, s)) {
+            r = r_in;
+            lb = 0.0f;
+            return 8;  // OC_ROLL_RAISES
+        }
+        if (s.kind == 0) c0 = c1 = ocro::kNoop;
+        c0 = c0 > ocro::kNoop ? ocro::kNoop : c0;
+        c1 = c1 > ocro::kNoop ? ocro::kNoop : c1;
+        const Target g0 = this->target(r, s.agent[0], c0), g1 = s.n == 2 ? this->target(r, s.agent[1], c1) : g0;
+        int fl = this->action_legal(r, s, c0, c1, g0, g1) ? 1 : 0;
+        this->interact(r, s.agent[0], c0, g0);
+        if (s.n == 2) this->interact(r, s.agent[1], c1, g1);
+        const bool asserted = s.n == 2 && this->agent_cell(r, s.agent[0]) == this->agent_cell(r, s.agent[1]);
+        if (asserted) fl |= 4;
+        else if (this->is_goal(r, s)) fl |= 2;
+        lb = lower_bound(r, s);
+        return fl;
+    }
+};
+// One round of blocks: G * B <= the grid's lanes (oc_rollout checks), so no grid-stride loop.
+template <int A, int K>
+__global__ __launch_bounds__(kRollBlock) void oc_rollout_group_kernel(RollArgs R, const uint8_t* __restrict__ sin,
+                                                                  uint8_t* __restrict__ sout,
+                                                                  const uint8_t* __restrict__ act,
+                                                                  const uint8_t* __restrict__ alloc,
+                                                                  const uint8_t* __restrict__ blob_g,
+                                                                  uint8_t* __restrict__ out_flags,
+                                                                  float* __restrict__ lb) {
+    constexpr int G = kRollGroup;
+    extern __shared__ __attribute__((aligned(16))) uint32_t blob_w[];
+    __shared__ ocro::Sub subs[OC_MAX_SUBTASKS];
+    const int64_t P = R.pitch;
+    using PL = Planes<A, K, false>;
+    const int q = (int)(threadIdx.x & (G - 1));
+    const int64_t e = (blockIdx.x * (int64_t)kRollBlock + threadIdx.x) / G;
+    const bool live = e < R.B;  // whole groups: B ends on a group boundary
+    ocro::RowT<K> r;
+    uint16_t t = 0;
+    uint8_t fl_in = 0;
+    int ai = 0;
+    uint32_t acts = 0;
+    if (live) {  // every lane of the group loads the row (the same bytes: one transaction)
+        r = load_row<A, K>(sin, P, e);
+        t = ((const uint16_t*)(sin + PL::T * P))[e];
+        fl_in = sin[PL::F * P + e];
+        ai = alloc != nullptr ? alloc[e] : 0;
+#pragma unroll
+        for (int a = 0; a < A; ++a) acts |= (uint32_t)act[a * P + e] << (8 * a);
+    }
+    stage_roll_tables<kRollBlock>(R, blob_g, blob_w, subs);
+    if (!live) return;
+    float bound = 0.0f;
+    int f = OC_ROLL_BADALLOC;
+    if (ai < R.nsub) {
+        const ocro::Sub& s = subs[ai];
+        const int c0 = (acts >> (8 * s.agent[0])) & 0xFFu, c1 = s.n == 2 ? (acts >> (8 * s.agent[1])) & 0xFFu : ocro::kNoop;
+        GroupRowOps<G, A, K> ops(R.L, (const uint8_t*)blob_w, q);
+        f = ops.run(r, s, c0, c1, bound);
+    }
+    if (q == 0) {
+        store_row<A, K, false, true>(sout, P, e, r);
         __builtin_nontemporal_store(t, (uint16_t*)(sout + PL::T * P) + e);
         __builtin_nontemporal_store(fl_in, sout + PL::F * P + e);
         __builtin_nontemporal_store((uint8_t)f, out_flags + e);
@@ -2488,6 +2677,17 @@ int oc_rollout(const oc_handle* h, const void* state_in, void* state_out, const 
     const int64_t need = (B + kRollBlock - 1) / kRollBlock, cap = (int64_t)h->cus * 8 * kBlock / kRollBlock;
     const dim3 grid((unsigned)(need < cap ? need : cap));
     hipStream_t st = (hipStream_t)stream;
+    if (!h->wide && !h->roll.dist_global && B * kRollGroup <= (int64_t)h->cus * kRollBlock) {
+        // one round of blocks with a lane group per row (oc_rollout_group_kernel)
+        const dim3 ggrid((unsigned)((B * kRollGroup + kRollBlock - 1) / kRollBlock));
+#define OC_LAUNCH_ROLL_GROUP(A, K)                                                                                  \
+    if (const int rc = allow_dyn_lds((const void*)oc_rollout_group_kernel<A, K>, R.blob_words * 4)) return rc;        \
+    hipLaunchKernelGGL((oc_rollout_group_kernel<A, K>), ggrid, dim3(kRollBlock), R.blob_words * 4, st, R,            \
+                       (const uint8_t*)state_in, (uint8_t*)state_out, actions, alloc, h->roll_blob, out_flags, lower_bound)
+        OC_DISPATCH(h->A, h->K, OC_LAUNCH_ROLL_GROUP)
+#undef OC_LAUNCH_ROLL_GROUP
+        return hip_check("oc_rollout launch");
+    }
 #define OC_LAUNCH_ROLL(A, K, W, GD)                                                                             \
     if (const int rc = allow_dyn_lds((const void*)oc_rollout_kernel<A, K, W, GD>, R.blob_words * 4)) return rc;   \
     hipLaunchKernelGGL((oc_rollout_kernel<A, K, W, GD>), grid, dim3(kRollBlock), R.blob_words * 4, st, R,            \

@@ -47,8 +47,11 @@ def _random_case(level, A, B, seed):
     return th.random_rollout_case(level, A, B, seed, planner_levels=(0, 1))
 
 
+# Launches of up to CUs x 256 / 4 rows (16,384 on MI355X) run a lane quad per row
+# (oc_rollout_group_kernel), larger ones a row per lane: both sides of that boundary are here.
 @pytest.mark.parametrize("level,A,B", [("open-divider_salad", 2, 5000), ("partial-divider_tl", 3, 4099),
-                                       ("full-divider_salad", 4, 1 << 18), ("open-divider_tomato", 1, 17)])
+                                       ("full-divider_salad", 4, 1 << 18), ("open-divider_tomato", 1, 17),
+                                       ("partial-divider_tl", 3, 16384), ("open-divider_salad", 2, 16385)])
 def test_rollout_matches_oracle_random(level, A, B):
     ob, s, acts, subs, alloc = _random_case(level, A, B, seed=B + A)
     o_out = ob.new_state()

@@ -250,6 +250,258 @@ __global__ __launch_bounds__(kBlk) void k_roll_early(RollArgs R, const uint8_t* 
     (void)tl;
 }
 
+
+// Ablations (timing only, outputs differ): the product row with phases left out.  SKIP bits:
+// 1 the bound, 2 the legality, 4 interact, 8 the Level-0 view (bound_config instead), 16 the
+// goal test, 32 every phase (load, stage, store).
+template <int SKIP>
+__global__ __launch_bounds__(kBlk) void k_ablate(RollArgs R, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
+                                                const uint8_t* __restrict__ act, const uint8_t* __restrict__ alloc,
+                                                const uint8_t* __restrict__ blob_g, uint8_t* __restrict__ out_flags,
+                                                float* __restrict__ lb, uint64_t* __restrict__ tl) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t blob_w[];
+    __shared__ ocro::Sub subs[64];
+    const int64_t P = R.pitch;
+    int64_t e = blockIdx.x * (int64_t)kBlk + threadIdx.x;
+    ocro::RowT<K> r;
+    uint16_t t = 0;
+    uint8_t fl = 0;
+    int ai = 0;
+    uint32_t acts = 0;
+    if (e < R.B) {
+        r = load_row(sin, P, e);
+        t = ((const uint16_t*)(sin + kPT * P))[e];
+        fl = sin[kPF * P + e];
+        ai = alloc[e];
+#pragma unroll
+        for (int a = 0; a < A; ++a) acts |= (uint32_t)act[a * P + e] << (8 * a);
+    }
+    {
+        const int n16 = R.blob_words >> 2;
+        for (int i = threadIdx.x; i < n16; i += kBlk) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
+        for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += kBlk) blob_w[i] = ((const uint32_t*)blob_g)[i];
+        for (int i = threadIdx.x; i < R.nsub * 4; i += kBlk) ((uint32_t*)subs)[i] = ((const uint32_t*)R.subs)[i];
+        __syncthreads();
+    }
+    const uint8_t* blob = (const uint8_t*)blob_w;
+    if (e >= R.B) return;
+    float bound = 0.0f;
+    int f = OC_ROLL_BADALLOC;
+    if (!(SKIP & 32) && ai < R.nsub) {
+        const ocro::Sub& s = subs[ai];
+        int c0 = (acts >> (8 * s.agent[0])) & 0xFFu, c1 = s.n == 2 ? (acts >> (8 * s.agent[1])) & 0xFFu : ocro::kNoop;
+        ocro::RowOps<A, K> ops(R.L, blob);
+        bool raised = false;
+        if (SKIP & 8) ops.bound_config(s);
+        else raised = ops.level0(r, s);
+        if (!raised) {
+            if (s.kind == 0) c0 = c1 = ocro::kNoop;
+            c0 = c0 > ocro::kNoop ? ocro::kNoop : c0;
+            c1 = c1 > ocro::kNoop ? ocro::kNoop : c1;
+            const auto g0 = ops.target(r, s.agent[0], c0);
+            const auto g1 = s.n == 2 ? ops.target(r, s.agent[1], c1) : g0;
+            f = (SKIP & 2) ? (g0.t ^ g1.t) & 1 : ops.action_legal(r, s, c0, c1, g0, g1) ? 1 : 0;
+            if (!(SKIP & 4)) {
+                ops.interact(r, s.agent[0], c0, g0);
+                if (s.n == 2) ops.interact(r, s.agent[1], c1, g1);
+            } else {
+                r.x ^= (uint32_t)(g0.c ^ g1.c);
+            }
+            if (!(SKIP & 16)) {
+                const bool asserted = s.n == 2 && ops.agent_cell(r, s.agent[0]) == ops.agent_cell(r, s.agent[1]);
+                if (asserted) f |= 4;
+                else if (ops.is_goal(r, s)) f |= 2;
+            }
+            if (!(SKIP & 1)) bound = ops.lower_bound(r, s);
+        } else {
+            f = 8;
+        }
+    }
+    store_row(sout, P, e, r);
+    __builtin_nontemporal_store(t, (uint16_t*)(sout + kPT * P) + e);
+    __builtin_nontemporal_store(fl, sout + kPF * P + e);
+    __builtin_nontemporal_store((uint8_t)f, out_flags + e);
+    __builtin_nontemporal_store(bound, lb + e);
+    (void)tl;
+}
+
+
+// Lane-group rows (VERDICT r05 #2's untried form): G = 2 or 4 lanes run row i together (lanes
+// G*i .. G*i + G - 1).  The bound's approach loops split between them (lane q takes A approaches
+// q*4/G .. ; a two-agent Merge takes B square q & 1 of each pair), a two-agent row's legality
+// splits by agent (LEG), and the group's minima meet by DPP swaps.  Everything else runs on
+// every lane of the group; lane 0 stores.
+template <int G>
+__device__ __forceinline__ float grp_min(float v) {
+    int o = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    v = __int_as_float(o) < v ? __int_as_float(o) : v;
+    if (G == 4) {
+        o = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+        v = __int_as_float(o) < v ? __int_as_float(o) : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int pair_and(int v) { return v & __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }
+template <int G>
+struct GrpOps : ocro::RowOps<A, K> {
+    using Base = ocro::RowOps<A, K>;
+    static constexpr int NA = 4 / G;  // A approaches per lane
+    int q;
+    __device__ GrpOps(const ocro::RollLevel& l, const uint8_t* blob, int lane) : Base(l, blob), q(lane) {}
+    __device__ int ia(bool four, int k) const { return four ? NA * q + k : 0; }
+    __device__ float helper_static_p(const ocro::Sub& s, int u0, int u1, int Ac, int nb, int side, const uint16_t* man_t) const {
+        const float per = (float)L.perimeter;
+        float lower = per + 1.0f;
+        if (nb == 0) return lower;
+        int vAs[4];
+        const bool four = ocro::wave_any(approaches(Ac, vAs));
+        if (s.n == 1) {
+#pragma unroll
+            for (int k = 0; k < NA; ++k) {
+                const int vA = vAs[ia(four, k)];
+                const int a1 = dn(u0, vA), m = dmin(side, vA);
+                const float bound = (float)(a1 + m - 1);
+                lower = vA != ocro::kNoNode && a1 >= 0 && m >= 0 && bound < lower ? bound : lower;
+                if (!four) break;
+            }
+        } else {
+            const int man = man_t[Ac];
+            float mA = per;
+#pragma unroll
+            for (int k = 0; k < NA; ++k) {
+                const int vA = vAs[ia(four, k)];
+                int t;
+                const float b1A = (t = dn(u0, vA)) < 0 ? per : (float)t;
+                const float b2A = (t = dn(u1, vA)) < 0 ? per : (float)t;
+                const float m2 = b1A < b2A ? b1A : b2A;
+                mA = m2 < mA ? m2 : mA;
+                if (!four) break;
+            }
+            const float bound = mA + (float)man - 1.0f;
+            if (bound < lower) lower = bound;
+        }
+        return lower > 1.0f ? lower : 1.0f;
+    }
+    __device__ float helper_p(const ocro::Sub& s, int u0, int u1, int Ac, int B1, int B2) const {
+        if (s.n == 1 && L.sq_off != 0) {
+            float lower = (float)L.perimeter + 1.0f;
+            int vA[4];
+            const bool four = ocro::wave_any(approaches(Ac, vA));
+#pragma unroll
+            for (int k = 0; k < NA; ++k) {
+                const int v = vA[ia(four, k)];
+                const int a1 = dn(u0, v);
+                const int b1 = dsq(v, B1), b2 = dsq(v, B2);
+                const float x1 = (float)(a1 + b1 - 1), x2 = (float)(a1 + b2 - 1);
+                lower = a1 >= 0 && b1 >= 0 && x1 < lower ? x1 : lower;
+                lower = a1 >= 0 && b2 >= 0 && x2 < lower ? x2 : lower;
+                if (!four) break;
+            }
+            return lower > 1.0f ? lower : 1.0f;
+        }
+        const int Bc[1] = {(q & 1) ? B2 : B1};
+        return helper_n<1>(s, u0, u1, Ac, Bc);
+    }
+    __device__ float lower_bound_p(const Row& r, const ocro::Sub& s) const {
+        const auto br = bound_row<false>(r);
+        int u0, u1;
+        float pen;
+        bound_agents<false>(br, s, u0, u1, pen);
+        float lower = (float)L.perimeter + 1.0f;
+        if (s.kind == 1 || s.kind == 3) {
+            const int nb = s.kind == 1 ? L.ncut : L.ndeliv;
+            const int side = s.kind == 1 ? 0 : 1;
+            const uint16_t* man_t = (const uint16_t*)(T + L.man_off) + (s.kind == 1 ? 0 : L.man_stride);
+            visit_objs<false>(br, r, s.start[0], s.kind == 3, [&](int Ac) {
+                const float b = helper_static_p(s, u0, u1, Ac, nb, side, man_t);
+                if (b < lower) lower = b;
+            });
+        } else if (s.kind == 2) {
+            visit_objs<false>(br, r, s.start[0], false, [&](int Ac) {
+                visit_obj_pairs<false>(br, r, s.start[1], false, [&](int B1, int B2) {
+                    const float b = helper_p(s, u0, u1, Ac, B1, B2);
+                    if (b < lower) lower = b;
+                });
+            });
+        }
+        return grp_min<G>(lower) + pen;
+    }
+    // action_legal (the rollout row's form) with a two-agent row's single_legal split by agent
+    __device__ bool action_legal_p(const Row& r, const ocro::Sub& s, int c0, int c1, const Target& g0, const Target& g1) const {
+        if (s.kind == 0) return c0 == ocro::kNoop && (s.n < 2 || c1 == ocro::kNoop);
+        if (s.n < 2) return single_legal_flat(r, s.agent[0], c0, g0);
+        const bool mine = (q & 1) ? single_legal_flat(r, s.agent[1], c1, g1) : single_legal_flat(r, s.agent[0], c0, g0);
+        return (pair_and((int)mine) & (int)no_collision(r, s.agent[0], s.agent[1], c0, c1)) != 0;
+    }
+};
+template <int G, bool LEG>
+__global__ __launch_bounds__(kBlk) void k_roll_grp(RollArgs R, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
+                                                  const uint8_t* __restrict__ act, const uint8_t* __restrict__ alloc,
+                                                  const uint8_t* __restrict__ blob_g, uint8_t* __restrict__ out_flags,
+                                                  float* __restrict__ lb, uint64_t* __restrict__ tl) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t blob_w[];
+    __shared__ ocro::Sub subs[64];
+    const int64_t P = R.pitch;
+    const int q = (int)(threadIdx.x & (G - 1));
+    int64_t e = (blockIdx.x * (int64_t)kBlk + threadIdx.x) / G;
+    const bool live = e < R.B;
+    ocro::RowT<K> r;
+    uint16_t t = 0;
+    uint8_t fl = 0;
+    int ai = 0;
+    uint32_t acts = 0;
+    if (live) {
+        r = load_row(sin, P, e);
+        t = ((const uint16_t*)(sin + kPT * P))[e];
+        fl = sin[kPF * P + e];
+        ai = alloc[e];
+#pragma unroll
+        for (int a = 0; a < A; ++a) acts |= (uint32_t)act[a * P + e] << (8 * a);
+    }
+    {
+        const int n16 = R.blob_words >> 2;
+        for (int i = threadIdx.x; i < n16; i += kBlk) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
+        for (int i = 4 * n16 + threadIdx.x; i < R.blob_words; i += kBlk) blob_w[i] = ((const uint32_t*)blob_g)[i];
+        for (int i = threadIdx.x; i < R.nsub * 4; i += kBlk) ((uint32_t*)subs)[i] = ((const uint32_t*)R.subs)[i];
+        __syncthreads();
+    }
+    if (!live) return;  // whole groups leave together
+    float bound = 0.0f;
+    int f = OC_ROLL_BADALLOC;
+    if (ai < R.nsub) {
+        const ocro::Sub& s = subs[ai];
+        int c0 = (acts >> (8 * s.agent[0])) & 0xFFu, c1 = s.n == 2 ? (acts >> (8 * s.agent[1])) & 0xFFu : ocro::kNoop;
+        GrpOps<G> ops(R.L, (const uint8_t*)blob_w, q);
+        const ocro::RowT<K> r_in = r;
+        if (ops.level0(r, s)) {
+            r = r_in;
+            f = 8;
+        } else {
+            if (s.kind == 0) c0 = c1 = ocro::kNoop;
+            c0 = c0 > ocro::kNoop ? ocro::kNoop : c0;
+            c1 = c1 > ocro::kNoop ? ocro::kNoop : c1;
+            const auto g0 = ops.target(r, s.agent[0], c0);
+            const auto g1 = s.n == 2 ? ops.target(r, s.agent[1], c1) : g0;
+            if (LEG) f = ops.action_legal_p(r, s, c0, c1, g0, g1) ? 1 : 0;
+            else f = ops.action_legal(r, s, c0, c1, g0, g1) ? 1 : 0;
+            ops.interact(r, s.agent[0], c0, g0);
+            if (s.n == 2) ops.interact(r, s.agent[1], c1, g1);
+            const bool asserted = s.n == 2 && ops.agent_cell(r, s.agent[0]) == ops.agent_cell(r, s.agent[1]);
+            if (asserted) f |= 4;
+            else if (ops.is_goal(r, s)) f |= 2;
+            bound = ops.lower_bound_p(r, s);
+        }
+    }
+    if (q == 0) {
+        store_row(sout, P, e, r);
+        __builtin_nontemporal_store(t, (uint16_t*)(sout + kPT * P) + e);
+        __builtin_nontemporal_store(fl, sout + kPF * P + e);
+        __builtin_nontemporal_store((uint8_t)f, out_flags + e);
+        __builtin_nontemporal_store(bound, lb + e);
+    }
+    (void)tl;
+}
+
 __global__ void k_gen(ocsw::SwarLevel sw, const uint32_t* cls4g, uint8_t* s, int64_t P, int steps, uint32_t seed) {
     __shared__ uint32_t cls4[64];
     if (threadIdx.x < 64u) cls4[threadIdx.x] = cls4g[threadIdx.x];
@@ -371,6 +623,7 @@ int main(int argc, char** argv) {
     CK(hipFuncSetAttribute((const void*)k_roll<false>, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(dyn, 1)));
     CK(hipFuncSetAttribute((const void*)k_roll<true>, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(dyn, 1)));
     CK(hipFuncSetAttribute((const void*)k_roll_early, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(dyn, 1)));
+    CK(hipFuncSetAttribute((const void*)k_ablate<1>, hipFuncAttributeMaxDynamicSharedMemorySize, std::max(dyn, 1)));
     if (R.blob_words / 4 > kQ * kBlk) { printf("blob too large for the early variant\n"); return 1; }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -382,7 +635,10 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(alloc, shape == 0 ? al.data() : al_small.data(), rows, hipMemcpyHostToDevice));
         const unsigned grid = (unsigned)((rows + kBlk - 1) / kBlk);
         auto go = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlk), dyn, nullptr, R, sin, sout, act, alloc, blob_g, fl, lb, tl);
+            const void* k = (const void*)kern;
+            const unsigned g = k == (const void*)k_roll_grp<2, false> || k == (const void*)k_roll_grp<2, true> ? 2 * grid
+                               : k == (const void*)k_roll_grp<4, false> || k == (const void*)k_roll_grp<4, true> ? 4 * grid : grid;
+            hipLaunchKernelGGL(kern, dim3(g), dim3(kBlk), dyn, nullptr, R, sin, sout, act, alloc, blob_g, fl, lb, tl);
         };
         auto tm = [&](const char* name, auto kern, int reps) {
             for (int i = 0; i < 3; ++i) go(kern);
@@ -411,8 +667,21 @@ int main(int argc, char** argv) {
             R.L.sq_off = sq_off;
             tm("product (node-to-square table)", k_roll<false>, shape == 0 ? 200 : 400);
             tm("early view, batched staging", k_roll_early, shape == 0 ? 200 : 400);
+            tm("lane pairs: bound split", k_roll_grp<2, false>, shape == 0 ? 200 : 400);
+            tm("lane pairs: bound, legality split", k_roll_grp<2, true>, shape == 0 ? 200 : 400);
+            tm("lane quads: bound split", k_roll_grp<4, false>, shape == 0 ? 200 : 400);
+            tm("lane quads: bound, legality split", k_roll_grp<4, true>, shape == 0 ? 200 : 400);
             tm("stamped", k_roll<true>, shape == 0 ? 200 : 400);
         }
+        const int reps = shape == 0 ? 200 : 400;
+        tm("ablate: no bound", k_ablate<1>, reps);
+        tm("ablate: no legality", k_ablate<2>, reps);
+        tm("ablate: no interact", k_ablate<4>, reps);
+        tm("ablate: no Level-0 view", k_ablate<8>, reps);
+        tm("ablate: no goal test", k_ablate<16>, reps);
+        tm("ablate: no bound, legality", k_ablate<3>, reps);
+        tm("ablate: only the bound", k_ablate<2 | 4 | 8 | 16>, reps);
+        tm("ablate: no row work", k_ablate<32>, reps);
         if (shape == 1) {  // the planner shape's phases per configuration (100 MHz stamps)
             const int nw = (int)((rows + 63) / 64);
             std::vector<uint64_t> v((size_t)nw * (kPhases + 2));
