@@ -502,6 +502,40 @@ __global__ __launch_bounds__(kBlk) void k_roll_grp(RollArgs R, const uint8_t* __
     (void)tl;
 }
 
+
+// Floors of a launch (timing only): an empty kernel; the row's loads and the table staging with
+// no stores; the stores alone.
+template <int WHAT>
+__global__ __launch_bounds__(kBlk) void k_floor(RollArgs R, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
+                                               const uint8_t* __restrict__ act, const uint8_t* __restrict__ alloc,
+                                               const uint8_t* __restrict__ blob_g, uint8_t* __restrict__ out_flags,
+                                               float* __restrict__ lb, uint64_t* __restrict__ tl) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t blob_w[];
+    const int64_t P = R.pitch;
+    int64_t e = blockIdx.x * (int64_t)kBlk + threadIdx.x;
+    if (WHAT == 0) return;
+    ocro::RowT<K> r;
+    uint32_t x = 0;
+    if (WHAT == 1 && e < R.B) {
+        r = load_row(sin, P, e);
+        x = r.x ^ r.y ^ r.h ^ (uint32_t)r.loc[0] ^ (uint32_t)r.mask[0] ^ alloc[e] ^ act[e];
+        const int n16 = R.blob_words >> 2;
+        for (int i = threadIdx.x; i < n16; i += kBlk) ((uint4*)blob_w)[i] = ((const uint4*)blob_g)[i];
+        __syncthreads();
+        x ^= blob_w[threadIdx.x];
+        if (x == 0x12345678u) out_flags[e] = 1;  // keeps the loads
+        return;
+    }
+    if (e >= R.B) return;
+    r.x = r.y = r.h = (uint32_t)e;
+    r.loc[0] = r.mask[0] = (uint64_t)e;
+    store_row(sout, P, e, r);
+    __builtin_nontemporal_store((uint16_t)e, (uint16_t*)(sout + kPT * P) + e);
+    __builtin_nontemporal_store((uint8_t)e, sout + kPF * P + e);
+    __builtin_nontemporal_store((uint8_t)e, out_flags + e);
+    __builtin_nontemporal_store(0.0f, lb + e);
+}
+
 __global__ void k_gen(ocsw::SwarLevel sw, const uint32_t* cls4g, uint8_t* s, int64_t P, int steps, uint32_t seed) {
     __shared__ uint32_t cls4[64];
     if (threadIdx.x < 64u) cls4[threadIdx.x] = cls4g[threadIdx.x];
@@ -682,6 +716,9 @@ int main(int argc, char** argv) {
         tm("ablate: no bound, legality", k_ablate<3>, reps);
         tm("ablate: only the bound", k_ablate<2 | 4 | 8 | 16>, reps);
         tm("ablate: no row work", k_ablate<32>, reps);
+        tm("floor: empty kernel", k_floor<0>, reps);
+        tm("floor: row loads + staging, no stores", k_floor<1>, reps);
+        tm("floor: stores only", k_floor<2>, reps);
         if (shape == 1) {  // the planner shape's phases per configuration (100 MHz stamps)
             const int nw = (int)((rows + 63) / 64);
             std::vector<uint64_t> v((size_t)nw * (kPhases + 2));
