@@ -6,6 +6,7 @@ Dispatches, on bench.py's C5 rows (full-divider_salad, 4 agents, 2^18 mid-episod
 64 Salad (subtask, agents) configurations, random allocation and joint action per row; rows in
 random order, or configuration-major with OC_C5_ORDER=grouped as bench.py times them):
   oc_rollout_kernel     x4
+  oc_rollout_group_kernel x4 (the planner's launch: 4,096 rows of a second batch, configuration-major)
   oc_bounds_kernel      x4
   oc_likelihood_kernel  x3
   oc_checksum_kernel    x3   (read calibration of FETCH_SIZE on the same batch)
@@ -49,6 +50,18 @@ flags = torch.empty(eb.pitch, dtype=torch.uint8, device=dev)
 lb = torch.empty(eb.pitch, dtype=torch.float32, device=dev)
 for _ in range(4):
     eb.rollout(s, out, a, table, alloc, flags, lb)
+eb4 = OvercookedBatch("full-divider_salad", A, 4096, max_T=100, device=dev)
+s4, s42, a4 = eb4.new_state(), eb4.new_state(), eb4.new_actions()
+eb4.reset(s4)
+for t in range(37):
+    eb4.gen_actions(a4, t, 11)
+    eb4.step(s4, s42, a4)
+    s4, s42 = s42, s4
+alloc4 = torch.sort(torch.randint(0, len(table), (eb4.pitch,), dtype=torch.uint8, device=dev, generator=gen))[0].contiguous()
+eb4.gen_actions(a4, 99, 12)
+out4 = eb4.new_state()
+for _ in range(4):
+    eb4.rollout(s4, out4, a4, table, alloc4)
 blb = torch.empty((len(table), eb.pitch), dtype=torch.float32, device=dev)
 bok = torch.empty((len(table), eb.pitch), dtype=torch.uint8, device=dev)
 for _ in range(4):

@@ -34,7 +34,7 @@ import json
 import os
 import sys
 
-KERNELS = ("oc_rollout_kernel", "oc_bounds_kernel", "oc_likelihood_compact_kernel", "oc_likelihood_kernel", "oc_checksum_kernel",
+KERNELS = ("oc_rollout_kernel", "oc_rollout_group_kernel", "oc_bounds_kernel", "oc_likelihood_compact_kernel", "oc_likelihood_kernel", "oc_checksum_kernel",
            "oc_step_n_kernel", "oc_render_kernel")
 CUS, SIMDS = 256, 1024
 TOP_CLOCK_GHZ = 2.4     # MI355X peak engine clock
