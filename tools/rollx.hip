@@ -434,8 +434,8 @@ struct GrpOps : ocro::RowOps<A, K> {
         return (pair_and((int)mine) & (int)no_collision(r, s.agent[0], s.agent[1], c0, c1)) != 0;
     }
 };
-template <int G, bool LEG>
-__global__ __launch_bounds__(kBlk) void k_roll_grp(RollArgs R, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
+template <int G, bool LEG, int WPE = 1>
+__global__ __launch_bounds__(kBlk, WPE) void k_roll_grp(RollArgs R, const uint8_t* __restrict__ sin, uint8_t* __restrict__ sout,
                                                   const uint8_t* __restrict__ act, const uint8_t* __restrict__ alloc,
                                                   const uint8_t* __restrict__ blob_g, uint8_t* __restrict__ out_flags,
                                                   float* __restrict__ lb, uint64_t* __restrict__ tl) {
@@ -670,7 +670,8 @@ int main(int argc, char** argv) {
         const unsigned grid = (unsigned)((rows + kBlk - 1) / kBlk);
         auto go = [&](auto kern) {
             const void* k = (const void*)kern;
-            const unsigned g = k == (const void*)k_roll_grp<2, false> || k == (const void*)k_roll_grp<2, true> ? 2 * grid
+            const unsigned g = k == (const void*)k_roll_grp<2, false> || k == (const void*)k_roll_grp<2, true> ||
+                                       k == (const void*)k_roll_grp<2, false, 8> ? 2 * grid
                                : k == (const void*)k_roll_grp<4, false> || k == (const void*)k_roll_grp<4, true> ? 4 * grid : grid;
             hipLaunchKernelGGL(kern, dim3(g), dim3(kBlk), dyn, nullptr, R, sin, sout, act, alloc, blob_g, fl, lb, tl);
         };
@@ -705,6 +706,7 @@ int main(int argc, char** argv) {
             tm("lane pairs: bound, legality split", k_roll_grp<2, true>, shape == 0 ? 200 : 400);
             tm("lane quads: bound split", k_roll_grp<4, false>, shape == 0 ? 200 : 400);
             tm("lane quads: bound, legality split", k_roll_grp<4, true>, shape == 0 ? 200 : 400);
+            tm("lane pairs, 8 waves per SIMD", k_roll_grp<2, false, 8>, shape == 0 ? 200 : 400);
             tm("stamped", k_roll<true>, shape == 0 ? 200 : 400);
         }
         const int reps = shape == 0 ? 200 : 400;
