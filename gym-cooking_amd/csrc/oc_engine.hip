@@ -2596,11 +2596,13 @@ int oc_step_n(const oc_handle* h, const void* state_in, void* state_out, const u
     return OC_OK;
 }
 
-// Shared argument block of oc_rollout / oc_nav_likelihood: level tables + validated subtasks.
+// Shared argument block of oc_rollout / oc_nav_likelihood / oc_subtask_bounds: level tables +
+// validated subtasks.  rollout: oc_rollout's call (Level-1 configurations allowed; the
+// node-to-square table staged only for launches of one round of blocks, below).
 static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num_subtasks, int64_t B, RollArgs& R,
-                     bool level1_ok = false) {
+                     bool rollout = false) {
     for (int i = 0; i < num_subtasks && subtasks != nullptr; ++i)
-        if (subtasks[i].level != OC_LEVEL0 && !level1_ok)
+        if (subtasks[i].level != OC_LEVEL0 && !rollout)
             return fail(OC_EINVAL, "subtask %d: only oc_rollout takes OC_LEVEL1", i);
     if (num_subtasks < 1 || num_subtasks > OC_MAX_SUBTASKS) return fail(OC_EINVAL, "num_subtasks %d", num_subtasks);
     if (h->roll.nnodes < 0)
@@ -2610,12 +2612,14 @@ static int roll_args(const oc_handle* h, const oc_subtask* subtasks, int32_t num
     R.L = h->roll;
     R.nsub = num_subtasks;
     R.blob_words = h->roll.lds_bytes / 4;  // staged in LDS: the whole blob, or the tables before the distances
-    if (R.L.sq_off != 0 && B > (int64_t)h->cus * kRollBlock) {
+    if (R.L.sq_off != 0 && rollout && B > (int64_t)h->cus * kRollBlock) {
         // The node-to-square table (the blob's tail) shortens the one-agent Merge bound from ~3.8
-        // to 1.1-2.0 us of a wave; that pays where a launch is one round of blocks (the planner's
-        // latency shape: 9.03 -> 8.87 us at 4096 rows) and not past it, where every block stages
-        // 40% more table for it (11.16-11.34 -> 11.35-11.51 us at 2^18): tools/rollx.hip,
-        // profiles/r06/pass_i.  Larger launches search B's approach nodes as before.
+        // to 1.1-2.0 us of a wave.  A rollout launch of one round of blocks (the planner's latency
+        // shape) gains (9.03 -> 8.87 us at 4096 rows); past that every rollout block stages 40%
+        // more table for one row per lane (11.16-11.34 -> 11.35-11.51 us at 2^18: tools/rollx.hip,
+        // profiles/r06/pass_i), so larger rollouts search B's approach nodes as before.  The bounds
+        // kernel (many configurations per staged table) gains at every size, 96-97 -> 85 us at C5,
+        // and the likelihood kernels are unchanged (profiles/r06/pass_w).
         R.blob_words = R.L.sq_off / 4;
         R.L.sq_off = 0;
     }
