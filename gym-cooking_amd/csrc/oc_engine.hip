@@ -1249,6 +1249,7 @@ __global__ __launch_bounds__(kBlock) void oc_bounds_kernel(RollArgs R, const uin
     for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < R.B; e += (int64_t)gridDim.x * kBlock) {
         const ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
         ocro::RowOps<A, K, W, false, GD> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+        ops.PT = R.L.pair_off != 0 ? (const uint32_t*)(blob_g + R.L.pair_off) : nullptr;  // the agent-pair table (device memory)
         const auto br = ops.template bound_row<true>(r);  // the row's agent nodes, slot sets: once for its configurations
         for (int i = i0; i < i1; ++i) {
             float v;

@@ -57,6 +57,7 @@ constexpr int kMaxCellsWide = 1024;  // wide levels (more than 255 cells): u16 c
 // round 5 refused such a graph)
 constexpr int kMaxNodes = 360;  // 360^2 + the other tables + the compacted likelihood's 18 KB < 160 KB
 constexpr int kMaxSqBytes = 8192;  // the node-to-square table is built when nnodes x cells fits this
+constexpr size_t kMaxPairBytes = (size_t)4 << 20;  // the agent-pair table: nnodes^2 x cells x 4 bytes
 constexpr int kMaxNodesNarrow = 5 * kMaxCells;    // narrow levels: every node 255 cells can make
 constexpr int kMaxNodesWide = 5 * kMaxCellsWide;  // wide levels: the distances stay in device memory
 constexpr uint8_t kNone = 0xFF;
@@ -83,6 +84,12 @@ constexpr int kDX[5] = {0, 0, -1, 1, 0}, kDY[5] = {1, -1, 0, 0, 0};  // World.NA
 //              (its own node for a Floor square), 0xFF = none reachable; only on a small narrow
 //              level whose blob stays in LDS (kMaxSqBytes), where the single-agent Merge bound
 //              reads it once per (A approach, B square) instead of walking B's approaches
+//   pair_off   u32 [nnodes][nnodes][cells] after everything the kernels stage (device memory
+//              only, never in LDS): for agent nodes (u0, u1) and a square, the two-agent bound's
+//              per-type minima over the square's approach nodes (byte 0: u0 strictly nearer, byte
+//              1: u1 strictly nearer, byte 2: a tie; 0xFF = no such approach), an unreachable
+//              distance counted as the perimeter as the walk does; only on a narrow level with LDS
+//              distances, a perimeter below 255 and at most kMaxPairBytes of entries (round 6)
 // Only the tile table's size is fixed (256 entries on a narrow level); the others follow the
 // level's cell count (round 6; before, every per-cell table had 256 entries on a narrow level).
 
@@ -106,6 +113,7 @@ struct RollLevel {  // scalars (kernel argument); the tables are in the blob
     int32_t sq_off;      // blob offset of the node-to-square table ([nnodes][cells] u8, the distance
                          // from a node to the nearest approach node of a square), 0 = none (round 6)
     int32_t sq_cells;    // its row length (the level's cell count)
+    int32_t pair_off;    // blob offset of the agent-pair table (device memory only), 0 = none
 };
 
 // A wide level's reset template (oc_reset_wide_kernel).
@@ -220,6 +228,7 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
     L.dist16 = 0;
     L.sq_off = 0;
     L.sq_cells = 0;
+    L.pair_off = 0;
     const int cells = W * H;
     L.wide = cells > kMaxCells ? 1 : 0;
     if (cells > kMaxCellsWide) return -1;
@@ -396,6 +405,37 @@ inline int build_roll_level(RollLevel& L, std::vector<uint8_t>& blob_v, int W, i
         L.blob_bytes = (int32_t)((L.sq_off + (size_t)n * cells + 3) & ~(size_t)3);
     }
     L.lds_bytes = L.dist_global ? L.dist_off : L.blob_bytes;
+    if (!L.dist_global && L.perimeter < 255 && (size_t)n * n * cells * 4 <= kMaxPairBytes) {
+        // the agent-pair table (device memory): side()'s per-type minima of helper_n's two-agent
+        // bound, for every (u0, u1, square), over the approach set approaches() walks on the
+        // static graph (a Floor square's own node, else its four approach nodes)
+        L.pair_off = L.blob_bytes;
+        blob_v.resize((size_t)L.pair_off + (size_t)n * n * cells * 4, 0);
+        blob = blob_v.data();
+        node = (uint16_t*)(blob + L.node_off);
+        uint32_t* pt = (uint32_t*)(blob + L.pair_off);
+        const uint32_t per = (uint32_t)L.perimeter;
+        for (int c = 0; c < cells; ++c) {
+            int vs[4], nv = 0;
+            if (node[c * 5 + 4] != kNoNode) vs[nv++] = node[c * 5 + 4];
+            else
+                for (int q = 0; q < 4; ++q) vs[nv++] = node[c * 5 + q];
+            for (int u0 = 0; u0 < n; ++u0)
+                for (int u1 = 0; u1 < n; ++u1) {
+                    uint32_t M[3] = {0xFFu, 0xFFu, 0xFFu};
+                    for (int i = 0; i < nv; ++i) {
+                        const int v = vs[i];
+                        const uint32_t d1 = v == kNoNode ? 0xFFFFu : d16[(size_t)u0 * n + v];
+                        const uint32_t d2 = v == kNoNode ? 0xFFFFu : d16[(size_t)u1 * n + v];
+                        const uint32_t b1 = d1 == 0xFFFFu ? per : d1, b2 = d2 == 0xFFFFu ? per : d2;
+                        const uint32_t m = b1 < b2 ? b1 : b2, t = b1 < b2 ? 0 : (b2 < b1 ? 1 : 2);
+                        if (m < M[t]) M[t] = m;
+                    }
+                    pt[((size_t)u0 * n + u1) * cells + c] = M[0] | M[1] << 8 | M[2] << 16;
+                }
+        }
+        L.blob_bytes = (int32_t)(L.pair_off + (size_t)n * n * cells * 4);
+    }
     blob_v.resize((size_t)L.blob_bytes, 0);
     return n;
 }
@@ -418,6 +458,8 @@ struct RowOps {
     const uint8_t* D;       // its distance table: in T (narrow), in device memory (wide)
     AcT ac = kNoAc;         // AgentCounter cells of this row's Level-0 view, one per byte (narrow) or
                             // u16 field (wide), all ones = none
+    const uint32_t* PT = nullptr;  // the agent-pair table (device memory; L.pair_off), or none:
+                                   // the kernel that reads it sets it (round 6)
     uint32_t active = 0;    // bit a: agent a is a subtask agent
     uint32_t blockers = 0;  // bit a: agent a's cell may not be moved into (get_single_actions)
 
@@ -721,6 +763,12 @@ struct RowOps {
     OC_RH float helper_n(const Sub& s, int u0, int u1, int Ac, const int (&Bc)[NB]) const {
         const float per = (float)L.perimeter;
         float lower = per + 1.0f;
+        if (PT != nullptr && s.n == 2) {  // wave-uniform: the per-type minima from the agent-pair table
+            bool ok = u0 != kNoNode && u1 != kNoNode && !is_ac(Ac);
+#pragma unroll
+            for (int j = 0; j < NB; ++j) ok = ok && !is_ac(Bc[j]);
+            if (!wave_any(!ok)) return pair_bound(u0, u1, Ac, Bc);
+        }
         int vA[4], vB[NB][4];
         const bool Acoll = approaches(Ac, vA);
         if (L.sq_off != 0 && s.n == 1) {  // wave-uniform: min over B's approaches from the table
@@ -782,22 +830,54 @@ struct RowOps {
                 M[2] = b1 == b2 && m < M[2] ? m : M[2];
             }
         };
-        auto mx = [](int x, int y) OC_RL { return x > y ? x : y; };
-        auto mn = [](int x, int y) OC_RL { return x < y ? x : y; };
         int MA[3] = {kInf, kInf, kInf};
         side(vA, nA, MA);
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
             int MB[3] = {kInf, kInf, kInf};
             side(vB[j], nB, MB);
-            const uint32_t pb = xy(Bc[j]);
-            const int dx = (int)(pa & 0xFFu) - (int)(pb & 0xFFu), dy = (int)(pa >> 8) - (int)(pb >> 8);
-            const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
-            const int single = mn(mx(MA[0], MB[1]), mx(MA[1], MB[0]));
-            const int dbl = mn(mn(mx(MA[0], MB[0]), mx(MA[1], MB[1])),
-                               mn(mx(MA[2], mn(mn(MB[0], MB[1]), MB[2])), mx(mn(mn(MA[0], MA[1]), MA[2]), MB[2])));
-            const int best = mn(single, 2 * dbl);
-            const float bound = (float)best + (man - 1.0f) * 0.5f;
+            const float bound = type_bound(MA, MB, pa, xy(Bc[j]));
+            lower = bound < lower ? bound : lower;
+        }
+        return lower > 1.0f ? lower : 1.0f;
+    }
+    // The two-agent (A, B) pair's bound from the per-type minima of its squares (helper_n above)
+    static constexpr int kInfM = 0x3FFFFFFF;
+    OC_RH static float type_bound(const int (&MA)[3], const int (&MB)[3], uint32_t pa, uint32_t pb) {
+        auto mx = [](int x, int y) OC_RL { return x > y ? x : y; };
+        auto mn = [](int x, int y) OC_RL { return x < y ? x : y; };
+        const int dx = (int)(pa & 0xFFu) - (int)(pb & 0xFFu), dy = (int)(pa >> 8) - (int)(pb >> 8);
+        const float man = (float)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
+        const int single = mn(mx(MA[0], MB[1]), mx(MA[1], MB[0]));
+        const int dbl = mn(mn(mx(MA[0], MB[0]), mx(MA[1], MB[1])),
+                           mn(mx(MA[2], mn(mn(MB[0], MB[1]), MB[2])), mx(mn(mn(MA[0], MA[1]), MA[2]), MB[2])));
+        const int best = mn(single, 2 * dbl);
+        return (float)best + (man - 1.0f) * 0.5f;
+    }
+    // helper_n's two-agent form with the squares' per-type minima read from the agent-pair table
+    // (one u32 per square instead of the walk's 8 distance reads per square; round 6)
+    template <int NB>
+    OC_RH float pair_bound(int u0, int u1, int Ac, const int (&Bc)[NB]) const {
+        const uint32_t* row = PT + (uint32_t)(u0 * L.nnodes + u1) * (uint32_t)(L.W * L.H);
+        auto unpack = [](uint32_t e, int (&M)[3]) OC_RL {
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int b = (int)((e >> (8 * t)) & 0xFFu);
+                M[t] = b == 0xFF ? kInfM : b;
+            }
+        };
+        uint32_t eb[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) eb[j] = row[Bc[j]];
+        int MA[3];
+        unpack(row[Ac], MA);
+        const uint32_t pa = xy(Ac);
+        float lower = (float)L.perimeter + 1.0f;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            int MB[3];
+            unpack(eb[j], MB);
+            const float bound = type_bound(MA, MB, pa, xy(Bc[j]));
             lower = bound < lower ? bound : lower;
         }
         return lower > 1.0f ? lower : 1.0f;

@@ -53,6 +53,7 @@ static void run(const oc_level_desc* lv, const uint8_t* sin, uint8_t* sout, cons
                         {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
             const int c0 = act[s.agent[0] * P + e], c1 = s.n == 2 ? act[s.agent[1] * P + e] : ocro::kNoop;
             ocro::RowOps<A, K, W, false, true> ops(L, blob);
+            ops.PT = L.pair_off ? (const uint32_t*)(blob + L.pair_off) : nullptr;  // the agent-pair table
             f = ops.run(r, s, c0, c1, bound);
         }
         for (int a = 0; a < A; ++a) {
@@ -93,6 +94,7 @@ static void lik(const oc_level_desc* lv, const uint8_t* sin, const uint8_t* take
             ocro::Sub s{o.kind, o.num_agents, {o.agent[0], (uint8_t)(o.num_agents == 2 ? o.agent[1] : o.agent[0])},
                         {o.start_mask[0], o.start_mask[1]}, o.goal_mask, o.goal_count, o.level, 0};
             ocro::RowOps<A, K, W, true, true> ops(L, blob);  // the likelihood kernels' lean flavour
+            ops.PT = L.pair_off ? (const uint32_t*)(blob + L.pair_off) : nullptr;
             f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
         }
         out[e] = f == OC_LIK_OK ? v : 0.0;
@@ -141,6 +143,7 @@ static void bounds(const oc_level_desc* lv, const uint8_t* sin, const oc_subtask
     for (int64_t e = 0; e < B; ++e) {
         const ocro::RowT<K, W> r = load<A, K, W>(sin, P, e);
         ocro::RowOps<A, K, W, false, true> ops(L, blob);
+            ops.PT = L.pair_off ? (const uint32_t*)(blob + L.pair_off) : nullptr;  // the agent-pair table
         const auto br = ops.template bound_row<true>(r);  // as the kernel: once per row
         for (int i = 0; i < nsub; ++i) {
             const oc_subtask& o = subs[i];
