@@ -629,6 +629,12 @@ __device__ __forceinline__ void store_row(uint8_t* __restrict__ sout, int64_t P,
 #ifndef OC_ROLL_BLOCK
 #define OC_ROLL_BLOCK 256
 #endif
+#ifndef OC_PT_LIK
+#define OC_PT_LIK 0
+#endif
+#ifndef OC_PT_ROLL
+#define OC_PT_ROLL 0
+#endif
 #ifndef OC_ROLL_GROUP
 #define OC_ROLL_GROUP 4
 #endif
@@ -690,6 +696,7 @@ __global__ __launch_bounds__(kRollBlock) void oc_rollout_kernel(RollArgs R, cons
             const ocro::Sub& s = subs[ai];
             const int c0 = (in.acts >> (8 * s.agent[0])) & 0xFFu, c1 = s.n == 2 ? (in.acts >> (8 * s.agent[1])) & 0xFFu : ocro::kNoop;
             ocro::RowOps<A, K, W, false, GD> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+            if (OC_PT_ROLL) ops.PT = R.L.pair_off != 0 ? (const uint32_t*)(blob_g + R.L.pair_off) : nullptr;
             f = ops.run(r, s, c0, c1, bound);
         }
         store_row<A, K, W, true>(sout, P, e, r);
@@ -875,6 +882,7 @@ __global__ __launch_bounds__(kRollBlock) void oc_rollout_group_kernel(RollArgs R
         const ocro::Sub& s = subs[ai];
         const int c0 = (acts >> (8 * s.agent[0])) & 0xFFu, c1 = s.n == 2 ? (acts >> (8 * s.agent[1])) & 0xFFu : ocro::kNoop;
         GroupRowOps<G, A, K> ops(R.L, (const uint8_t*)blob_w, q);
+        if (OC_PT_ROLL) ops.PT = R.L.pair_off != 0 ? (const uint32_t*)(blob_g + R.L.pair_off) : nullptr;
         f = ops.run(r, s, c0, c1, bound);
     }
     if (q == 0) {
@@ -929,6 +937,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_kernel(RollArgs R, const
 #pragma unroll
             for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
             ocro::RowOps<A, K, W, true, GD> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);  // distances: LDS (narrow), device memory (wide)
+            if (OC_PT_LIK) ops.PT = R.L.pair_off != 0 ? (const uint32_t*)(blob_g + R.L.pair_off) : nullptr;
             if (s.kind == 0) {
                 f = 0;
                 if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
@@ -1110,6 +1119,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
 #pragma unroll
                     for (int a = 0; a < A; ++a) taken |= (uint32_t)taken_p[a * P + e] << (8 * a);
                     ocro::RowOps<A, K, W, true, GD> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
+                    if (OC_PT_LIK) ops.PT = R.L.pair_off != 0 ? (const uint32_t*)(blob_g + R.L.pair_off) : nullptr;
                     if (s.kind == 0) {
                         f = 0;
                         if (lane == 0) f = ops.likelihood(r, s, taken, self_agent, beta, nap, v);
@@ -1168,6 +1178,7 @@ __global__ __launch_bounds__(kBlock) void oc_likelihood_compact_kernel(RollArgs 
                 const ocro::Sub& s = subs[ai];
                 ocro::RowT<K, W> r = load_row<A, K, W>(sin, P, e);
                 ocro::RowOps<A, K, W, true, GD> ops(R.L, blob, GD ? blob_g + R.L.dist_off : blob + R.L.dist_off);
+                if (OC_PT_LIK) ops.PT = R.L.pair_off != 0 ? (const uint32_t*)(blob_g + R.L.pair_off) : nullptr;
                 ops.level0(r, s);
                 const bool joint = s.n == 2;
                 const int a0 = joint ? k / 5 : k, c1 = joint ? k % 5 : ocro::kNoop;
