@@ -629,11 +629,15 @@ __device__ __forceinline__ void store_row(uint8_t* __restrict__ sout, int64_t P,
 #ifndef OC_ROLL_BLOCK
 #define OC_ROLL_BLOCK 256
 #endif
+// The agent-pair table (oc_rollout.h pair_off: the two-agent bound's per-type minima, device
+// memory) in the rollout kernels: 2^18 rows 11.35-11.40 -> 10.78-10.83 us, 4,096 rows unchanged;
+// in the likelihood kernels 188-192 -> 193-195 us, so off there (profiles/r06/pass_z); the bounds
+// kernel always reads it (85 -> 70 us, pass_y).  Every output byte identical.
 #ifndef OC_PT_LIK
 #define OC_PT_LIK 0
 #endif
 #ifndef OC_PT_ROLL
-#define OC_PT_ROLL 0
+#define OC_PT_ROLL 1
 #endif
 #ifndef OC_ROLL_GROUP
 #define OC_ROLL_GROUP 4
